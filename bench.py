@@ -1,0 +1,162 @@
+#!/usr/bin/env python3
+"""Benchmark: env-steps/s of the batched cattle-herding env on N MI355X (BASELINE.json metric).
+
+A "step" = one env.step() of every env on the GPU (reference: BaseAviary.step,
+sb3_envs/BaseAviary.py:335-465) = one launch of the fused HIP step kernel over device-resident
+state, with synthetic Philox random actions drawn in the kernel and SB3-style auto-reset.
+Workload (default, BASELINE configs[3] per GPU): 4096 envs/GPU x (4 drones, 16 cattle), CTDE
+(12, 86) observations.  Multi-GPU: one process per GPU (torchrun), envs sharded by env_id_offset,
+no per-step exchange; one RCCL all-reduce of the metric vector closes the rollout.
+
+Prints ONE JSON line (rank 0).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "rl-cattle-herding_amd"))
+
+WORKLOADS = {
+    # name: (mode, envs/GPU, drones, cattle, description)
+    "c4": ("ctde", 4096, 4, 16, "BASELINE configs[3]: 4096 envs/GPU x (4 drones, 16 cattle), CTDE obs (12,86), "
+                                "random-action rollout with auto-reset"),
+    "c2": ("ctde", 1024, 2, 8, "BASELINE configs[1]: 1024 envs x (2 drones, 8 cattle), CTDE, random actions"),
+    "c3": ("ctde", 4096, 2, 8, "BASELINE configs[2] env side: 4096 envs x (2 drones, 8 cattle), CTDE"),
+    "c5": ("marl", 4096, 4, 32, "BASELINE configs[4]: 4096 envs x (4 drones, 32 cattle), MARL per-agent obs (4,86)"),
+}
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def algorithmic_bytes(mode, n, m, rows, real_bytes):
+    """HBM bytes one env-step must move with this SoA layout (DESIGN.md "Roofline")."""
+    drone = 22 * real_bytes * 2 * n                   # state read + write
+    actions = 16 * n                                  # drawn actions written to actions_out
+    cattle = (4 * real_bytes + 2 * real_bytes + real_bytes) * m   # read pos+vel, write pos, vel every 2nd step
+    env = 2 * (9 * 4 + 2 * real_bytes)                # env scalars read + write
+    metrics = 2 * 7 * 8                               # per-env metric accumulators read + write
+    obs = rows * 86 * 4
+    k = 1 if mode == "ctde" else n
+    flags = 4 * k + 2 * k + n + 1                     # reward, terminated, truncated, agent_active, reset flag
+    return drone + actions + cattle + env + metrics + obs + flags
+
+
+def cpu_baseline(mode, n, m, seconds=12.0):
+    """The CPU oracle (scalar fp64 C port, OpenMP one env per thread) on a bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle as O
+    from cattleherd._lib import spawn_table
+    table = spawn_table(m)
+    threads = max(1, min(16, os.cpu_count() or 1))
+    E = threads * 4
+    secs, steps = O.batch_rollout(0 if mode == "ctde" else 1, n, m, table, E=E, T=20, threads=threads)
+    T = max(20, int(seconds / max(secs, 1e-6) * 20))
+    secs, steps = O.batch_rollout(0 if mode == "ctde" else 1, n, m, table, E=E, T=T, threads=threads)
+    del np
+    return {"value": steps / secs, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{E} envs x {T} random-action steps ({steps} env-steps, {secs:.1f} s) of the fp64 C oracle, "
+                      f"{threads} OpenMP threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
+    ap.add_argument("--envs", type=int, default=None, help="override envs per GPU")
+    ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    from cattleherd.env import HerdBatch
+
+    mode, E, n, m, desc = WORKLOADS[args.workload]
+    if args.envs:
+        E = args.envs
+    b = HerdBatch(E, n, m, mode=mode, precision=args.precision, env_id_offset=rank * E)
+    b.reset()
+    stream = torch.cuda.current_stream()
+    for _ in range(args.warmup):
+        b.step(random_actions=True, autoreset=True, terminal_obs=False)
+    b.metrics(reset=True)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        b.step(random_actions=True, autoreset=True, terminal_obs=False)
+    met = torch.tensor(b.metrics(reset=True), dtype=torch.float64, device=b.device)  # end-of-rollout metrics
+    if world > 1:
+        dist.all_reduce(met)   # RCCL over xGMI: the only collective of the rollout
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    dt_t = torch.tensor([dt], dtype=torch.float64, device=b.device)
+    if world > 1:
+        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+    dt = float(dt_t.item())
+
+    # live per-launch kernel timing with HIP events on the launch stream (roofline)
+    nk = min(200, args.steps)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nk)]
+    for s_ev, e_ev in evs:
+        s_ev.record(stream)
+        b.step(random_actions=True, autoreset=True, terminal_obs=False)
+        e_ev.record(stream)
+    torch.cuda.synchronize()
+    kern_us = sum(s.elapsed_time(e) for s, e in evs) / nk * 1000.0
+    rb = 8 if args.precision == "f64" else 4
+    bytes_step = algorithmic_bytes(mode, n, m, b.obs_rows, rb)
+    achieved = bytes_step * E / (kern_us * 1e-6) / 1e9
+
+    out = None
+    if rank == 0:
+        value = E * world * args.steps / dt
+        mv = met.cpu().numpy()
+        out = {
+            "metric": "env-steps/sec (agent-steps/sec) at 4096 envs/GPU, 1/2/4/8 MI355X",
+            "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1000.0, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": args.precision, "agent_steps_per_s": value * n,
+            "data": "synthetic: Philox4x32 random VEL actions in-kernel, spawn table from config/cattle_positions.yaml",
+            "config": {"workload": desc, "envs_per_gpu": E, "num_drones": n, "num_cattle": m, "mode": mode,
+                       "parallelism": f"env-sharded x{world} (no per-step collective)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "ch::k_env<R,TEAM,false> (fused step)", "kernel_us": kern_us,
+                         "bytes_per_env_step": bytes_step},
+            "rollout_metrics": {"episodes": mv[1], "mean_return": (mv[2] / mv[1]) if mv[1] else None,
+                                "nan_rewards": mv[6], "terminated": mv[4], "truncated": mv[5]},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(mode, n, m, args.cpu_seconds)
+        elif world == 1:
+            out["cpu_baseline"] = None
+    b.close()
+    if world > 1:
+        dist.destroy_process_group()
+    if out is not None:
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,154 @@
+/*
+ * cattleherd.h — C ABI of the MI355X-native batched cattle-herding environment (libcattleherd.so).
+ *
+ * The reference (BenCooper305/RL-Cattle-Herding, gym_pybullet_drones/) has no native FFI: its
+ * hot path is a Python gym.Env whose step() drives PyBullet.  This ABI replaces that env object
+ * for a whole batch of environments at once; each entry point names the reference interface it
+ * stands in for (paths relative to gym_pybullet_drones/).  INTEGRATION.md shows the ctypes
+ * binding and the Gymnasium / SB3 / RLlib adapters layered on top.
+ *
+ * Conventions
+ *   - Every call returns an int status: CH_OK (0) or a negative CH_ERR_*; ch_last_error() gives the
+ *     message.  No exception crosses the ABI.  NaN/Inf in the simulation propagate exactly like the
+ *     reference (e.g. the CTDE reward is NaN for 2 drones — see DESIGN.md "Quirks").
+ *   - Buffers passed to ch_reset/ch_step are DEVICE pointers owned by the caller (e.g. torch
+ *     tensors' data_ptr()); state is owned by the handle and lives in HBM.
+ *   - One handle <-> one device.  Work is enqueued on the given hipStream_t (NULL = default stream)
+ *     and is asynchronous until the caller synchronises.  One host thread per handle.
+ *   - Layouts (E = n_envs, N = num_drones from the config, R = obs rows, K = reward columns):
+ *       actions       float32 [E][N][4]          (VEL action, BaseRLAviary.py:185-222)
+ *       obs           float32 [E][R][86]         R = 12 (CTDE, BaseRLAviary.py:272-342) or N (MARL,
+ *                                                BaseMARLAviary.py:253-303)
+ *       reward        float32 [E][K]             K = 1 (CTDE) or N (MARL, per agent)
+ *       terminated    uint8   [E][K]
+ *       truncated     uint8   [E][K]
+ *       agent_active  uint8   [E][N]             MARL wrapper's live agents (marl_wrapper.py:112-113)
+ */
+#ifndef CATTLEHERD_H
+#define CATTLEHERD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CH_ABI_VERSION 1
+
+enum {
+    CH_OK = 0,
+    CH_ERR_INVALID = -1,     /* bad argument / configuration (reference: print+exit / ValueError) */
+    CH_ERR_DEVICE = -2,      /* HIP runtime error */
+    CH_ERR_NOMEM = -3,
+    CH_ERR_UNSUPPORTED = -4  /* configuration the reference itself cannot run (e.g. 1 drone) */
+};
+
+enum { CH_MODE_CTDE = 0, CH_MODE_MARL = 1 };
+enum { CH_PREC_F64 = 0, CH_PREC_F32 = 1 };
+
+/* Flags for ch_step_io.flags */
+#define CH_STEP_AUTORESET      0x1u  /* reset finished envs in the same launch (SB3 VecEnv semantics) */
+#define CH_STEP_RANDOM_ACTIONS 0x2u  /* draw U[-1,1) actions on device (Philox4x32-10, key = seed,
+                                        counter = (step, drone, env)); written to actions_out if set */
+
+/* Environment configuration.  Mirrors the constructor of CattleAviary (sb3_envs/CattleAviary.py:14-28)
+ * / MARLCattleAviary (rllib_envs/MARLCattleAviary.py:14-28) plus the knobs the reference hard-codes. */
+typedef struct ch_config {
+    int32_t abi_version;      /* = CH_ABI_VERSION */
+    int32_t mode;             /* CH_MODE_CTDE (sb3_envs) or CH_MODE_MARL (rllib_envs) */
+    int32_t num_drones;       /* constructor num_drones: action rows (BaseRLAviary.py:80), <= 12 */
+    int32_t num_cattle;       /* num_cattle, <= 64 (reference spawns at most 16, BaseAviary.py:611) */
+    int32_t min_drones;       /* NUM_DRONES drawn per reset in [min, max] (BaseAviary.py:307);      */
+    int32_t max_drones;       /*   -1 = num_drones (pinned)                                          */
+    int32_t curriculum_level; /* starting level; -1 = reference default (CTDE 7, MARL 0)             */
+    int32_t ctrl_freq;        /* 60 (CattleAviary.py:23) */
+    int32_t pyb_freq;         /* 240 (CattleAviary.py:22) */
+    int32_t compat;           /* 1 = reproduce reference quirks bit-for-bit (DESIGN.md "Quirks") */
+    int32_t precision;        /* CH_PREC_F64 (reference arithmetic) or CH_PREC_F32 */
+    int32_t torque_world;     /* 1 = applyExternalTorque(LINK_FRAME) acts in world frame (default) */
+    int32_t gyro;             /* 1 = gyroscopic term (btMultiBody default) */
+    double damping;           /* btMultiBody default linear/angular damping 0.04 */
+    uint64_t seed;            /* Philox key for resets and random actions */
+    int64_t env_id_offset;    /* global index of env 0 (multi-GPU sharding) */
+    const double* spawn_table;/* host [spawn_scenarios][spawn_cows][2]; NULL = built-in table
+                                 (config/cattle_positions.yaml, 100 x 16; extended for > 16 cows) */
+    int32_t spawn_scenarios;
+    int32_t spawn_cows;
+} ch_config;
+
+typedef struct ch_handle ch_handle;
+
+/* Fill *cfg with the reference defaults for `mode` (CattleAviary / MARLCattleAviary constructors). */
+int ch_default_config(ch_config* cfg, int32_t mode, int32_t num_drones, int32_t num_cattle);
+
+/* Replaces: CattleAviary.__init__ (sb3_envs/CattleAviary.py:14-105) — one env — with n_envs envs on
+ * `device`.  Allocates the SoA state in HBM and uploads the spawn table. */
+int ch_create(const ch_config* cfg, int64_t n_envs, int32_t device, ch_handle** out);
+
+/* Replaces: BaseAviary.close (sb3_envs/BaseAviary.py:498-503). */
+int ch_destroy(ch_handle* h);
+
+/* Message of the last failing call on `h` (or of the last failing ch_create when h == NULL). */
+const char* ch_last_error(const ch_handle* h);
+
+/* Shapes: obs rows R and reward columns K. */
+int ch_shape(const ch_handle* h, int64_t* n_envs, int32_t* obs_rows, int32_t* obs_cols, int32_t* reward_cols);
+
+/* Replaces: BaseAviary.reset (sb3_envs/BaseAviary.py:280-331; rllib_envs/BaseAviary.py:280-318).
+ * Resets the envs whose mask byte is non-zero (mask = NULL: all) and writes their initial
+ * observation into obs (device, [E][R][86]); other envs' obs rows are left untouched. */
+int ch_reset(ch_handle* h, const uint8_t* mask_dev, float* obs_dev, void* stream);
+
+typedef struct ch_step_io {
+    const float* actions;      /* device [E][N][4]; ignored with CH_STEP_RANDOM_ACTIONS */
+    float* actions_out;        /* optional: where device-drawn random actions are stored */
+    float* obs;                /* device [E][R][86] (required) */
+    float* reward;             /* device [E][K] (required) */
+    uint8_t* terminated;       /* device [E][K] (required) */
+    uint8_t* truncated;        /* device [E][K] (required) */
+    float* terminal_obs;       /* optional device [E][R][86]: pre-reset obs of envs that auto-reset */
+    uint8_t* agent_active;     /* optional device [E][N]: MARL live-agent mask after this step */
+    uint8_t* reset_happened;   /* optional device [E]: 1 where the env auto-reset in this call */
+    uint32_t flags;            /* CH_STEP_* */
+    uint32_t _pad;
+} ch_step_io;
+
+/* Replaces: BaseAviary.step (sb3_envs/BaseAviary.py:335-465) for every env at once — VEL action →
+ * DSLPIDControl → motor model → pyb_freq/ctrl_freq physics substeps → flocking every 2nd step →
+ * observation → reward / terminated / truncated; with CH_STEP_AUTORESET, SB3 VecEnv auto-reset.
+ * MARL mode additionally applies RLlibMultiAgentWrapper.step's per-agent recomputation
+ * (rllib_envs/marl_wrapper.py:77-119). */
+int ch_step(ch_handle* h, const ch_step_io* io, void* stream);
+
+/* Full SoA state, for checkpoint/resume and parity state-injection.  Layout of the two host
+ * buffers (counts from ch_state_size):
+ *   doubles: drone[22][E][N] (px py pz qx qy qz qw vx vy vz wx wy wz pid_last_rpy[3]
+ *            pid_int_pos[3] pid_int_rpy[3]), cattle[4][E][M] (x y vx vy), env[2][E] (prev_cent clock)
+ *   int32:   env[10][E] (n, step_counter, step_counter_A, has_prev, level, tally, spawn_index,
+ *            active_mask, episode, reserved) */
+int ch_state_size(const ch_handle* h, int64_t* n_doubles, int64_t* n_ints);
+int ch_get_state(ch_handle* h, double* host_doubles, int32_t* host_ints, void* stream);
+int ch_set_state(ch_handle* h, const double* host_doubles, const int32_t* host_ints, void* stream);
+
+/* End-of-rollout metrics (host double[CH_METRIC_COUNT]) accumulated on device since the last call
+ * with reset_after != 0: see CH_METRIC_* below.  Rank-local; bench.py all-reduces them over RCCL. */
+enum {
+    CH_METRIC_STEPS = 0, CH_METRIC_EPISODES, CH_METRIC_RETURN_SUM, CH_METRIC_LENGTH_SUM,
+    CH_METRIC_TERMINATED, CH_METRIC_TRUNCATED, CH_METRIC_NAN_REWARDS, CH_METRIC_EFFECTIVENESS_SUM,
+    CH_METRIC_COUNT
+};
+int ch_metrics(ch_handle* h, double* host_out, int32_t reset_after, void* stream);
+
+/* Number of built-in spawn scenarios / cows, and a copy of the table (host double[S][C][2]):
+ * config/cattle_positions.yaml, 100 scenarios x 16 cows (BaseAviary.py:88-94). */
+int ch_builtin_spawn_table(double* out, int32_t* scenarios, int32_t* cows);
+
+/* The table ch_create uses when cfg->spawn_table is NULL: the built-in 16 cows per scenario, extended
+ * deterministically for cows > 16 (out: host double[100][max(cows,16)][2]; out may be NULL to query). */
+int ch_spawn_table(int32_t cows, double* out, int32_t* scenarios, int32_t* out_cows);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CATTLEHERD_H */

@@ -1,0 +1,104 @@
+"""ctypes binding of libcattleherd.so (C ABI in include/cattleherd.h).
+
+The product path has no CPU fallback: if the HIP library is missing or no device is visible,
+``lib()`` / ``HerdBatch`` raise.
+"""
+import ctypes
+import os
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "libcattleherd.so")
+
+CH_OK, CH_ERR_INVALID, CH_ERR_DEVICE, CH_ERR_NOMEM, CH_ERR_UNSUPPORTED = 0, -1, -2, -3, -4
+CH_MODE_CTDE, CH_MODE_MARL = 0, 1
+CH_PREC_F64, CH_PREC_F32 = 0, 1
+CH_STEP_AUTORESET, CH_STEP_RANDOM_ACTIONS = 0x1, 0x2
+METRIC_NAMES = ("steps", "episodes", "return_sum", "length_sum", "terminated", "truncated", "nan_rewards",
+                "effectiveness_sum")
+ABI_VERSION = 1
+
+# every symbol include/cattleherd.h declares
+EXPORTS = ("ch_default_config", "ch_create", "ch_destroy", "ch_last_error", "ch_shape", "ch_reset", "ch_step",
+           "ch_state_size", "ch_get_state", "ch_set_state", "ch_metrics", "ch_builtin_spawn_table",
+           "ch_spawn_table")
+
+
+class ChConfig(ctypes.Structure):
+    _fields_ = [("abi_version", ctypes.c_int32), ("mode", ctypes.c_int32), ("num_drones", ctypes.c_int32),
+                ("num_cattle", ctypes.c_int32), ("min_drones", ctypes.c_int32), ("max_drones", ctypes.c_int32),
+                ("curriculum_level", ctypes.c_int32), ("ctrl_freq", ctypes.c_int32), ("pyb_freq", ctypes.c_int32),
+                ("compat", ctypes.c_int32), ("precision", ctypes.c_int32), ("torque_world", ctypes.c_int32),
+                ("gyro", ctypes.c_int32), ("damping", ctypes.c_double), ("seed", ctypes.c_uint64),
+                ("env_id_offset", ctypes.c_int64), ("spawn_table", ctypes.POINTER(ctypes.c_double)),
+                ("spawn_scenarios", ctypes.c_int32), ("spawn_cows", ctypes.c_int32)]
+
+
+class ChStepIO(ctypes.Structure):
+    _fields_ = [("actions", ctypes.c_void_p), ("actions_out", ctypes.c_void_p), ("obs", ctypes.c_void_p),
+                ("reward", ctypes.c_void_p), ("terminated", ctypes.c_void_p), ("truncated", ctypes.c_void_p),
+                ("terminal_obs", ctypes.c_void_p), ("agent_active", ctypes.c_void_p),
+                ("reset_happened", ctypes.c_void_p), ("flags", ctypes.c_uint32), ("_pad", ctypes.c_uint32)]
+
+
+class ChError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"libcattleherd error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def lib():
+    """Load libcattleherd.so; raises if it is missing (no fallback path exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                          "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    P = ctypes.POINTER
+    L.ch_default_config.argtypes = [P(ChConfig), i32, i32, i32]
+    L.ch_create.argtypes = [P(ChConfig), i64, i32, P(vp)]
+    L.ch_destroy.argtypes = [vp]
+    L.ch_last_error.argtypes = [vp]
+    L.ch_last_error.restype = ctypes.c_char_p
+    L.ch_shape.argtypes = [vp, P(i64), P(i32), P(i32), P(i32)]
+    L.ch_reset.argtypes = [vp, vp, vp, vp]
+    L.ch_step.argtypes = [vp, P(ChStepIO), vp]
+    L.ch_state_size.argtypes = [vp, P(i64), P(i64)]
+    L.ch_get_state.argtypes = [vp, vp, vp, vp]
+    L.ch_set_state.argtypes = [vp, vp, vp, vp]
+    L.ch_metrics.argtypes = [vp, vp, i32, vp]
+    L.ch_builtin_spawn_table.argtypes = [vp, P(i32), P(i32)]
+    L.ch_spawn_table.argtypes = [i32, vp, P(i32), P(i32)]
+    for name in EXPORTS:
+        if name not in ("ch_last_error",):
+            getattr(L, name).restype = ctypes.c_int
+    _lib = L
+    return L
+
+
+def check(rc, handle=None):
+    if rc != CH_OK:
+        msg = lib().ch_last_error(handle)
+        raise ChError(rc, msg.decode() if msg else "")
+    return rc
+
+
+def default_config(mode, num_drones, num_cattle):
+    c = ChConfig()
+    check(lib().ch_default_config(ctypes.byref(c), mode, num_drones, num_cattle))
+    return c
+
+
+def spawn_table(cows):
+    """The spawn table ch_create uses by default (numpy float64 [100, max(cows,16), 2])."""
+    import numpy as np
+    s, c = ctypes.c_int32(), ctypes.c_int32()
+    check(lib().ch_spawn_table(cows, None, ctypes.byref(s), ctypes.byref(c)))
+    out = np.zeros((s.value, c.value, 2), np.float64)
+    check(lib().ch_spawn_table(cows, out.ctypes.data, None, None))
+    return out

@@ -1,0 +1,194 @@
+"""HerdBatch: E cattle-herding environments resident in HBM, stepped by one HIP launch per step.
+
+This is the product-side host object over the C ABI (include/cattleherd.h).  It owns the device
+buffers the kernels write (torch tensors, so a torch policy can read observations in place) and
+exposes reset/step/get_state/set_state/metrics.  The Gymnasium, SB3-VecEnv and RLlib adapters in
+``gym_pybullet_drones`` and ``cattleherd.vec_env`` are thin layers over it.
+
+Reference: one ``CattleAviary`` (sb3_envs/CattleAviary.py) / ``MARLCattleAviary``
+(rllib_envs/MARLCattleAviary.py) per OS process; here one HerdBatch holds all of a GPU's envs.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib as L
+
+DRONE_COMPS = 22
+CATTLE_COMPS = 4
+ENV_INTS = ("n", "step_counter", "step_counter_A", "has_prev", "level", "tally", "spawn_index", "active_mask",
+            "episode", "reserved")
+
+
+class HerdBatch:
+    def __init__(self, n_envs, num_drones, num_cattle, mode="ctde", device=None, compat=True, precision="f64",
+                 min_drones=None, max_drones=None, curriculum_level=None, seed=0x5EED, env_id_offset=0,
+                 damping=0.04, torque_world=True, gyro=True, ctrl_freq=60, pyb_freq=240, spawn_table=None):
+        import torch
+        if not torch.cuda.is_available():
+            raise RuntimeError("HerdBatch needs a ROCm GPU (torch.cuda.is_available() is False); there is no CPU "
+                               "fallback for the product path")
+        self.torch = torch
+        self.mode = {"ctde": L.CH_MODE_CTDE, "marl": L.CH_MODE_MARL}[mode] if isinstance(mode, str) else int(mode)
+        dev_index = torch.cuda.current_device() if device is None else int(device)
+        cfg = L.default_config(self.mode, num_drones, num_cattle)
+        cfg.compat = int(bool(compat))
+        cfg.precision = {"f64": L.CH_PREC_F64, "f32": L.CH_PREC_F32}[precision]
+        cfg.min_drones = -1 if min_drones is None else int(min_drones)
+        cfg.max_drones = -1 if max_drones is None else int(max_drones)
+        cfg.curriculum_level = -1 if curriculum_level is None else int(curriculum_level)
+        cfg.seed = int(seed)
+        cfg.env_id_offset = int(env_id_offset)
+        cfg.damping = float(damping)
+        cfg.torque_world = int(bool(torque_world))
+        cfg.gyro = int(bool(gyro))
+        cfg.ctrl_freq = int(ctrl_freq)
+        cfg.pyb_freq = int(pyb_freq)
+        self._table = None
+        if spawn_table is not None:
+            self._table = np.ascontiguousarray(spawn_table, np.float64)
+            cfg.spawn_table = self._table.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+            cfg.spawn_scenarios, cfg.spawn_cows = self._table.shape[0], self._table.shape[1]
+        self.cfg = cfg
+        self.handle = ctypes.c_void_p()
+        torch.cuda.set_device(dev_index)
+        L.check(L.lib().ch_create(ctypes.byref(cfg), int(n_envs), dev_index, ctypes.byref(self.handle)))
+        E, R, C, K = ctypes.c_int64(), ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        L.check(L.lib().ch_shape(self.handle, ctypes.byref(E), ctypes.byref(R), ctypes.byref(C), ctypes.byref(K)),
+                self.handle)
+        self.n_envs, self.obs_rows, self.obs_cols, self.reward_cols = E.value, R.value, C.value, K.value
+        self.num_drones, self.num_cattle = num_drones, num_cattle
+        self.device = torch.device("cuda", dev_index)
+        z = dict(device=self.device)
+        self.obs = torch.zeros((self.n_envs, self.obs_rows, 86), dtype=torch.float32, **z)
+        self.terminal_obs = torch.zeros_like(self.obs)
+        self.reward = torch.zeros((self.n_envs, self.reward_cols), dtype=torch.float32, **z)
+        self.terminated = torch.zeros((self.n_envs, self.reward_cols), dtype=torch.uint8, **z)
+        self.truncated = torch.zeros_like(self.terminated)
+        self.agent_active = torch.zeros((self.n_envs, num_drones), dtype=torch.uint8, **z)
+        self.reset_happened = torch.zeros(self.n_envs, dtype=torch.uint8, **z)
+        self.actions = torch.zeros((self.n_envs, num_drones, 4), dtype=torch.float32, **z)
+        self._io = L.ChStepIO()
+
+    # ------------------------------------------------------------------------------------------
+    def _stream(self):
+        return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+
+    def reset(self, mask=None):
+        """BaseAviary.reset for the envs selected by ``mask`` (bool/uint8 [E] device tensor; None = all)."""
+        m = None
+        if mask is not None:
+            mask = mask.to(device=self.device, dtype=self.torch.uint8).contiguous()
+            m = ctypes.c_void_p(mask.data_ptr())
+        L.check(L.lib().ch_reset(self.handle, m, ctypes.c_void_p(self.obs.data_ptr()), self._stream()), self.handle)
+        return self.obs
+
+    def step(self, actions=None, autoreset=True, random_actions=False, terminal_obs=True, step_io=None):
+        """BaseAviary.step for every env.  ``actions``: float32 [E, num_drones, 4] device tensor."""
+        io = self._io
+        flags = (L.CH_STEP_AUTORESET if autoreset else 0) | (L.CH_STEP_RANDOM_ACTIONS if random_actions else 0)
+        if random_actions:
+            io.actions = None
+            io.actions_out = self.actions.data_ptr()
+        else:
+            if actions is None:
+                actions = self.actions
+            if actions.dtype != self.torch.float32 or actions.device != self.device or not actions.is_contiguous():
+                actions = actions.to(device=self.device, dtype=self.torch.float32).contiguous()
+            if tuple(actions.shape) != (self.n_envs, self.num_drones, 4):
+                raise ValueError(f"actions must have shape {(self.n_envs, self.num_drones, 4)}, got {tuple(actions.shape)}")
+            self._keep = actions
+            io.actions = actions.data_ptr()
+            io.actions_out = None
+        io.obs = self.obs.data_ptr()
+        io.reward = self.reward.data_ptr()
+        io.terminated = self.terminated.data_ptr()
+        io.truncated = self.truncated.data_ptr()
+        io.terminal_obs = self.terminal_obs.data_ptr() if (terminal_obs and autoreset) else None
+        io.agent_active = self.agent_active.data_ptr()
+        io.reset_happened = self.reset_happened.data_ptr()
+        io.flags = flags
+        L.check(L.lib().ch_step(self.handle, ctypes.byref(io), self._stream()), self.handle)
+        return self.obs, self.reward, self.terminated, self.truncated
+
+    # ------------------------------------------------------------------------------------------
+    def state_size(self):
+        nd, ni = ctypes.c_int64(), ctypes.c_int64()
+        L.check(L.lib().ch_state_size(self.handle, ctypes.byref(nd), ctypes.byref(ni)), self.handle)
+        return nd.value, ni.value
+
+    def get_state_raw(self):
+        nd, ni = self.state_size()
+        d = np.zeros(nd, np.float64)
+        i = np.zeros(ni, np.int32)
+        L.check(L.lib().ch_get_state(self.handle, d.ctypes.data, i.ctypes.data, self._stream()), self.handle)
+        return d, i
+
+    def set_state_raw(self, d, i):
+        d = np.ascontiguousarray(d, np.float64)
+        i = np.ascontiguousarray(i, np.int32)
+        L.check(L.lib().ch_set_state(self.handle, d.ctypes.data, i.ctypes.data, self._stream()), self.handle)
+
+    def get_state(self):
+        """SoA state as a dict of numpy arrays with a leading env axis (keys as in tests/golden)."""
+        d, ints = self.get_state_raw()
+        E, N, M = self.n_envs, self.num_drones, self.num_cattle
+        nd, nc = DRONE_COMPS * E * N, CATTLE_COMPS * E * M
+        dr = d[:nd].reshape(DRONE_COMPS, E, N)
+        ca = d[nd:nd + nc].reshape(CATTLE_COMPS, E, M)
+        er = d[nd + nc:].reshape(2, E)
+        iv = ints.reshape(len(ENV_INTS), E)
+        s = {"drone_pos": dr[0:3].transpose(1, 2, 0), "drone_quat": dr[3:7].transpose(1, 2, 0),
+             "drone_vel": dr[7:10].transpose(1, 2, 0), "drone_angv": dr[10:13].transpose(1, 2, 0),
+             "pid_last_rpy": dr[13:16].transpose(1, 2, 0), "pid_int_pos": dr[16:19].transpose(1, 2, 0),
+             "pid_int_rpy": dr[19:22].transpose(1, 2, 0),
+             "cow_pos": ca[0:2].transpose(1, 2, 0), "cow_vel": ca[2:4].transpose(1, 2, 0),
+             "prev_cent": er[0].copy(), "clock": er[1].copy()}
+        for k, name in enumerate(ENV_INTS):
+            s[name] = iv[k].copy()
+        s["active"] = ((s["active_mask"][:, None] >> np.arange(N)[None, :]) & 1).astype(np.uint8)
+        return {k: np.ascontiguousarray(v) for k, v in s.items()}
+
+    def set_state(self, s):
+        """Inverse of get_state; any key left out keeps its current value."""
+        d, ints = self.get_state_raw()
+        E, N, M = self.n_envs, self.num_drones, self.num_cattle
+        nd, nc = DRONE_COMPS * E * N, CATTLE_COMPS * E * M
+        dr = d[:nd].reshape(DRONE_COMPS, E, N)
+        ca = d[nd:nd + nc].reshape(CATTLE_COMPS, E, M)
+        er = d[nd + nc:].reshape(2, E)
+        iv = ints.reshape(len(ENV_INTS), E)
+        for key, lo, hi in (("drone_pos", 0, 3), ("drone_quat", 3, 7), ("drone_vel", 7, 10), ("drone_angv", 10, 13),
+                            ("pid_last_rpy", 13, 16), ("pid_int_pos", 16, 19), ("pid_int_rpy", 19, 22)):
+            if key in s:
+                dr[lo:hi] = np.asarray(s[key], np.float64)[:, :N, :].transpose(2, 0, 1)
+        for key, lo, hi in (("cow_pos", 0, 2), ("cow_vel", 2, 4)):
+            if key in s:
+                ca[lo:hi] = np.asarray(s[key], np.float64)[:, :M, :].transpose(2, 0, 1)
+        if "prev_cent" in s:
+            er[0] = np.nan_to_num(np.asarray(s["prev_cent"], np.float64), nan=0.0)
+        if "clock" in s:
+            er[1] = s["clock"]
+        if "active" in s and "active_mask" not in s:
+            a = np.asarray(s["active"]).astype(np.int64)[:, :N]
+            s = dict(s, active_mask=(a << np.arange(N)[None, :]).sum(1))
+        for k, name in enumerate(ENV_INTS):
+            if name in s:
+                iv[k] = np.asarray(s[name]).astype(np.int64)
+        self.set_state_raw(d, ints)
+
+    def metrics(self, reset=False):
+        out = np.zeros(len(L.METRIC_NAMES), np.float64)
+        L.check(L.lib().ch_metrics(self.handle, out.ctypes.data, int(bool(reset)), self._stream()), self.handle)
+        return out
+
+    def close(self):
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            L.lib().ch_destroy(self.handle)
+            self.handle = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,426 @@
+// ch_api.cpp — C ABI of libcattleherd.so (see include/cattleherd.h).
+//
+// Host side: validates the configuration the way the reference's constructors do, owns the SoA
+// state in HBM, and launches the kernels in ch_kernels.hip.  No host<->device traffic on the
+// ch_step path: actions, observations, rewards and flags stay in caller-owned device buffers.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "ch_internal.h"
+#include "ch_spawn_table.inc"
+
+using namespace ch;
+
+struct ch_handle {
+    ch_config cfg{};
+    int64_t E = 0;
+    int device = 0;
+    int NC = 0, M = 0, rows = 0, K = 0, team = 0;
+    int start_level = 0;
+    double episode_len = 0;
+    size_t rsize = 8;
+    void* drone = nullptr;
+    void* cattle = nullptr;
+    void* envr = nullptr;
+    int* envi = nullptr;
+    double* metrics = nullptr;
+    double* spawn = nullptr;
+    int n_scen = 0, n_cows = 0;
+    int64_t step_index = 0;
+    std::string err;
+};
+
+static thread_local std::string g_create_err;
+
+static int fail(ch_handle* h, int code, const std::string& msg) {
+    if (h) h->err = msg; else g_create_err = msg;
+    return code;
+}
+
+#define HIP_TRY(h, expr)                                                                           \
+    do {                                                                                           \
+        hipError_t _e = (expr);                                                                    \
+        if (_e != hipSuccess)                                                                      \
+            return fail((h), CH_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e));   \
+    } while (0)
+
+// episode_length per curriculum level (curriculum_learning.py:24-182)
+static const double kEpisodeLen[8] = {40, 40, 40, 40, 80, 40, 80, 80};
+static const int kLevelMin[8] = {3, 4, 4, 4, 4, 4, 4, 4};
+static const int kLevelMax[8] = {3, 4, 4, 4, 4, 4, 12, 12};
+
+// --------------------------------------------------------------------------------------------
+// Spawn table.  Cows 0..15 of every scenario come from config/cattle_positions.yaml (the
+// reference's only table, BaseAviary.py:88-94, 600-637).  For num_cattle > 16 (beyond what the
+// reference can run, BaseAviary.py:611,719) extra cows are drawn around the scenario's herd
+// centroid with the generator's rules (utils/cattle_spawn.py:5-12: min spacing 0.8, uniform
+// offsets), the offset box widened by 1.25 sqrt(cows/16), rounded to 3 decimals, from a fixed-seed
+// splitmix64 stream — deterministic and identical for every caller.
+// --------------------------------------------------------------------------------------------
+static uint64_t splitmix(uint64_t& s) {
+    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+static std::vector<double> make_spawn_table(int cows) {
+    const int S = CH_SPAWN_SCENARIOS, C0 = CH_SPAWN_COWS;
+    const int C = std::max(cows, C0);
+    std::vector<double> t((size_t)S * C * 2);
+    for (int s = 0; s < S; ++s) {
+        double cx = 0, cy = 0;
+        for (int j = 0; j < C0; ++j) {
+            t[((size_t)s * C + j) * 2] = CH_SPAWN_TABLE[(s * C0 + j) * 2];
+            t[((size_t)s * C + j) * 2 + 1] = CH_SPAWN_TABLE[(s * C0 + j) * 2 + 1];
+            cx += CH_SPAWN_TABLE[(s * C0 + j) * 2];
+            cy += CH_SPAWN_TABLE[(s * C0 + j) * 2 + 1];
+        }
+        cx /= C0; cy /= C0;
+        uint64_t st = 0xC0FFEEull * (s + 1);
+        double half = 2.5 * std::sqrt((double)C / C0), mind = 0.8;
+        for (int j = C0; j < C; ++j) {
+            for (int attempt = 0;; ++attempt) {
+                if (attempt > 0 && attempt % 2000 == 0) mind *= 0.95;
+                double ox = ((splitmix(st) >> 11) * (1.0 / 9007199254740992.0) * 2 - 1) * half;
+                double oy = ((splitmix(st) >> 11) * (1.0 / 9007199254740992.0) * 2 - 1) * half;
+                double x = std::round((cx + ox) * 1000.0) / 1000.0, y = std::round((cy + oy) * 1000.0) / 1000.0;
+                bool ok = true;
+                for (int k = 0; k < j && ok; ++k) {
+                    double dx = x - t[((size_t)s * C + k) * 2], dy = y - t[((size_t)s * C + k) * 2 + 1];
+                    ok = std::sqrt(dx * dx + dy * dy) >= mind;
+                }
+                if (ok) { t[((size_t)s * C + j) * 2] = x; t[((size_t)s * C + j) * 2 + 1] = y; break; }
+            }
+        }
+    }
+    return t;
+}
+
+template <class R>
+static StepParams<R> params(ch_handle* h) {
+    StepParams<R> p{};
+    const ch_config& c = h->cfg;
+    p.E = (int)h->E; p.NC = h->NC; p.M = h->M; p.mode = c.mode; p.rows = h->rows;
+    p.min_drones = c.min_drones; p.max_drones = c.max_drones; p.ctrl_freq = c.ctrl_freq;
+    p.substeps = c.pyb_freq / c.ctrl_freq; p.compat = c.compat; p.torque_world = c.torque_world; p.gyro = c.gyro;
+    p.episode_len = h->episode_len; p.damping = c.damping;
+    p.dt_ctrl = 1.0 / c.ctrl_freq; p.dt = 1.0 / c.pyb_freq;
+    p.k0 = (uint32_t)c.seed; p.k1 = (uint32_t)(c.seed >> 32);
+    p.env_off = c.env_id_offset; p.step_index = h->step_index;
+    p.drone = (R*)h->drone; p.cattle = (R*)h->cattle; p.envr = (R*)h->envr; p.envi = h->envi;
+    p.metrics = h->metrics; p.spawn = h->spawn; p.n_scen = h->n_scen; p.n_cows = h->n_cows;
+    return p;
+}
+
+extern "C" {
+
+int ch_builtin_spawn_table(double* out, int32_t* scenarios, int32_t* cows) {
+    if (scenarios) *scenarios = CH_SPAWN_SCENARIOS;
+    if (cows) *cows = CH_SPAWN_COWS;
+    if (out) std::memcpy(out, CH_SPAWN_TABLE, sizeof(CH_SPAWN_TABLE));
+    return CH_OK;
+}
+
+int ch_spawn_table(int32_t cows, double* out, int32_t* scenarios, int32_t* out_cows) {
+    std::vector<double> t = make_spawn_table(cows);
+    int C = std::max(cows, (int)CH_SPAWN_COWS);
+    if (scenarios) *scenarios = CH_SPAWN_SCENARIOS;
+    if (out_cows) *out_cows = C;
+    if (out) std::memcpy(out, t.data(), t.size() * sizeof(double));
+    return CH_OK;
+}
+
+int ch_default_config(ch_config* c, int32_t mode, int32_t num_drones, int32_t num_cattle) {
+    if (!c) return fail(nullptr, CH_ERR_INVALID, "ch_default_config: cfg is NULL");
+    std::memset(c, 0, sizeof(*c));
+    c->abi_version = CH_ABI_VERSION;
+    c->mode = mode;
+    c->num_drones = num_drones;
+    c->num_cattle = num_cattle;
+    c->min_drones = -1;
+    c->max_drones = -1;
+    c->curriculum_level = -1;
+    c->ctrl_freq = 60;
+    c->pyb_freq = 240;
+    c->compat = 1;
+    c->precision = CH_PREC_F64;
+    c->torque_world = 1;
+    c->gyro = 1;
+    c->damping = 0.04;
+    c->seed = 0x5EEDull;
+    c->env_id_offset = 0;
+    c->spawn_table = nullptr;
+    return CH_OK;
+}
+
+const char* ch_last_error(const ch_handle* h) { return h ? h->err.c_str() : g_create_err.c_str(); }
+
+static void free_all(ch_handle* h) {
+    void* ptrs[] = {h->drone, h->cattle, h->envr, h->envi, h->metrics, h->spawn};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+}
+
+int ch_create(const ch_config* c, int64_t n_envs, int32_t device, ch_handle** out) {
+    if (!c || !out) return fail(nullptr, CH_ERR_INVALID, "ch_create: NULL argument");
+    *out = nullptr;
+    if (c->abi_version != CH_ABI_VERSION) return fail(nullptr, CH_ERR_INVALID, "ch_create: abi_version mismatch");
+    if (c->mode != CH_MODE_CTDE && c->mode != CH_MODE_MARL) return fail(nullptr, CH_ERR_INVALID, "ch_create: bad mode");
+    if (n_envs <= 0 || n_envs > (1ll << 28)) return fail(nullptr, CH_ERR_INVALID, "ch_create: n_envs out of range");
+    if (c->num_drones < 1 || c->num_drones > kNMax)
+        return fail(nullptr, CH_ERR_INVALID, "ch_create: num_drones must be in [1, 12] (GLOBAL_MAX_NUM_DRONES)");
+    if (c->num_cattle < 1 || c->num_cattle > kMMax)
+        return fail(nullptr, CH_ERR_INVALID, "ch_create: num_cattle must be in [1, 64]");
+    if (c->ctrl_freq <= 0 || c->pyb_freq <= 0 || c->pyb_freq % c->ctrl_freq != 0)
+        return fail(nullptr, CH_ERR_INVALID, "[ERROR] in BaseAviary.__init__(), pyb_freq is not divisible by env_freq.");
+    if (c->precision != CH_PREC_F64 && c->precision != CH_PREC_F32)
+        return fail(nullptr, CH_ERR_INVALID, "ch_create: bad precision");
+    int level = c->curriculum_level < 0 ? (c->mode == CH_MODE_CTDE ? 7 : 0) : c->curriculum_level;
+    if (level > 7) return fail(nullptr, CH_ERR_INVALID, "ch_create: curriculum_level must be in [0, 7]");
+    int mn = c->min_drones < 0 ? c->num_drones : c->min_drones;
+    int mx = c->max_drones < 0 ? c->num_drones : c->max_drones;
+    if (mn < 1 || mx < mn || mx > c->num_drones)
+        return fail(nullptr, CH_ERR_INVALID,
+                    "ch_create: need 1 <= min_drones <= max_drones <= num_drones (the reference indexes "
+                    "self.ctrl[k] sized by num_drones, BaseRLAviary.py:80)");
+    if (c->compat && mn < 2)
+        return fail(nullptr, CH_ERR_UNSUPPORTED,
+                    "compat mode: the reference raises ValueError for a single drone (np.partition kth=1, "
+                    "CattleAviary.py:234); use compat=0");
+    if (c->spawn_table && (c->spawn_scenarios < 1 || c->spawn_cows < c->num_cattle))
+        return fail(nullptr, CH_ERR_INVALID, "ch_create: spawn table smaller than num_cattle");
+    int dev_count = 0;
+    hipError_t ge = hipGetDeviceCount(&dev_count);
+    if (ge != hipSuccess || dev_count == 0)
+        return fail(nullptr, CH_ERR_DEVICE, std::string("ch_create: no HIP device: ") + hipGetErrorString(ge));
+    if (device < 0 || device >= dev_count) return fail(nullptr, CH_ERR_INVALID, "ch_create: bad device index");
+
+    ch_handle* h = new (std::nothrow) ch_handle();
+    if (!h) return fail(nullptr, CH_ERR_NOMEM, "ch_create: out of host memory");
+    h->cfg = *c;
+    h->cfg.curriculum_level = level;
+    h->cfg.min_drones = mn;
+    h->cfg.max_drones = mx;
+    h->E = n_envs;
+    h->device = device;
+    h->NC = c->num_drones;
+    h->M = c->num_cattle;
+    h->rows = c->mode == CH_MODE_CTDE ? 12 : c->num_drones;
+    h->K = c->mode == CH_MODE_CTDE ? 1 : c->num_drones;
+    int need = std::max(h->NC, h->M);
+    h->team = need <= 16 ? 16 : (need <= 32 ? 32 : 64);
+    h->start_level = level;
+    h->episode_len = kEpisodeLen[level];
+    h->rsize = c->precision == CH_PREC_F64 ? sizeof(double) : sizeof(float);
+    (void)kLevelMin; (void)kLevelMax;
+
+    auto cleanup = [&](int code) { free_all(h); std::string m = h->err; delete h; g_create_err = m; return code; };
+#define CTRY(expr)                                                                                  \
+    do {                                                                                            \
+        hipError_t _e = (expr);                                                                     \
+        if (_e != hipSuccess) {                                                                     \
+            h->err = std::string(#expr) + ": " + hipGetErrorString(_e);                             \
+            return cleanup(_e == hipErrorOutOfMemory ? CH_ERR_NOMEM : CH_ERR_DEVICE);               \
+        }                                                                                           \
+    } while (0)
+    CTRY(hipSetDevice(device));
+    const int64_t E = h->E;
+    CTRY(hipMalloc(&h->drone, h->rsize * kDroneComps * E * h->NC));
+    CTRY(hipMalloc(&h->cattle, h->rsize * kCattleComps * E * h->M));
+    CTRY(hipMalloc(&h->envr, h->rsize * kEnvReal * E));
+    CTRY(hipMalloc(&h->envi, sizeof(int) * kEnvInt * E));
+    CTRY(hipMalloc(&h->metrics, sizeof(double) * kMetricRows * E));
+
+    std::vector<double> table;
+    if (c->spawn_table) {
+        table.assign(c->spawn_table, c->spawn_table + (size_t)c->spawn_scenarios * c->spawn_cows * 2);
+        h->n_scen = c->spawn_scenarios;
+        h->n_cows = c->spawn_cows;
+    } else {
+        table = make_spawn_table(h->M);
+        h->n_scen = CH_SPAWN_SCENARIOS;
+        h->n_cows = std::max(h->M, (int)CH_SPAWN_COWS);
+    }
+    CTRY(hipMalloc(&h->spawn, table.size() * sizeof(double)));
+    CTRY(hipMemcpy(h->spawn, table.data(), table.size() * sizeof(double), hipMemcpyHostToDevice));
+
+    // initial state = what the constructors leave behind before the first reset():
+    // identity quaternions, zero PID state, spawn index advanced once by __init__'s _housekeeping.
+    std::vector<double> dz((size_t)kDroneComps * E * h->NC, 0.0);
+    for (int64_t i = 0; i < E * h->NC; ++i) dz[(size_t)6 * E * h->NC + i] = 1.0;
+    std::vector<int> ei((size_t)kEnvInt * E, 0);
+    for (int64_t e = 0; e < E; ++e) {
+        ei[4 * E + e] = level;
+        ei[6 * E + e] = (int)((1 + c->env_id_offset + e) % h->n_scen);
+    }
+    int rc = 0;
+    {
+        std::vector<double> cz((size_t)kCattleComps * E * h->M, 0.0), rz((size_t)kEnvReal * E, 0.0);
+        if (h->rsize == sizeof(double)) {
+            CTRY(hipMemcpy(h->drone, dz.data(), dz.size() * 8, hipMemcpyHostToDevice));
+            CTRY(hipMemcpy(h->cattle, cz.data(), cz.size() * 8, hipMemcpyHostToDevice));
+            CTRY(hipMemcpy(h->envr, rz.data(), rz.size() * 8, hipMemcpyHostToDevice));
+        } else {
+            std::vector<float> f(dz.begin(), dz.end()), fc(cz.begin(), cz.end()), fr(rz.begin(), rz.end());
+            CTRY(hipMemcpy(h->drone, f.data(), f.size() * 4, hipMemcpyHostToDevice));
+            CTRY(hipMemcpy(h->cattle, fc.data(), fc.size() * 4, hipMemcpyHostToDevice));
+            CTRY(hipMemcpy(h->envr, fr.data(), fr.size() * 4, hipMemcpyHostToDevice));
+        }
+        CTRY(hipMemcpy(h->envi, ei.data(), ei.size() * sizeof(int), hipMemcpyHostToDevice));
+        CTRY(hipMemset(h->metrics, 0, sizeof(double) * kMetricRows * E));
+    }
+    (void)rc;
+#undef CTRY
+    *out = h;
+    return CH_OK;
+}
+
+int ch_destroy(ch_handle* h) {
+    if (!h) return CH_OK;
+    (void)hipSetDevice(h->device);
+    free_all(h);
+    delete h;
+    return CH_OK;
+}
+
+int ch_shape(const ch_handle* h, int64_t* n_envs, int32_t* obs_rows, int32_t* obs_cols, int32_t* reward_cols) {
+    if (!h) return fail(nullptr, CH_ERR_INVALID, "ch_shape: NULL handle");
+    if (n_envs) *n_envs = h->E;
+    if (obs_rows) *obs_rows = h->rows;
+    if (obs_cols) *obs_cols = 86;
+    if (reward_cols) *reward_cols = h->K;
+    return CH_OK;
+}
+
+int ch_reset(ch_handle* h, const uint8_t* mask_dev, float* obs_dev, void* stream) {
+    if (!h) return fail(nullptr, CH_ERR_INVALID, "ch_reset: NULL handle");
+    if (!obs_dev) return fail(h, CH_ERR_INVALID, "ch_reset: obs is NULL");
+    HIP_TRY(h, hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e;
+    if (h->rsize == sizeof(double)) {
+        StepParams<double> p = params<double>(h);
+        p.reset_mask = mask_dev; p.obs = obs_dev;
+        e = launch_reset(p, h->team, st);
+    } else {
+        StepParams<float> p = params<float>(h);
+        p.reset_mask = mask_dev; p.obs = obs_dev;
+        e = launch_reset(p, h->team, st);
+    }
+    if (e != hipSuccess) return fail(h, CH_ERR_DEVICE, std::string("ch_reset launch: ") + hipGetErrorString(e));
+    return CH_OK;
+}
+
+int ch_step(ch_handle* h, const ch_step_io* io, void* stream) {
+    if (!h) return fail(nullptr, CH_ERR_INVALID, "ch_step: NULL handle");
+    if (!io) return fail(h, CH_ERR_INVALID, "ch_step: io is NULL");
+    if (!io->obs || !io->reward || !io->terminated || !io->truncated)
+        return fail(h, CH_ERR_INVALID, "ch_step: obs, reward, terminated and truncated are required");
+    if (!(io->flags & CH_STEP_RANDOM_ACTIONS) && !io->actions)
+        return fail(h, CH_ERR_INVALID, "ch_step: actions is NULL (and CH_STEP_RANDOM_ACTIONS not set)");
+    if (io->actions && (reinterpret_cast<uintptr_t>(io->actions) & 15))
+        return fail(h, CH_ERR_INVALID, "ch_step: actions must be 16-byte aligned");
+    if ((reinterpret_cast<uintptr_t>(io->obs) & 15) ||
+        (io->terminal_obs && (reinterpret_cast<uintptr_t>(io->terminal_obs) & 15)))
+        return fail(h, CH_ERR_INVALID, "ch_step: obs buffers must be 16-byte aligned");
+    HIP_TRY(h, hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e;
+    auto fill = [&](auto& p) {
+        p.actions = io->actions; p.actions_out = io->actions_out; p.obs = io->obs; p.reward = io->reward;
+        p.term = io->terminated; p.trunc = io->truncated; p.terminal_obs = io->terminal_obs;
+        p.agent_active = io->agent_active; p.reset_happened = io->reset_happened; p.flags = io->flags;
+    };
+    if (h->rsize == sizeof(double)) {
+        StepParams<double> p = params<double>(h);
+        fill(p);
+        e = launch_step(p, h->team, st);
+    } else {
+        StepParams<float> p = params<float>(h);
+        fill(p);
+        e = launch_step(p, h->team, st);
+    }
+    if (e != hipSuccess) return fail(h, CH_ERR_DEVICE, std::string("ch_step launch: ") + hipGetErrorString(e));
+    h->step_index += 1;
+    return CH_OK;
+}
+
+int ch_state_size(const ch_handle* h, int64_t* n_doubles, int64_t* n_ints) {
+    if (!h) return fail(nullptr, CH_ERR_INVALID, "ch_state_size: NULL handle");
+    if (n_doubles) *n_doubles = (int64_t)kDroneComps * h->E * h->NC + (int64_t)kCattleComps * h->E * h->M + kEnvReal * h->E;
+    if (n_ints) *n_ints = (int64_t)kEnvInt * h->E;
+    return CH_OK;
+}
+
+int ch_get_state(ch_handle* h, double* hd, int32_t* hi, void* stream) {
+    if (!h) return fail(nullptr, CH_ERR_INVALID, "ch_get_state: NULL handle");
+    HIP_TRY(h, hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    HIP_TRY(h, hipStreamSynchronize(st));
+    const size_t nd = (size_t)kDroneComps * h->E * h->NC, nc = (size_t)kCattleComps * h->E * h->M,
+                 nr = (size_t)kEnvReal * h->E;
+    if (hd) {
+        if (h->rsize == sizeof(double)) {
+            HIP_TRY(h, hipMemcpy(hd, h->drone, nd * 8, hipMemcpyDeviceToHost));
+            HIP_TRY(h, hipMemcpy(hd + nd, h->cattle, nc * 8, hipMemcpyDeviceToHost));
+            HIP_TRY(h, hipMemcpy(hd + nd + nc, h->envr, nr * 8, hipMemcpyDeviceToHost));
+        } else {
+            std::vector<float> f(nd + nc + nr);
+            HIP_TRY(h, hipMemcpy(f.data(), h->drone, nd * 4, hipMemcpyDeviceToHost));
+            HIP_TRY(h, hipMemcpy(f.data() + nd, h->cattle, nc * 4, hipMemcpyDeviceToHost));
+            HIP_TRY(h, hipMemcpy(f.data() + nd + nc, h->envr, nr * 4, hipMemcpyDeviceToHost));
+            for (size_t i = 0; i < f.size(); ++i) hd[i] = f[i];
+        }
+    }
+    if (hi) HIP_TRY(h, hipMemcpy(hi, h->envi, sizeof(int) * kEnvInt * h->E, hipMemcpyDeviceToHost));
+    return CH_OK;
+}
+
+int ch_set_state(ch_handle* h, const double* hd, const int32_t* hi, void* stream) {
+    if (!h) return fail(nullptr, CH_ERR_INVALID, "ch_set_state: NULL handle");
+    HIP_TRY(h, hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    HIP_TRY(h, hipStreamSynchronize(st));
+    const size_t nd = (size_t)kDroneComps * h->E * h->NC, nc = (size_t)kCattleComps * h->E * h->M,
+                 nr = (size_t)kEnvReal * h->E;
+    if (hd) {
+        if (h->rsize == sizeof(double)) {
+            HIP_TRY(h, hipMemcpy(h->drone, hd, nd * 8, hipMemcpyHostToDevice));
+            HIP_TRY(h, hipMemcpy(h->cattle, hd + nd, nc * 8, hipMemcpyHostToDevice));
+            HIP_TRY(h, hipMemcpy(h->envr, hd + nd + nc, nr * 8, hipMemcpyHostToDevice));
+        } else {
+            std::vector<float> f(hd, hd + nd + nc + nr);
+            HIP_TRY(h, hipMemcpy(h->drone, f.data(), nd * 4, hipMemcpyHostToDevice));
+            HIP_TRY(h, hipMemcpy(h->cattle, f.data() + nd, nc * 4, hipMemcpyHostToDevice));
+            HIP_TRY(h, hipMemcpy(h->envr, f.data() + nd + nc, nr * 4, hipMemcpyHostToDevice));
+        }
+    }
+    if (hi) HIP_TRY(h, hipMemcpy(h->envi, hi, sizeof(int) * kEnvInt * h->E, hipMemcpyHostToDevice));
+    return CH_OK;
+}
+
+int ch_metrics(ch_handle* h, double* out, int32_t reset_after, void* stream) {
+    if (!h || !out) return fail(h, CH_ERR_INVALID, "ch_metrics: NULL argument");
+    HIP_TRY(h, hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    HIP_TRY(h, hipStreamSynchronize(st));
+    std::vector<double> m((size_t)kMetricRows * h->E);
+    HIP_TRY(h, hipMemcpy(m.data(), h->metrics, m.size() * sizeof(double), hipMemcpyDeviceToHost));
+    for (int r = 0; r < CH_METRIC_COUNT; ++r) {
+        double s = 0;
+        for (int64_t e = 0; e < h->E; ++e) s += m[(size_t)r * h->E + e];
+        out[r] = s;
+    }
+    if (reset_after) HIP_TRY(h, hipMemset(h->metrics, 0, sizeof(double) * CH_METRIC_COUNT * h->E));
+    return CH_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,291 @@
+// ch_device.h — device-side math of the batched cattle-herding step (gfx950, HIP).
+//
+// Each function restates one piece of the reference's env.step() (paths relative to
+// gym_pybullet_drones/ in BenCooper305/RL-Cattle-Herding).  Templated on the state precision R
+// (double = the reference's arithmetic; float = throughput mode).  Operation order follows the
+// reference so that, with -ffp-contract=off, the fp64 path reproduces the CPU oracle to the last
+// few ulps (transcendentals differ by <= 1 ulp between ocml and glibc).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ch {
+
+// ---- constants: assets/cf2x.urdf:5-12, BaseAviary.py:97-173, DSLPIDControl.py:37-53 ----------
+constexpr double kG = 9.8, kMass = 0.027, kKF = 3.16e-10, kKM = 7.94e-12;
+constexpr double kJx = 1.4e-5, kJy = 1.4e-5, kJz = 2.17e-5;
+constexpr double kTargetAlt = 0.45;
+constexpr double kPwmScale = 0.2685, kPwmConst = 4070.3, kMinPwm = 20000, kMaxPwm = 65535;
+constexpr double kMaxSpeedKmh = 30.0;
+constexpr double kMaxVelCattle = 0.2;                       // BaseAviary.py:579
+constexpr double kMissionBoundary = 15, kMaxFormation = 8, kCollision = 0.2;  // CattleAviary.py:94-97
+constexpr double kPi = 3.14159265358979323846;
+
+// curriculum_learning.py:10-194
+struct Level {
+    double desired, tol, hold, approach_min, min_eff, cattle_desired, cattle_tol;
+    int min_drones, max_drones;
+    double episode_len;
+    double w_simple, w_complex, w_survival, w_approach, w_eff, w_cattle;
+    int required_tally;
+};
+__constant__ static const Level kLevels[8] = {
+    {0.8, 0.3, 10, 0.0, 0, 0.0, 0.0, 3, 3, 40, 1, 0, 0, 0, 0, 0.0, 100},
+    {0.8, 0.2, 25, 0.0, 0, 0.0, 0.0, 4, 4, 40, 0, 1, -0.5, 0, 0, 0.0, 300},
+    {0.8, 0.2, 15, 0.6, 0, 0.0, 0.0, 4, 4, 40, 0, 0.8, 0, 1, 0, 0.0, 100},
+    {0.8, 0.2, 15, 0.3, 0, 0.0, 0.0, 4, 4, 40, 0, 0.8, -0.5, 1, 0, 0.0, 400},
+    {0.8, 0.2, 15, 0.3, 20, 0.0, 0.0, 4, 4, 80, 0, 0.7, -0.0, 0.8, 1, 0.0, 600},
+    {0.8, 0.2, 15, 0.3, 50, 0.8, 0.1, 4, 4, 40, 0, 0.7, -0.5, 0.6, 1, 0.8, 600},
+    {0.8, 0.3, 15, 0.2, 50, 0.0, 0.0, 4, 12, 80, 0.7, 0.0, -0.0, 0.8, 1, 0.0, 600},
+    {0.8, 0.3, 15, 0.2, 50, 0.0, 0.0, 4, 12, 80, 0.0, 0.0, -0.0, 1, 1, 0.0, 600},
+};
+
+template <class R> __device__ __forceinline__ R clip(R x, R lo, R hi) { return x < lo ? lo : (x > hi ? hi : x); }
+template <class R> __device__ __forceinline__ R norm2(R x, R y) { return sqrt(x * x + y * y); }
+
+// ---- pybullet.c quaternion conventions (x, y, z, w) ------------------------------------------
+template <class R> __device__ __forceinline__ void quat_to_mat(const R q[4], R M[9]) {
+    R x = q[0], y = q[1], z = q[2], w = q[3];
+    R d = x * x + y * y + z * z + w * w, s = R(2.0) / d;
+    R xs = x * s, ys = y * s, zs = z * s;
+    R wx = w * xs, wy = w * ys, wz = w * zs, xx = x * xs, xy = x * ys, xz = x * zs;
+    R yy = y * ys, yz = y * zs, zz = z * zs;
+    M[0] = R(1.0) - (yy + zz); M[1] = xy - wz; M[2] = xz + wy;
+    M[3] = xy + wz; M[4] = R(1.0) - (xx + zz); M[5] = yz - wx;
+    M[6] = xz - wy; M[7] = yz + wx; M[8] = R(1.0) - (xx + yy);
+}
+
+template <class R> __device__ __forceinline__ void quat_to_euler(const R q[4], R rpy[3]) {
+    R x = q[0], y = q[1], z = q[2], w = q[3];
+    R sqx = x * x, sqy = y * y, sqz = z * z, squ = w * w;
+    R sarg = R(-2.0) * (x * z - w * y);
+    if (sarg <= R(-0.99999)) {
+        rpy[0] = 0; rpy[1] = R(-0.5 * kPi); rpy[2] = R(2) * atan2(x, -y);
+    } else if (sarg >= R(0.99999)) {
+        rpy[0] = 0; rpy[1] = R(0.5 * kPi); rpy[2] = R(2) * atan2(-x, y);
+    } else {
+        rpy[0] = atan2(R(2) * (y * z + w * x), squ - sqx - sqy + sqz);
+        rpy[1] = asin(sarg);
+        rpy[2] = atan2(R(2) * (x * y + w * z), squ + sqx - sqy - sqz);
+    }
+}
+
+// ---- DSLPIDControl.computeControl for a VEL target (DSLPIDControl.py:82-259,
+//      BaseRLAviary.py:185-222).  pid[9] = last_rpy[3], integral_pos_e[3], integral_rpy_e[3].
+template <class R>
+__device__ __forceinline__ void pid_vel(const R pos[3], const R q[4], const R vel[3], const R Rm[9], const R rpy[3],
+                                        const float act[4], R dt, R pid[9], R rpm[4]) {
+    // _preprocessAction VEL branch: the float32 action row keeps the unit vector in float32;
+    // SPEED_LIMIT * abs(a[3]) is float32 under NumPy >= 2 (DESIGN.md "Numerics").
+    const double speed_limit = 0.3 * kMaxSpeedKmh * (1000.0 / 3600.0);
+    float hx = act[0], hy = act[1];
+    float hn = __fsqrt_rn(__fadd_rn(__fmul_rn(hx, hx), __fmul_rn(hy, hy)));
+    float ux = 0.0f, uy = 0.0f;
+    if (hn != 0.0f) { ux = __fdiv_rn(hx, hn); uy = __fdiv_rn(hy, hn); }
+    float sc = __fmul_rn((float)speed_limit, fabsf(act[3]));
+    const R tv[3] = {R((double)ux * (double)sc), R((double)uy * (double)sc), R(0.0 * (double)sc)};
+    const R tp[3] = {pos[0], pos[1], R(kTargetAlt)};
+    const R yaw = rpy[2];
+
+    const R P_FOR[3] = {R(.4), R(.4), R(1.25)}, I_FOR[3] = {R(.05), R(.05), R(.05)}, D_FOR[3] = {R(.2), R(.2), R(.5)};
+    R pe[3], ve[3], T[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        pe[i] = tp[i] - pos[i];
+        ve[i] = tv[i] - vel[i];
+        pid[3 + i] = clip(pid[3 + i] + pe[i] * dt, R(-2.), R(2.));
+    }
+    pid[5] = clip(pid[5], R(-0.15), R(.15));
+#pragma unroll
+    for (int i = 0; i < 3; ++i) T[i] = P_FOR[i] * pe[i] + I_FOR[i] * pid[3 + i] + D_FOR[i] * ve[i];
+    T[2] += R(kG * kMass);
+    R scalar = T[0] * Rm[2] + T[1] * Rm[5] + T[2] * Rm[8];
+    if (!(scalar > R(0))) scalar = 0;
+    R thrust = (sqrt(scalar / (R(4) * R(kKF))) - R(kPwmConst)) / R(kPwmScale);
+    R tn = sqrt(T[0] * T[0] + T[1] * T[1] + T[2] * T[2]);
+    R z[3] = {T[0] / tn, T[1] / tn, T[2] / tn};
+    R xc[3] = {cos(yaw), sin(yaw), R(0)};
+    R yt[3] = {z[1] * xc[2] - z[2] * xc[1], z[2] * xc[0] - z[0] * xc[2], z[0] * xc[1] - z[1] * xc[0]};
+    R yn = sqrt(yt[0] * yt[0] + yt[1] * yt[1] + yt[2] * yt[2]);
+    R y[3] = {yt[0] / yn, yt[1] / yn, yt[2] / yn};
+    R x[3] = {y[1] * z[2] - y[2] * z[1], y[2] * z[0] - y[0] * z[2], y[0] * z[1] - y[1] * z[0]};
+    // target rotation columns x, y, z; rot_e from (Rt^T R - R^T Rt)
+    const R Rt[9] = {x[0], y[0], z[0], x[1], y[1], z[1], x[2], y[2], z[2]};
+    auto E = [&](int i, int j) {
+        R a = 0, b = 0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { a += Rt[k * 3 + i] * Rm[k * 3 + j]; b += Rm[k * 3 + i] * Rt[k * 3 + j]; }
+        return a - b;
+    };
+    const R rot_e[3] = {E(2, 1), E(0, 2), E(1, 0)};
+    const R P_TOR[3] = {R(70000.), R(70000.), R(60000.)}, I_TOR[3] = {R(.0), R(.0), R(500.)},
+            D_TOR[3] = {R(20000.), R(20000.), R(12000.)};
+    R rates_e[3], tt[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        rates_e[i] = R(0.0) - (rpy[i] - pid[i]) / dt;
+        pid[i] = rpy[i];
+        pid[6 + i] = clip(pid[6 + i] - rot_e[i] * dt, R(-1500.), R(1500.));
+    }
+    pid[6] = clip(pid[6], R(-1.), R(1.));
+    pid[7] = clip(pid[7], R(-1.), R(1.));
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+        tt[i] = clip(-P_TOR[i] * rot_e[i] + D_TOR[i] * rates_e[i] + I_TOR[i] * pid[6 + i], R(-3200), R(3200));
+    const R MIX[4][3] = {{R(-.5), R(-.5), R(-1)}, {R(-.5), R(.5), R(1)}, {R(.5), R(.5), R(-1)}, {R(.5), R(-.5), R(1)}};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        R pwm = thrust + (MIX[k][0] * tt[0] + MIX[k][1] * tt[1] + MIX[k][2] * tt[2]);
+        pwm = clip(pwm, R(kMinPwm), R(kMaxPwm));
+        rpm[k] = R(kPwmScale) * pwm + R(kPwmConst);
+    }
+    (void)q;
+}
+
+// ---- _physics (BaseAviary.py:907-939) + one p.stepSimulation substep (448): btMultiBody model ----
+template <class R>
+__device__ __forceinline__ void drone_substep(R p[3], R q[4], R v[3], R w[3], const R rpm[4], R dt, R damping,
+                                              bool torque_world, bool gyro) {
+    const R PX[4] = {R(0.028), R(-0.028), R(-0.028), R(0.028)}, PY[4] = {R(-0.028), R(-0.028), R(0.028), R(0.028)};
+    R M[9];
+    quat_to_mat(q, M);
+    R F[3] = {0, 0, 0}, Tw[3] = {0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        R f = rpm[i] * rpm[i] * R(kKF);
+        R fw[3] = {M[2] * f, M[5] * f, M[8] * f};
+        R rw[3] = {M[0] * PX[i] + M[1] * PY[i], M[3] * PX[i] + M[4] * PY[i], M[6] * PX[i] + M[7] * PY[i]};
+        R t[3] = {rw[1] * fw[2] - rw[2] * fw[1], rw[2] * fw[0] - rw[0] * fw[2], rw[0] * fw[1] - rw[1] * fw[0]};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { F[k] += fw[k]; Tw[k] += t[k]; }
+    }
+    R t0 = rpm[0] * rpm[0] * R(kKM), t1 = rpm[1] * rpm[1] * R(kKM), t2 = rpm[2] * rpm[2] * R(kKM),
+      t3 = rpm[3] * rpm[3] * R(kKM);
+    R tz = (-t0 + t1 - t2 + t3);
+    if (torque_world) Tw[2] += tz;
+    else { Tw[0] += M[2] * tz; Tw[1] += M[5] * tz; Tw[2] += M[8] * tz; }
+    F[2] += R(-kMass * kG);
+    const R k = damping;
+    if (k != R(0)) {
+        R sp = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) F[i] -= R(kMass) * v[i] * (k + k * sp);
+    }
+    R wb[3], tb[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        wb[i] = M[0 + i] * w[0] + M[3 + i] * w[1] + M[6 + i] * w[2];
+        tb[i] = M[0 + i] * Tw[0] + M[3 + i] * Tw[1] + M[6 + i] * Tw[2];
+    }
+    const R J[3] = {R(kJx), R(kJy), R(kJz)};
+    if (k != R(0)) {
+        R sw = sqrt(wb[0] * wb[0] + wb[1] * wb[1] + wb[2] * wb[2]);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) tb[i] -= J[i] * wb[i] * (k + k * sw);
+    }
+    if (gyro) {
+        R Jw[3] = {J[0] * wb[0], J[1] * wb[1], J[2] * wb[2]};
+        R g[3] = {wb[1] * Jw[2] - wb[2] * Jw[1], wb[2] * Jw[0] - wb[0] * Jw[2], wb[0] * Jw[1] - wb[1] * Jw[0]};
+#pragma unroll
+        for (int i = 0; i < 3; ++i) tb[i] -= g[i];
+    }
+    R ab[3] = {tb[0] / J[0], tb[1] / J[1], tb[2] / J[2]};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        R aw = M[i * 3 + 0] * ab[0] + M[i * 3 + 1] * ab[1] + M[i * 3 + 2] * ab[2];
+        v[i] = v[i] + (F[i] / R(kMass)) * dt;
+        w[i] = w[i] + aw * dt;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) p[i] = p[i] + v[i] * dt;
+    // btMultiBody::stepPositionsMultiDof exponential-map quaternion update (base body)
+    R fang = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    if (fang * dt > R(0.5 * (0.5 * kPi))) fang = R(0.5 * (0.5 * kPi)) / dt;
+    R s;
+    if (fang < R(0.001)) s = R(0.5) * dt - (dt * dt * dt) * R(0.020833333333) * fang * fang;
+    else s = sin(R(0.5) * fang * dt) / fang;
+    R a[4] = {w[0] * s, w[1] * s, w[2] * s, cos(fang * dt * R(0.5))};
+    R o[4] = {a[3] * q[0] + a[0] * q[3] + a[1] * q[2] - a[2] * q[1],
+              a[3] * q[1] + a[1] * q[3] + a[2] * q[0] - a[0] * q[2],
+              a[3] * q[2] + a[2] * q[3] + a[0] * q[1] - a[1] * q[0],
+              a[3] * q[3] - a[0] * q[0] - a[1] * q[1] - a[2] * q[2]};
+    R n = sqrt(o[0] * o[0] + o[1] * o[1] + o[2] * o[2] + o[3] * o[3]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = o[i] / n;
+}
+
+// ---- flocking: MathematicalFlock (flockUtils.py:11-382) ----------------------------------------
+constexpr double kEps = 0.1, kH = 0.2;
+template <class R> __device__ __forceinline__ R sigma_norm_n(R n) { return (sqrt(R(1) + R(kEps) * (n * n)) - R(1)) / R(kEps); }
+template <class R> __device__ __forceinline__ R bump(R z) {
+    if (z < R(0)) return R(0);
+    if (z < R(kH)) return R(1);
+    if (z <= R(1)) return (R(1) + cos(R(kPi) * (z - R(kH)) / (R(1) - R(kH)))) / R(2);
+    return R(0);
+}
+template <class R> __device__ __forceinline__ R sigma_1(R z) { return z / sqrt(R(1) + z * z); }
+
+// gradient (phi_alpha * n_ij) and velocity-consensus (a_ij * (pj - pi)) contributions of one
+// neighbour (flockUtils.py:327-337, 41-49, 365-374); ra = sigma_norm(r), da = sigma_norm(d)
+template <class R>
+__device__ __forceinline__ void pair_terms(R qix, R qiy, R pix, R piy, R qjx, R qjy, R pjx, R pjy, R ra, R da,
+                                           R& gx, R& gy, R& cx, R& cy) {
+    R zx = qjx - qix, zy = qjy - qiy;
+    R n = sqrt(zx * zx + zy * zy);
+    R den = sqrt(R(1) + R(kEps) * (n * n));
+    R sn = (den - R(1)) / R(kEps);
+    R b = bump(sn / ra);
+    R zz = sn - da;
+    R ph = b * ((R(5.0 + 5.0) * sigma_1(zz + R(0.0)) + R(5.0 - 5.0)) / R(2));
+    gx += ph * (zx / den);
+    gy += ph * (zy / den);
+    cx += b * (pjx - pix);
+    cy += b * (pjy - piy);
+}
+
+// ---- spacing rewards: CattleAviary.py:572-679 -------------------------------------------------
+template <class R> __device__ __forceinline__ R simple_spacing(R r, const Level& L) {
+    R desired = R(L.desired), tol = desired * R(L.tol);
+    R lb = desired - tol, ub = desired + tol;
+    if (lb <= r && r <= ub) return R(1.0);
+    if (r < lb) return R(-1) + (r / lb) * R(2);
+    if (r > ub) return R(1) - ((r - ub) / (R(7.0) - ub)) * R(2);
+    return R(-1.0);
+}
+template <class R> __device__ __forceinline__ R complex_spacing(R r, const Level& L) {
+    R ds = R(L.desired);
+    R t = (r - ds) / R(0.4 + 1e-9);
+    R gauss = exp(R(-0.5) * (t * t));
+    R coll = r < R(0.3) ? R(-1.0) * (R(1.0) - (r / R(0.3 + 1e-9))) : R(0.0);
+    R pull = r > R(1.5) ? R(-0.3) * (r - R(1.5)) / R(5.0 - 1.5) : R(0.0);
+    R rew = gauss + coll + pull;
+    rew += R(0.1) * (R(1) - fabs(r - ds));
+    return rew;
+}
+template <class R> __device__ __forceinline__ R cattle_spacing(R r) {
+    const double A = 1.2, B = 2.1, C = 3.3, K = 0.2, D = -1, R0 = 1.3, LAM = 0.8;
+    if (r <= R(R0))
+        return R(A) * exp(-((r - R(D)) * (r - R(D))) / R(2 * (C * C))) - R(B) * exp(-(r * r) / R(2 * (K * K)));
+    R fr0 = R(A) * exp(-(R(R0 - D) * R(R0 - D)) / R(2 * (C * C))) - R(B) * exp(-(R(R0) * R(R0)) / R(2 * (K * K)));
+    R Cc = fr0 / exp(R(-LAM) * R(R0));
+    return Cc * exp(R(-LAM) * r);
+}
+
+// ---- Philox4x32-10 (Random123) ------------------------------------------------------------------
+__device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        uint32_t lo0 = 0xD2511F53u * c[0], hi0 = __umulhi(0xD2511F53u, c[0]);
+        uint32_t lo1 = 0xCD9E8D57u * c[2], hi1 = __umulhi(0xCD9E8D57u, c[2]);
+        uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+        c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+}
+__device__ __forceinline__ double philox_uniform53(uint32_t k0, uint32_t k1, uint64_t episode, uint32_t j, uint32_t env) {
+    uint32_t c[4] = {(uint32_t)episode, (uint32_t)(episode >> 32), j | (1u << 16), env};
+    philox(c, k0, k1);
+    return ((double)(c[0] >> 5) * 67108864.0 + (double)(c[1] >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+}  // namespace ch

@@ -1,0 +1,71 @@
+"""CPU tests: the C-ABI library loads, exports every symbol include/cattleherd.h declares, and its
+host-only entry points behave (no GPU needed)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_symbols():
+    src = open(os.path.join(ROOT, "include", "cattleherd.h")).read()
+    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(ch_\w+)\(", src, re.M)))
+
+
+def test_library_exports_header_symbols():
+    from cattleherd import _lib
+    L = _lib.lib()
+    syms = _header_symbols()
+    assert len(syms) >= 12
+    for s in syms:
+        assert hasattr(L, s), s
+    assert set(syms) == set(_lib.EXPORTS)
+
+
+def test_default_config_and_struct_layout():
+    from cattleherd import _lib
+    c = _lib.default_config(_lib.CH_MODE_CTDE, 12, 16)
+    assert c.abi_version == _lib.ABI_VERSION and c.ctrl_freq == 60 and c.pyb_freq == 240
+    assert c.compat == 1 and c.damping == 0.04 and c.min_drones == -1
+    assert ctypes.sizeof(_lib.ChStepIO) == 9 * 8 + 8
+
+
+def test_builtin_spawn_table_is_the_reference_yaml(spawn16):
+    from cattleherd import _lib
+    t = _lib.spawn_table(16)
+    assert t.shape == (100, 16, 2)
+    assert np.array_equal(t, spawn16)
+    t32 = _lib.spawn_table(32)
+    assert t32.shape == (100, 32, 2) and np.array_equal(t32[:, :16], spawn16)
+    d = np.linalg.norm(t32[:, 16:, None] - t32[:, None], axis=-1)   # extra cows vs all cows
+    d[:, np.arange(16), 16 + np.arange(16)] = 9
+    assert d.min() >= 0.75   # the generator's 0.8 spacing (cattle_spawn.py:12), relaxed at most 5 %
+
+
+def test_create_without_gpu_fails_loudly():
+    """No CPU fallback: ch_create reports a device error when no HIP device is visible."""
+    import torch
+    if torch.cuda.is_available():
+        return
+    from cattleherd import _lib
+    c = _lib.default_config(0, 4, 16)
+    h = ctypes.c_void_p()
+    rc = _lib.lib().ch_create(ctypes.byref(c), 8, 0, ctypes.byref(h))
+    assert rc == _lib.CH_ERR_DEVICE
+    assert b"no HIP device" in _lib.lib().ch_last_error(None)
+
+
+def test_invalid_configs_rejected():
+    from cattleherd import _lib
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    c = _lib.default_config(0, 13, 16)
+    assert L.ch_create(ctypes.byref(c), 8, 0, ctypes.byref(h)) == _lib.CH_ERR_INVALID
+    c = _lib.default_config(0, 4, 16)
+    c.pyb_freq = 250
+    assert L.ch_create(ctypes.byref(c), 8, 0, ctypes.byref(h)) == _lib.CH_ERR_INVALID
+    assert b"pyb_freq is not divisible" in L.ch_last_error(None)
+    c = _lib.default_config(0, 1, 4)
+    assert L.ch_create(ctypes.byref(c), 8, 0, ctypes.byref(h)) == _lib.CH_ERR_UNSUPPORTED

@@ -1,0 +1,229 @@
+"""GPU parity tests: the HIP path (libcattleherd.so via its C ABI) against the reference's golden
+vectors and against the CPU oracle on identical seeded inputs.
+
+Tolerances (stated per north_star's fp32 bar, tighter for the fp64 path):
+  fp64 path: obs (float32 outputs) rtol 1e-6 / atol 1e-7; reward rtol 1e-9; states rtol 1e-9;
+             flags exact.
+  fp32 path: obs / reward / state rtol 1e-4 (the north_star's 1e-4 relative), flags on >= 99 %.
+"""
+import numpy as np
+import pytest
+
+from helpers import close, load, rollout_files, stack, state_at
+
+pytestmark = pytest.mark.gpu
+
+
+def _batch(mode, n, m, E, ctor_level, **kw):
+    from cattleherd.env import HerdBatch
+    return HerdBatch(E, n, m, mode="ctde" if mode == 0 else "marl", curriculum_level=ctor_level, **kw)
+
+
+def _inject(b, states):
+    s = stack(states)
+    s = {k: v for k, v in s.items() if k not in ("m", "ctor_level", "episode_len")}
+    b.set_state(s)
+
+
+@pytest.mark.parametrize("fname", rollout_files())
+def test_rollout_fixture_parity(fname):
+    """Every step of each golden rollout, batched: env t starts from fixture state t and takes
+    fixture action t; one launch steps them all."""
+    import torch
+    d = load(fname)
+    mode = 0 if fname.startswith("ctde") else 1
+    T = len(d["action"])
+    states = [state_at(d, "state_", t) for t in range(T)]
+    n, m, lvl = int(states[0]["n"]), int(states[0]["m"]), int(states[0]["ctor_level"])
+    b = _batch(mode, n, m, T, lvl)
+    b.reset()
+    _inject(b, states)
+    acts = torch.tensor(d["action"], device=b.device)
+    obs, rew, te, tr = b.step(acts, autoreset=False)
+    torch.cuda.synchronize()
+    obs, rew, te, tr = obs.cpu().numpy(), rew.cpu().numpy(), te.cpu().numpy(), tr.cpu().numpy()
+    if mode == 0:
+        assert close(obs, d["obs"], 1e-6, 1e-7)[0]
+        assert close(rew[:, 0], d["reward"], 1e-9, 1e-9)[0]
+        assert np.array_equal(te[:, 0], d["terminated"]) and np.array_equal(tr[:, 0], d["truncated"])
+    else:
+        act = np.stack([s["active"][:n] for s in states]).astype(bool)
+        assert close(obs[act], d["obs"][act], 1e-6, 1e-7)[0]
+        assert close(rew[act], d["reward"][act], 1e-9, 1e-9)[0]
+        assert np.array_equal(te[act], d["terminated"][act]) and np.array_equal(tr[act], d["truncated"][act])
+    g = b.get_state()
+    resets = set(d["reset_at"].tolist())
+    idx = [t for t in range(T - 1) if t not in resets]
+    nxt = stack([states[t + 1] for t in idx])
+    for k in ("drone_pos", "drone_quat", "drone_vel", "drone_angv", "pid_int_rpy", "pid_int_pos", "pid_last_rpy"):
+        assert close(g[k][idx, :n], nxt[k][:, :n], 1e-9, 1e-12)[0], k
+    assert close(g["cow_pos"][idx, :m], nxt["cow_pos"][:, :m], 1e-12, 1e-13)[0]
+    assert close(g["cow_vel"][idx, :m], nxt["cow_vel"][:, :m], 1e-12, 1e-14)[0]
+    for k in ("step_counter", "step_counter_A", "level", "tally"):
+        assert np.array_equal(g[k][idx], nxt[k]), k
+    b.close()
+
+
+def _oracle_states(mode, n, m, E, table, steps, seed, level, compat=True):
+    """E oracle envs, each advanced a different number of random steps (diverse states)."""
+    import oracle as O
+    envs, states = [], []
+    rng = np.random.default_rng(seed)
+    for e in range(E):
+        env = O.Env(mode, n, m, table, start_level=level, env_id=e, compat=compat)
+        env.reset()
+        for t in range(int(rng.integers(0, steps))):
+            env.step(rng.uniform(-1, 1, (n, 4)).astype(np.float32), autoreset=True)
+        envs.append(env)
+        states.append(env.get_state())
+    return envs, states
+
+
+@pytest.mark.parametrize("mode,n,m,level,compat", [
+    (0, 4, 16, 7, True), (0, 2, 8, 7, True), (0, 12, 16, 7, True), (0, 5, 16, 0, True), (0, 4, 16, 4, True),
+    (0, 3, 4, 2, True), (0, 2, 8, 7, False), (1, 3, 8, 0, True), (1, 4, 32, 0, True), (1, 4, 16, 6, True),
+    (1, 6, 16, 1, False), (0, 4, 32, 7, True), (0, 8, 64, 7, True)])
+def test_step_vs_oracle(mode, n, m, level, compat):
+    """One GPU launch over E diverse states vs the oracle stepping each state (no auto-reset)."""
+    import torch
+    from cattleherd._lib import spawn_table
+    table = spawn_table(m)
+    E = 48
+    envs, states = _oracle_states(mode, n, m, E, table, 160, seed=n * 100 + m + level, level=level, compat=compat)
+    b = _batch(mode, n, m, E, level, compat=compat)
+    b.reset()
+    b.set_state(stack([{k: v for k, v in s.items() if k != "episode"} for s in states]))
+    rng = np.random.default_rng(7)
+    acts = rng.uniform(-1, 1, (E, n, 4)).astype(np.float32)
+    obs, rew, te, tr = b.step(torch.tensor(acts, device=b.device), autoreset=False)
+    torch.cuda.synchronize()
+    ref = [env.step(acts[e], autoreset=False) for e, env in enumerate(envs)]
+    R = b.obs_rows
+    assert close(obs.cpu().numpy(), np.stack([r[0] for r in ref]).reshape(E, R, 86), 1e-6, 1e-7)[0]
+    K = b.reward_cols
+    rr = np.stack([r[1] for r in ref]).reshape(E, K)
+    assert close(rew.cpu().numpy(), rr.astype(np.float32), 1e-6, 1e-6)[0]
+    assert np.array_equal(te.cpu().numpy(), np.stack([r[2] for r in ref]).reshape(E, K))
+    assert np.array_equal(tr.cpu().numpy(), np.stack([r[3] for r in ref]).reshape(E, K))
+    g = b.get_state()
+    want = stack([env.get_state() for env in envs])
+    for k in ("drone_pos", "drone_quat", "drone_vel", "drone_angv", "pid_int_rpy", "pid_int_pos", "pid_last_rpy"):
+        assert close(g[k][:, :n], want[k][:, :n], 1e-9, 1e-12)[0], k
+    assert close(g["cow_pos"], want["cow_pos"][:, :m], 1e-12, 1e-13)[0]
+    assert close(g["cow_vel"], want["cow_vel"][:, :m], 1e-12, 1e-14)[0]
+    for k in ("step_counter", "step_counter_A", "level", "tally", "has_prev", "spawn_index"):
+        assert np.array_equal(g[k], want[k]), k
+    assert close(g["clock"], want["clock"], 1e-12, 1e-12)[0]
+    if mode == 1:
+        assert np.array_equal(g["active"][:, :n], want["active"][:, :n])
+    b.close()
+
+
+@pytest.mark.parametrize("mode,n,m", [(0, 4, 16), (1, 4, 16), (0, 2, 8)])
+def test_random_rollout_with_autoreset_vs_oracle(mode, n, m):
+    """Device Philox actions + in-kernel auto-reset for 240 steps vs the oracle's identical Philox
+    stream: actions bit-exact, per-step rewards / flags / reset timing agree."""
+    import torch
+    import oracle as O
+    from cattleherd._lib import spawn_table
+    table = spawn_table(m)
+    E, T = 16, 240
+    b = _batch(mode, n, m, E, None)
+    b.reset()
+    envs = [O.Env(mode, n, m, table, env_id=e) for e in range(E)]
+    o0 = np.stack([env.reset() for env in envs])
+    assert close(b.obs.cpu().numpy(), o0, 1e-6, 1e-7)[0]
+    mismatched_flags = 0
+    for t in range(T):
+        b.step(random_actions=True, autoreset=True)
+        torch.cuda.synchronize()
+        acts = b.actions.cpu().numpy()
+        for e, env in enumerate(envs):
+            a = env.random_actions(t)
+            assert np.array_equal(a, acts[e]), (t, e)
+            o, r, te, tr, done, _ = env.step(a, autoreset=True)
+            if mode == 0:
+                mismatched_flags += int(te[0] != b.terminated[e, 0].item() or tr[0] != b.truncated[e, 0].item())
+    st = b.get_state()
+    want = stack([env.get_state() for env in envs])
+    assert mismatched_flags == 0
+    assert np.array_equal(st["episode"], want["episode"])
+    assert np.array_equal(st["spawn_index"], want["spawn_index"])
+    assert close(st["cow_pos"], want["cow_pos"][:, :m], 1e-7, 1e-8)[0]
+    assert close(st["drone_pos"][:, :n], want["drone_pos"][:, :n], 1e-6, 1e-7)[0]
+    b.close()
+
+
+def test_reset_parity_and_spawn():
+    """ch_reset: spawn scenario (env_id+2) mod 100 on the first reset, start layout, Philox cattle
+    velocities identical to the oracle's."""
+    import torch
+    import oracle as O
+    from cattleherd._lib import spawn_table
+    for n, m in ((4, 16), (7, 16), (3, 32)):
+        table = spawn_table(m)
+        E = 130
+        b = _batch(0, n, m, E, None)
+        obs = b.reset()
+        torch.cuda.synchronize()
+        envs = [O.Env(0, n, m, table, env_id=e) for e in range(E)]
+        o = np.stack([env.reset() for env in envs])
+        assert close(obs.cpu().numpy(), o, 1e-6, 1e-7)[0]
+        st = b.get_state()
+        assert np.array_equal(st["spawn_index"], (np.arange(E) + 2) % 100)
+        want = stack([env.get_state() for env in envs])
+        assert close(st["cow_vel"], want["cow_vel"][:, :m], 1e-15, 1e-15)[0]
+        assert np.array_equal(st["cow_pos"], want["cow_pos"][:, :m])
+        b.close()
+
+
+def test_f32_path_within_north_star_tolerance():
+    """CH_PREC_F32: one step from the same diverse states within 1e-4 relative of the fp64 oracle."""
+    import torch
+    from cattleherd._lib import spawn_table
+    n, m, E = 4, 16, 64
+    table = spawn_table(m)
+    envs, states = _oracle_states(0, n, m, E, table, 120, seed=3, level=7)
+    b = _batch(0, n, m, E, 7, precision="f32")
+    b.reset()
+    b.set_state(stack([{k: v for k, v in s.items() if k != "episode"} for s in states]))
+    acts = np.random.default_rng(1).uniform(-1, 1, (E, n, 4)).astype(np.float32)
+    obs, rew, te, tr = b.step(torch.tensor(acts, device=b.device), autoreset=False)
+    torch.cuda.synchronize()
+    ref = [env.step(acts[e], autoreset=False) for e, env in enumerate(envs)]
+    ro = np.stack([r[0] for r in ref])
+    assert close(obs.cpu().numpy(), ro, 1e-4, 1e-4)[0]
+    rr = np.array([r[1][0] for r in ref])
+    assert close(rew.cpu().numpy()[:, 0], rr, 1e-3, 1e-3)[0]
+    agree = np.mean(tr.cpu().numpy()[:, 0] == np.array([r[3][0] for r in ref]))
+    assert agree >= 0.99
+    b.close()
+
+
+def test_full_size_properties():
+    """BASELINE size (4096 envs x (4 drones, 16 cattle)): determinism across handles, sharding
+    invariance (env_id_offset), unit quaternions, cattle speed cap, counters, finite obs."""
+    import torch
+    E, n, m, T = 4096, 4, 16, 64
+    a = _batch(0, n, m, E, None)
+    b2 = _batch(0, n, m, E, None)
+    sh = _batch(0, n, m, E // 2, None, env_id_offset=E // 2)
+    for h in (a, b2, sh):
+        h.reset()
+    for t in range(T):
+        for h in (a, b2, sh):
+            h.step(random_actions=True, autoreset=True)
+    torch.cuda.synchronize()
+    assert torch.equal(a.obs, b2.obs) and torch.equal(a.reward, b2.reward)
+    assert torch.equal(a.obs[E // 2:], sh.obs)
+    s = a.get_state()
+    q = np.linalg.norm(s["drone_quat"], axis=-1)
+    assert np.all(np.abs(q - 1) < 1e-12)
+    sp = np.linalg.norm(s["cow_vel"], axis=-1)
+    assert np.all(sp <= 0.2 + 1e-12)
+    assert np.all(s["step_counter_A"] <= T) and np.all(s["step_counter"] % 4 == 0)
+    assert torch.isfinite(a.obs).all()
+    met = a.metrics()
+    assert met[0] == E * T
+    for h in (a, b2, sh):
+        h.close()

@@ -1,0 +1,173 @@
+"""CPU tests: the oracle (oracle/ch_oracle.c) against the golden vectors generated from the reference's
+own Python (tests/golden/make_golden.py) and against the recorded PyBullet trace.
+
+These pin the oracle before it is trusted as the checker of the HIP path.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from helpers import close, load, rollout_files, state_at
+
+
+def test_flock_matches_reference():
+    """BaseAviary._flockingStep (sb3_envs/BaseAviary.py:1352-1400) incl. predator range <= 1.1 m."""
+    f = load("flock.npz")
+    for i in range(len(f["n"])):
+        n, m = int(f["n"][i]), int(f["m"][i])
+        out = O.flock_update(f["cow_pos"][i, :m], f["cow_vel"][i, :m], f["drone_pos"][i, :n])
+        ok, err = close(out, f["new_vel"][i, :m], rtol=1e-12, atol=1e-15)
+        assert ok, (i, err)
+
+
+def test_effectiveness_matches_reference():
+    """evaluate_herding_effectiveness (utils/evaluation.py:100-138), exact incl. lattice edge cases."""
+    e = load("effectiveness.npz")
+    for i in range(len(e["n"])):
+        v = O.effectiveness(e["cow_pos"][i, :e["m"][i]], e["drone_pos"][i, :e["n"][i]])
+        assert v == e["eff"][i], i
+
+
+def test_pid_sequences_match_reference():
+    """DSLPIDControl.computeControl (control/DSLPIDControl.py:82-259), stateful sequences."""
+    p = load("pid.npz")
+    for s in range(p["pos"].shape[0]):
+        lr, ip, ir = np.zeros(3), np.zeros(3), np.zeros(3)
+        for t in range(p["pos"].shape[1]):
+            rpm, lr, ip, ir = O.pid_vel(p["pos"][s, t], p["quat"][s, t], p["vel"][s, t], p["target_pos"][s, t],
+                                        p["target_rpy"][s, t], p["target_vel"][s, t], 1 / 60, lr, ip, ir)
+            assert close(rpm, p["rpm"][s, t], 1e-12, 1e-9)[0], (s, t)
+            for a, k in ((lr, "last_rpy"), (ip, "int_pos"), (ir, "int_rpy")):
+                assert close(a, p[k][s, t], 1e-12, 1e-12)[0], (s, t, k)
+
+
+def test_spacing_rewards_match_reference():
+    """SimpleSpacingReward / DroneSpacingRewardFunction / CattleSpacingRewardFunction incl. inf/NaN inputs."""
+    s = load("spacing.npz")
+    for lvl in range(8):
+        a = np.array([O.simple_spacing(r, lvl) for r in s["r"]])
+        b = np.array([O.complex_spacing(r, lvl) for r in s["r"]])
+        assert close(a, s[f"simple_{lvl}"], 1e-14, 1e-14)[0]
+        assert close(b, s[f"complex_{lvl}"], 1e-14, 1e-14)[0]
+    c = np.array([O.cattle_spacing(r) for r in s["r"]])
+    assert close(c, s["cattle"], 1e-14, 1e-14)[0]
+
+
+@pytest.mark.parametrize("fname,mode", [("task_ctde.npz", 0), ("task_marl.npz", 1)])
+def test_task_sequence_matches_reference(fname, mode, spawn16):
+    """reward → terminated → truncated with their side effects (clock, prev_cent, curriculum, agents)."""
+    d = load(fname)
+    for i in range(len(d["reward"])):
+        sin, sout = state_at(d, "in_", i), state_at(d, "out_", i)
+        n = int(sin["n"])
+        env = O.Env(mode, n, int(sin["m"]), spawn16, start_level=int(sin["ctor_level"]))
+        env.set_state(sin)
+        r, te, tr = env.task()
+        st = env.get_state()
+        if mode == 0:
+            assert close(r, [d["reward"][i]], 1e-9, 1e-12)[0], i
+            assert te[0] == d["terminated"][i] and tr[0] == d["truncated"][i], i
+        else:
+            act = sin["active"][:n].astype(bool)
+            assert close(r[:n][act], d["reward"][i][:n][act], 1e-9, 1e-12)[0], i
+            assert np.array_equal(te[:n], d["terminated"][i][:n]) and np.array_equal(tr[:n], d["truncated"][i][:n]), i
+            assert np.array_equal(st["active"][:n], sout["active"][:n]), i
+        assert st["level"] == sout["level"] and st["tally"] == sout["tally"], i
+        assert abs(st["clock"] - sout["clock"]) < 1e-12, i
+        assert st["has_prev"] == sout["has_prev"], i
+        if st["has_prev"]:
+            assert abs(st["prev_cent"] - sout["prev_cent"]) < 1e-12, i
+
+
+@pytest.mark.parametrize("fname", rollout_files())
+def test_rollout_step_matches_reference(fname, spawn16):
+    """Whole env.step with state injection at every step (stub physics in the reference's loop)."""
+    d = load(fname)
+    mode = 0 if fname.startswith("ctde") else 1
+    s0 = state_at(d, "state_", 0)
+    n, m = int(s0["n"]), int(s0["m"])
+    env = O.Env(mode, n, m, spawn16, start_level=int(s0["ctor_level"]))
+    resets = set(d["reset_at"].tolist())
+    T = len(d["action"])
+    for t in range(T):
+        st = state_at(d, "state_", t)
+        env.set_state(st)
+        o, r, te, tr, _, _ = env.step(d["action"][t], autoreset=False)
+        if mode == 0:
+            assert close(o, d["obs"][t], 1e-6, 1e-9)[0], t
+            assert close(r, [d["reward"][t]], 1e-9, 1e-11)[0], t
+            assert te[0] == d["terminated"][t] and tr[0] == d["truncated"][t], t
+        else:
+            act = st["active"][:n].astype(bool)
+            assert close(o[:n][act], d["obs"][t][act], 1e-6, 1e-9)[0], t
+            assert close(r[:n][act], d["reward"][t][act], 1e-9, 1e-11)[0], t
+            assert np.array_equal(te[:n][act], d["terminated"][t][act]), t
+            assert np.array_equal(tr[:n][act], d["truncated"][t][act]), t
+        if t + 1 < T and t not in resets:
+            nx = state_at(d, "state_", t + 1)
+            g = env.get_state()
+            for k, w in (("drone_pos", 3), ("drone_quat", 4), ("drone_vel", 3), ("drone_angv", 3),
+                         ("pid_int_rpy", 3), ("pid_int_pos", 3), ("pid_last_rpy", 3)):
+                assert close(g[k][:n], nx[k][:n], 1e-9, 1e-12)[0], (t, k)
+            assert close(g["cow_pos"][:m], nx["cow_pos"][:m], 1e-12, 1e-13)[0], t
+            assert close(g["cow_vel"][:m], nx["cow_vel"][:m], 1e-12, 1e-14)[0], t
+            for k in ("step_counter", "step_counter_A", "level", "tally"):
+                assert g[k] == nx[k], (t, k)
+
+
+def test_reset_bookkeeping_matches_reference(spawn16):
+    """reset(): spawn index advances before use (first reset after the ctor uses scenario 2),
+    drone start layout (BaseAviary.py:251-277), cattle from the YAML table."""
+    r = load("reset.npz")
+    env = O.Env(0, 5, 16, spawn16)
+    for k in range(len(r["spawn_index"])):
+        env.reset()
+        st = env.get_state()
+        assert st["spawn_index"] == r["spawn_index"][k]
+        assert np.array_equal(st["drone_pos"][:5], r["drone_pos_n5"][k])
+        assert np.array_equal(st["cow_pos"][:16], r["cow_pos"][k])
+    for n in range(2, 13):
+        e = O.Env(0, n, 4, spawn16)
+        e.reset()
+        assert np.array_equal(e.get_state()["drone_pos"][:n], r[f"init_pos_n{n}"]), n
+
+
+@pytest.mark.parametrize("seg", ["seg0", "seg1"])
+def test_trace_replay_real_pybullet(seg):
+    """evaluation_data.pkl (real PyBullet): every recorded flock update and cattle position is
+    reproduced; drone xy fits semi-implicit Euler at 240 Hz far better than explicit Euler."""
+    d = load("trace_eval.npz")
+    cp, cv, dp, dv = d[seg + "_cattle_pos"], d[seg + "_cattle_vel"], d[seg + "_drone_pos"], d[seg + "_drone_vel"]
+    for k in range(len(cp) - 1):
+        nv = O.flock_update(cp[k], cv[k], dp[k]) if (k + 1) % 2 == 0 else cv[k]
+        assert close(nv, cv[k + 1], 0, 1e-15)[0], k
+        p = cp[k].copy()
+        for _ in range(4):
+            p = p + cv[k + 1] * (1 / 240)
+        assert np.array_equal(p, cp[k + 1]), k
+        assert O.effectiveness(cp[k], dp[k]) == d[seg + "_effectiveness"][k]
+    dt = 1 / 240
+    sym = dp[1:] - dp[:-1] - dt * (1.5 * dv[:-1] + 2.5 * dv[1:])
+    exp_ = dp[1:] - dp[:-1] - 4 * dt * dv[:-1]
+    assert np.sqrt(np.mean(sym ** 2)) * 10 < np.sqrt(np.mean(exp_ ** 2))
+
+
+def test_nan_reward_quirk_two_drones(spawn16):
+    """CTDE reward is NaN for 2 drones (inf nearest-neighbour distance x weight 0), CattleAviary.py:234-300."""
+    d = load("ctde_roll_n2_m8_l7.npz")
+    assert np.all(np.isnan(d["reward"]))
+    env = O.Env(0, 2, 8, spawn16)
+    env.reset()
+    _, r, _, _, _, _ = env.step(np.zeros((2, 4), np.float32))
+    assert np.isnan(r[0])
+    env2 = O.Env(0, 2, 8, spawn16, compat=False)
+    env2.reset()
+    _, r2, _, _, _, _ = env2.step(np.zeros((2, 4), np.float32))
+    assert np.isfinite(r2[0])
+
+
+def test_batch_rollout_runs():
+    """CPU baseline entry point (OpenMP over envs) runs and auto-resets."""
+    table = load("reset.npz")["spawn_table"]
+    secs, steps = O.batch_rollout(0, 4, 16, table, E=8, T=50, threads=2)
+    assert steps == 400 and secs > 0
