@@ -68,6 +68,10 @@ typedef struct ch_config {
     int32_t precision;        /* CH_PREC_F64 (reference arithmetic) or CH_PREC_F32 */
     int32_t torque_world;     /* 1 = applyExternalTorque(LINK_FRAME) acts in world frame (default) */
     int32_t gyro;             /* 1 = gyroscopic term (btMultiBody default) */
+    int32_t marl_wrapper;     /* MARL only: 1 = RLlibMultiAgentWrapper.step semantics (marl_wrapper.py:77-119:
+                                 per-agent recomputation, finished agents drop out, episode ends when all
+                                 agents terminated); 0 = bare MARLCattleAviary.step dicts
+                                 (rllib_envs/BaseAviary.py:425-431) */
     double damping;           /* btMultiBody default linear/angular damping 0.04 */
     uint64_t seed;            /* Philox key for resets and random actions */
     int64_t env_id_offset;    /* global index of env 0 (multi-GPU sharding) */

@@ -587,11 +587,19 @@ void och_task(const och_config* c, och_state* s, double* reward, uint8_t* termin
         truncated[0] = (uint8_t)trunc_ctde(c, s, &g);
     } else {
         int n = s->n;
-        /* env.step's own dicts (rllib_envs/BaseAviary.py:425-431) — side effects only */
-        for (int i = 0; i < n; ++i) (void)reward_marl(c, s, &g, i);
-        for (int i = 0; i < n; ++i) (void)term_call(c, s, &g);
-        /* the wrapper's recomputation for active agents (marl_wrapper.py:104-113) */
+        /* env.step's own dicts (rllib_envs/BaseAviary.py:425-431) */
+        double r1[OCH_NMAX];
+        uint8_t d1[OCH_NMAX];
+        for (int i = 0; i < n; ++i) r1[i] = reward_marl(c, s, &g, i);
+        for (int i = 0; i < n; ++i) d1[i] = (uint8_t)term_call(c, s, &g);
         for (int i = 0; i < c->n_ctor; ++i) { reward[i] = NAN; terminated[i] = 0; truncated[i] = 0; }
+        if (!c->marl_wrapper) {
+            for (int i = 0; i < n; ++i) {
+                reward[i] = r1[i]; terminated[i] = d1[i]; truncated[i] = (uint8_t)trunc_marl(c, s, &g, i);
+            }
+            return;
+        }
+        /* the wrapper's recomputation for active agents (marl_wrapper.py:104-113) */
         for (int i = 0; i < n; ++i) {
             if (!s->active[i]) continue;
             reward[i] = reward_marl(c, s, &g, i);
@@ -764,7 +772,8 @@ int och_step(const och_config* c, och_state* s, const float* actions, float* obs
     s->step_counter += (c->mode == 0) ? substeps : 1;
     int done;
     if (c->mode == 0) done = terminated[0] || truncated[0];
-    else { done = 1; for (int i = 0; i < n; ++i) if (s->active[i]) done = 0; }
+    else if (c->marl_wrapper) { done = 1; for (int i = 0; i < n; ++i) if (s->active[i]) done = 0; }
+    else { done = 1; for (int i = 0; i < n; ++i) done &= terminated[i]; }
     if (done && autoreset) {
         if (terminal_obs) och_obs(c, s, terminal_obs);
         och_reset(c, s);

@@ -30,6 +30,7 @@ typedef struct och_config {
     uint64_t seed;
     const double* spawn_table;   /* [n_scen][n_cows][2] */
     int32_t spawn_scenarios, spawn_cows;
+    int32_t marl_wrapper;     /* MARL: 1 = RLlibMultiAgentWrapper.step semantics, 0 = bare env.step */
 } och_config;
 
 typedef struct och_state {

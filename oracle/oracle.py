@@ -30,7 +30,7 @@ class Config(ctypes.Structure):
                 ("compat", ctypes.c_int32), ("damping", ctypes.c_double), ("torque_world", ctypes.c_int32),
                 ("gyro", ctypes.c_int32), ("seed", ctypes.c_uint64),
                 ("spawn_table", ctypes.POINTER(ctypes.c_double)), ("spawn_scenarios", ctypes.c_int32),
-                ("spawn_cows", ctypes.c_int32)]
+                ("spawn_cows", ctypes.c_int32), ("marl_wrapper", ctypes.c_int32)]
 
 
 D3 = ctypes.c_double * 3
@@ -146,7 +146,7 @@ class Env:
 
     def __init__(self, mode, n_ctor, m, spawn_table, min_drones=None, max_drones=None, start_level=None,
                  compat=True, seed=0x5EED, env_id=0, damping=0.04, torque_world=True, gyro=True,
-                 ctrl_freq=60, pyb_freq=240):
+                 ctrl_freq=60, pyb_freq=240, marl_wrapper=True):
         self.table = np.ascontiguousarray(spawn_table, np.float64)
         if start_level is None:
             start_level = 7 if mode == 0 else 0
@@ -156,7 +156,7 @@ class Env:
                           start_level=start_level, ctrl_freq=ctrl_freq, pyb_freq=pyb_freq,
                           compat=int(compat), damping=damping, torque_world=int(torque_world), gyro=int(gyro),
                           seed=seed, spawn_table=_dp(self.table), spawn_scenarios=self.table.shape[0],
-                          spawn_cows=self.table.shape[1])
+                          spawn_cows=self.table.shape[1], marl_wrapper=int(marl_wrapper))
         self.st = State()
         lib().och_init(ctypes.byref(self.cfg), ctypes.byref(self.st), env_id)
         self.rows = lib().och_obs_rows(ctypes.byref(self.cfg))
@@ -236,7 +236,7 @@ def batch_rollout(mode, n, m, spawn_table, E, T, threads=0, seed=0x5EED, compat=
     table = np.ascontiguousarray(spawn_table, np.float64)
     cfg = Config(mode=mode, n_ctor=n, m=m, min_drones=n, max_drones=n, start_level=7 if mode == 0 else 0,
                  ctrl_freq=60, pyb_freq=240, compat=int(compat), damping=0.04, torque_world=1, gyro=1, seed=seed,
-                 spawn_table=_dp(table), spawn_scenarios=table.shape[0], spawn_cows=table.shape[1])
+                 spawn_table=_dp(table), spawn_scenarios=table.shape[0], spawn_cows=table.shape[1], marl_wrapper=1)
     states = (State * E)()
     L = lib()
     for e in range(E):

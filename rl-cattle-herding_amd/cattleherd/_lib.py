@@ -28,7 +28,7 @@ class ChConfig(ctypes.Structure):
                 ("num_cattle", ctypes.c_int32), ("min_drones", ctypes.c_int32), ("max_drones", ctypes.c_int32),
                 ("curriculum_level", ctypes.c_int32), ("ctrl_freq", ctypes.c_int32), ("pyb_freq", ctypes.c_int32),
                 ("compat", ctypes.c_int32), ("precision", ctypes.c_int32), ("torque_world", ctypes.c_int32),
-                ("gyro", ctypes.c_int32), ("damping", ctypes.c_double), ("seed", ctypes.c_uint64),
+                ("gyro", ctypes.c_int32), ("marl_wrapper", ctypes.c_int32), ("damping", ctypes.c_double), ("seed", ctypes.c_uint64),
                 ("env_id_offset", ctypes.c_int64), ("spawn_table", ctypes.POINTER(ctypes.c_double)),
                 ("spawn_scenarios", ctypes.c_int32), ("spawn_cows", ctypes.c_int32)]
 

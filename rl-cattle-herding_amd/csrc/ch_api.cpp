@@ -111,6 +111,7 @@ static StepParams<R> params(ch_handle* h) {
     p.E = (int)h->E; p.NC = h->NC; p.M = h->M; p.mode = c.mode; p.rows = h->rows;
     p.min_drones = c.min_drones; p.max_drones = c.max_drones; p.ctrl_freq = c.ctrl_freq;
     p.substeps = c.pyb_freq / c.ctrl_freq; p.compat = c.compat; p.torque_world = c.torque_world; p.gyro = c.gyro;
+    p.marl_wrapper = c.marl_wrapper;
     p.episode_len = h->episode_len; p.damping = c.damping;
     p.dt_ctrl = 1.0 / c.ctrl_freq; p.dt = 1.0 / c.pyb_freq;
     p.k0 = (uint32_t)c.seed; p.k1 = (uint32_t)(c.seed >> 32);
@@ -154,6 +155,7 @@ int ch_default_config(ch_config* c, int32_t mode, int32_t num_drones, int32_t nu
     c->precision = CH_PREC_F64;
     c->torque_world = 1;
     c->gyro = 1;
+    c->marl_wrapper = 1;
     c->damping = 0.04;
     c->seed = 0x5EEDull;
     c->env_id_offset = 0;

@@ -20,7 +20,7 @@ constexpr int kMetricRows = CH_METRIC_COUNT + 2;
 template <class R>
 struct StepParams {
     int E, NC, M, mode, rows;
-    int min_drones, max_drones, ctrl_freq, substeps, compat, torque_world, gyro;
+    int min_drones, max_drones, ctrl_freq, substeps, compat, torque_world, gyro, marl_wrapper;
     double episode_len, damping, dt_ctrl, dt;
     uint32_t k0, k1;
     long long env_off, step_index;

@@ -495,19 +495,31 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
                     }
                     return r;
                 };
-                for (int i = 0; i < n; ++i) (void)reward_i(i);
-                for (int i = 0; i < n; ++i) (void)term_call(level, clock, inc, ms, cent, eff);
+                R r1[kNMax];
+                uint8_t d1[kNMax];
+                for (int i = 0; i < n; ++i) r1[i] = reward_i(i);
+                for (int i = 0; i < n; ++i) d1[i] = term_call(level, clock, inc, ms, cent, eff);
                 for (int i = 0; i < p.NC; ++i) { rout[i] = R(NAN); tout[i] = 0; trout[i] = 0; }
-                for (int i = 0; i < n; ++i) {
-                    if (!((active >> i) & 1)) continue;
-                    rout[i] = reward_i(i);
-                    tout[i] = term_call(level, clock, inc, ms, cent, eff);
-                    trout[i] = trunc_i(i);
+                if (p.marl_wrapper) {
+                    for (int i = 0; i < n; ++i) {
+                        if (!((active >> i) & 1)) continue;
+                        rout[i] = reward_i(i);
+                        tout[i] = term_call(level, clock, inc, ms, cent, eff);
+                        trout[i] = trunc_i(i);
+                    }
+                    int live = 0;
+                    for (int i = 0; i < n; ++i)
+                        if (((active >> i) & 1) && tout[i]) active &= ~(1 << i);
+                    for (int i = 0; i < n; ++i) live += (active >> i) & 1;
+                    done = live == 0;
+                } else {
+                    // bare env.step dicts; done = done["__all__"] = all(done.values())
+                    done = 1;
+                    for (int i = 0; i < n; ++i) {
+                        rout[i] = r1[i]; tout[i] = d1[i]; trout[i] = trunc_i(i);
+                        done &= tout[i];
+                    }
                 }
-                int live = 0;
-                for (int i = 0; i < n; ++i)
-                    if (((active >> i) & 1) && tout[i]) active &= ~(1 << i);
-                for (int i = 0; i < n; ++i) live += (active >> i) & 1;
                 for (int i = 0; i < p.NC; ++i) {
                     p.reward[(long long)e * p.NC + i] = (float)rout[i];
                     p.term[(long long)e * p.NC + i] = tout[i];
@@ -516,7 +528,6 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
                     n_term += tout[i]; n_trunc += trout[i];
                     if (i < n && ((active >> i) & 1 || tout[i]) && rout[i] != rout[i]) n_nan += 1;
                 }
-                done = live == 0;
             }
             sc += marl ? 1 : p.substeps;
             // metrics (rank-local accumulators; bench.py all-reduces them)
