@@ -25,7 +25,7 @@ struct Slot {
     float nbr[kNMax][4];
     uint8_t dflags[kNMax];  // bit0 altitude, bit1 collision, bit2 isolated, bit3 NaN distance
     uint8_t herded[TEAM];
-    int done, n, reset;
+    int done, n, reset, spawn, episode;
 };
 
 enum { F_ALT = 1, F_COLL = 2, F_ISO = 4, F_NAN = 8 };
@@ -567,11 +567,11 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
     // ---- auto-reset / reset ------------------------------------------------------------------
     if (do_reset && t == 0) {
         reset_scalars(p, e, n, sc, scA, spawn, episode, active, has_prev, prev, clock);
-        S.n = n;
+        S.n = n; S.spawn = spawn; S.episode = episode;
     }
     __syncthreads();
     if (do_reset) {
-        n = S.n;
+        n = S.n; spawn = S.spawn; episode = S.episode;   // lane 0 drew them; every lane needs them
         reset_env(p, S, e, t, n, spawn, (uint32_t)(episode - 1), &own_z);
         if (t < n) {
             const R qid[4] = {0, 0, 0, 1};
