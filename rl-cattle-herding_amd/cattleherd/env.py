@@ -23,7 +23,8 @@ ENV_INTS = ("n", "step_counter", "step_counter_A", "has_prev", "level", "tally",
 class HerdBatch:
     def __init__(self, n_envs, num_drones, num_cattle, mode="ctde", device=None, compat=True, precision="f64",
                  min_drones=None, max_drones=None, curriculum_level=None, seed=0x5EED, env_id_offset=0,
-                 damping=0.04, torque_world=True, gyro=True, ctrl_freq=60, pyb_freq=240, spawn_table=None):
+                 damping=0.04, torque_world=True, gyro=True, ctrl_freq=60, pyb_freq=240, spawn_table=None,
+                 marl_wrapper=True):
         import torch
         if not torch.cuda.is_available():
             raise RuntimeError("HerdBatch needs a ROCm GPU (torch.cuda.is_available() is False); there is no CPU "
@@ -42,6 +43,7 @@ class HerdBatch:
         cfg.damping = float(damping)
         cfg.torque_world = int(bool(torque_world))
         cfg.gyro = int(bool(gyro))
+        cfg.marl_wrapper = int(bool(marl_wrapper))
         cfg.ctrl_freq = int(ctrl_freq)
         cfg.pyb_freq = int(pyb_freq)
         self._table = None
