@@ -34,6 +34,7 @@ struct ch_handle {
     double* spawn = nullptr;
     int n_scen = 0, n_cows = 0;
     int64_t step_index = 0;
+    double* debug = nullptr;
     std::string err;
 };
 
@@ -118,6 +119,7 @@ static StepParams<R> params(ch_handle* h) {
     p.env_off = c.env_id_offset; p.step_index = h->step_index;
     p.drone = (R*)h->drone; p.cattle = (R*)h->cattle; p.envr = (R*)h->envr; p.envi = h->envi;
     p.metrics = h->metrics; p.spawn = h->spawn; p.n_scen = h->n_scen; p.n_cows = h->n_cows;
+    p.debug = h->debug;
     return p;
 }
 
@@ -406,6 +408,13 @@ int ch_set_state(ch_handle* h, const double* hd, const int32_t* hi, void* stream
         }
     }
     if (hi) HIP_TRY(h, hipMemcpy(h->envi, hi, sizeof(int) * kEnvInt * h->E, hipMemcpyHostToDevice));
+    return CH_OK;
+}
+
+/* Internal, not part of the public ABI: device buffer [E][N][16] receiving per-drone PID intermediates. */
+int ch__set_debug(ch_handle* h, double* dev) {
+    if (!h) return CH_ERR_INVALID;
+    h->debug = dev;
     return CH_OK;
 }
 

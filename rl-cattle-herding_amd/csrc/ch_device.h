@@ -74,15 +74,17 @@ template <class R> __device__ __forceinline__ void quat_to_euler(const R q[4], R
 //      BaseRLAviary.py:185-222).  pid[9] = last_rpy[3], integral_pos_e[3], integral_rpy_e[3].
 template <class R>
 __device__ __forceinline__ void pid_vel(const R pos[3], const R q[4], const R vel[3], const R Rm[9], const R rpy[3],
-                                        const float act[4], R dt, R pid[9], R rpm[4]) {
+                                        const float act[4], R dt, R pid[9], R rpm[4], double* dbg = nullptr) {
     // _preprocessAction VEL branch: the float32 action row keeps the unit vector in float32;
     // SPEED_LIMIT * abs(a[3]) is float32 under NumPy >= 2 (DESIGN.md "Numerics").
     const double speed_limit = 0.3 * kMaxSpeedKmh * (1000.0 / 3600.0);
     float hx = act[0], hy = act[1];
-    float hn = __fsqrt_rn(__fadd_rn(__fmul_rn(hx, hx), __fmul_rn(hy, hy)));
+    // plain sqrtf / '/' lower to the correctly rounded sequences (v_sqrt_f32 + fma refinement,
+    // v_div_scale/fmas/fixup); __fsqrt_rn lowers to the bare 1-ulp v_sqrt_f32 on gfx950
+    float hn = sqrtf(hx * hx + hy * hy);
     float ux = 0.0f, uy = 0.0f;
-    if (hn != 0.0f) { ux = __fdiv_rn(hx, hn); uy = __fdiv_rn(hy, hn); }
-    float sc = __fmul_rn((float)speed_limit, fabsf(act[3]));
+    if (hn != 0.0f) { ux = hx / hn; uy = hy / hn; }
+    float sc = (float)speed_limit * fabsf(act[3]);
     const R tv[3] = {R((double)ux * (double)sc), R((double)uy * (double)sc), R(0.0 * (double)sc)};
     const R tp[3] = {pos[0], pos[1], R(kTargetAlt)};
     const R yaw = rpy[2];
@@ -138,6 +140,14 @@ __device__ __forceinline__ void pid_vel(const R pos[3], const R q[4], const R ve
         R pwm = thrust + (MIX[k][0] * tt[0] + MIX[k][1] * tt[1] + MIX[k][2] * tt[2]);
         pwm = clip(pwm, R(kMinPwm), R(kMaxPwm));
         rpm[k] = R(kPwmScale) * pwm + R(kPwmConst);
+    }
+    if (dbg) {
+        dbg[0] = tv[0]; dbg[1] = tv[1]; dbg[2] = tv[2];
+        dbg[3] = T[0]; dbg[4] = T[1]; dbg[5] = T[2];
+        dbg[6] = rot_e[0]; dbg[7] = rot_e[1]; dbg[8] = rot_e[2];
+        dbg[9] = thrust;
+        dbg[10] = rpm[0]; dbg[11] = rpm[1]; dbg[12] = rpm[2]; dbg[13] = rpm[3];
+        dbg[14] = (double)hn; dbg[15] = (double)sc;
     }
     (void)q;
 }

@@ -42,6 +42,7 @@ struct StepParams {
     uint8_t* reset_happened;
     const uint8_t* reset_mask;
     uint32_t flags;
+    double* debug;  // optional [E][NC][16] per-drone intermediates (diagnostics only)
 };
 
 template <class R> hipError_t launch_step(const StepParams<R>& p, int team, hipStream_t st);

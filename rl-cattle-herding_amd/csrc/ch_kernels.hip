@@ -250,7 +250,7 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
             quat_to_mat(q, Rm);
             quat_to_euler(q, rpy);
             R rpm[4];
-            pid_vel(pos, q, v, Rm, rpy, a, R(p.dt_ctrl), pid, rpm);
+            pid_vel(pos, q, v, Rm, rpy, a, R(p.dt_ctrl), pid, rpm, p.debug ? p.debug + di * 16 : nullptr);
             for (int s = 0; s < p.substeps; ++s)
                 drone_substep(pos, q, v, w, rpm, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0);
             R* D = p.drone;
