@@ -1,0 +1,98 @@
+"""CPU tests of the host-side adapters (drop-in surfaces) over an oracle-backed FakeBatch:
+the reference's RLlib wrapper dicts (marl_wrapper.py:77-119), the Gymnasium CattleAviary
+reset/step contract (sb3_envs/BaseAviary.py:280-465) and the SB3 VecEnv auto-reset info keys."""
+import numpy as np
+import pytest
+
+from fake_batch import FakeBatch
+from helpers import close, load, state_at
+
+
+@pytest.fixture
+def patched(monkeypatch):
+    import importlib
+    ve = importlib.import_module("cattleherd.vec_env")
+    ma = importlib.import_module("gym_pybullet_drones.rllib_envs.MARLCattleAviary")
+    ca = importlib.import_module("gym_pybullet_drones.sb3_envs.CattleAviary")
+    for mod in (ca, ma, ve):
+        monkeypatch.setattr(mod, "HerdBatch", FakeBatch)
+    return ca, ma, ve
+
+
+def test_rllib_wrapper_reproduces_reference_dicts(patched):
+    """Replay the golden RLlib wrapper rollout: same agent ids, rewards, dones, truncs, __all__."""
+    from gym_pybullet_drones.rllib_envs.marl_wrapper import RLlibMultiAgentWrapper
+    d = load("marl_roll_n3_m8_l0.npz")
+    s0 = state_at(d, "state_", 0)
+    n = int(s0["n"])
+    w = RLlibMultiAgentWrapper({"num_drones": n, "num_cattle": int(s0["m"]), "obs": "cokin", "act": "vel",
+                                "gui": False, "record": False, "unknown_key": 1})
+    obs, infos = w.reset()
+    assert sorted(obs) == [f"agent_{i}" for i in range(n)] and all(v == {} for v in infos.values())
+    assert w.get_observation_space("agent_0").shape == (86,) and w.get_action_space("agent_0").shape == (4,)
+    w.env.batch.set_state({k: np.asarray(v)[None] for k, v in s0.items() if k not in ("m", "ctor_level", "episode_len")})
+    for t in range(40):
+        st = state_at(d, "state_", t)
+        o, r, dn, tr, inf = w.step({f"agent_{i}": d["action"][t][i] for i in range(n)})
+        act = [i for i in range(n) if st["active"][i]]
+        assert sorted(o) == [f"agent_{i}" for i in act]
+        for i in act:
+            assert close(o[f"agent_{i}"], d["obs"][t][i], 1e-6, 1e-7)[0]
+            assert close([r[f"agent_{i}"]], [d["reward"][t][i]], 1e-6, 1e-6)[0]  # float32 reward buffer
+            assert dn[f"agent_{i}"] == bool(d["terminated"][t][i]) and tr[f"agent_{i}"] == bool(d["truncated"][t][i])
+        assert dn["__all__"] == bool(d["all_done"][t]) and tr["__all__"] == dn["__all__"]
+
+
+def test_marl_env_bare_dicts(patched):
+    """MARLCattleAviary.step returns the bare env.step dicts keyed by drone index with __all__."""
+    _, ma, _ = patched
+    env = ma.MARLCattleAviary(num_drones=3, num_cattle=8)
+    obs, info = env.reset()
+    assert sorted(obs) == [0, 1, 2] and info == {"__all__": {}}
+    o, r, d, t, i = env.step(np.zeros((3, 4), np.float32))
+    assert set(d) == {0, 1, 2, "__all__"} and set(t) == {0, 1, 2, "__all__"}
+    assert d["__all__"] == all(d[k] for k in range(3))
+
+
+def test_gym_cattle_aviary_contract(patched):
+    """reset → (obs (12,86) float32, {'answer': 42}); step → 5-tuple; 2 drones → NaN reward quirk."""
+    ca, _, _ = patched
+    env = ca.CattleAviary(num_drones=4, num_cattle=16)
+    assert env.EPISODE_LEN_SEC == 80 and env.CTRL_FREQ == 60 and env.action_space.shape == (4, 4)
+    obs, info = env.reset(seed=42, options={})
+    assert obs.shape == (12, 86) and obs.dtype == np.float32 and info == {"answer": 42}
+    assert env.NUM_DRONES == 4
+    o, r, te, tr, inf = env.step(np.zeros((4, 4), np.float32))
+    assert isinstance(r, float) and isinstance(te, bool) and isinstance(tr, bool) and inf == {"answer": 42}
+    env2 = ca.CattleAviary(num_drones=2, num_cattle=8)
+    env2.reset()
+    _, r2, _, _, _ = env2.step(np.zeros((2, 4), np.float32))
+    assert np.isnan(r2)
+
+
+def test_gym_cattle_aviary_unsupported_options(patched):
+    ca, _, _ = patched
+    with pytest.raises(NotImplementedError):
+        ca.CattleAviary(num_drones=4, num_cattle=4, act="rpm")
+    with pytest.raises(ValueError):
+        ca.CattleAviary(num_drones=4, num_cattle=4, pyb_freq=250)
+
+
+def test_vec_env_autoreset_infos(patched):
+    """SB3 VecEnv semantics: done = terminated | truncated, auto-reset inside step, terminal_observation
+    and TimeLimit.truncated in infos."""
+    _, _, ve = patched
+    venv = ve.CattleHerdVecEnv(4, num_drones=4, num_cattle=16)
+    obs = venv.reset()
+    assert obs.shape == (4, 12, 86)
+    rng = np.random.default_rng(0)
+    saw_done = False
+    for _ in range(150):
+        obs, rew, dones, infos = venv.step(rng.uniform(-1, 1, (4, 4, 4)).astype(np.float32))
+        assert obs.shape == (4, 12, 86) and rew.shape == (4,) and dones.shape == (4,)
+        for e in np.nonzero(dones)[0]:
+            saw_done = True
+            assert infos[e]["terminal_observation"].shape == (12, 86)
+            assert "TimeLimit.truncated" in infos[e]
+    assert saw_done
+    assert venv.get_attr("EPISODE_LEN_SEC") == [80] * 4 and venv.env_is_wrapped(object) == [False] * 4
