@@ -35,6 +35,7 @@ struct ch_handle {
     int n_scen = 0, n_cows = 0;
     int64_t step_index = 0;
     double* debug = nullptr;
+    int phase_mask = 0;
     std::string err;
 };
 
@@ -120,6 +121,7 @@ static StepParams<R> params(ch_handle* h) {
     p.drone = (R*)h->drone; p.cattle = (R*)h->cattle; p.envr = (R*)h->envr; p.envi = h->envi;
     p.metrics = h->metrics; p.spawn = h->spawn; p.n_scen = h->n_scen; p.n_cows = h->n_cows;
     p.debug = h->debug;
+    p.phase_mask = h->phase_mask;
     return p;
 }
 
@@ -415,6 +417,13 @@ int ch_set_state(ch_handle* h, const double* hd, const int32_t* hi, void* stream
 int ch__set_debug(ch_handle* h, double* dev) {
     if (!h) return CH_ERR_INVALID;
     h->debug = dev;
+    return CH_OK;
+}
+
+/* Internal diagnostics: skip kernel phases (1 drones, 2 flock, 4 task, 8 obs) to attribute time. */
+int ch__set_phase_mask(ch_handle* h, int32_t mask) {
+    if (!h) return CH_ERR_INVALID;
+    h->phase_mask = mask;
     return CH_OK;
 }
 

@@ -43,6 +43,7 @@ struct StepParams {
     const uint8_t* reset_mask;
     uint32_t flags;
     double* debug;  // optional [E][NC][16] per-drone intermediates (diagnostics only)
+    int phase_mask; // diagnostics only: skip phases (1 drones, 2 flock, 4 task, 8 obs) for time attribution
 };
 
 template <class R> hipError_t launch_step(const StepParams<R>& p, int team, hipStream_t st);

@@ -250,9 +250,11 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
             quat_to_mat(q, Rm);
             quat_to_euler(q, rpy);
             R rpm[4];
-            pid_vel(pos, q, v, Rm, rpy, a, R(p.dt_ctrl), pid, rpm, p.debug ? p.debug + di * 16 : nullptr);
-            for (int s = 0; s < p.substeps; ++s)
-                drone_substep(pos, q, v, w, rpm, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0);
+            if (!(p.phase_mask & 1)) {
+                pid_vel(pos, q, v, Rm, rpy, a, R(p.dt_ctrl), pid, rpm, p.debug ? p.debug + di * 16 : nullptr);
+                for (int s = 0; s < p.substeps; ++s)
+                    drone_substep(pos, q, v, w, rpm, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0);
+            }
             R* D = p.drone;
             D[0 * DS + di] = pos[0]; D[1 * DS + di] = pos[1]; D[2 * DS + di] = pos[2];
             D[3 * DS + di] = q[0]; D[4 * DS + di] = q[1]; D[5 * DS + di] = q[2]; D[6 * DS + di] = q[3];
@@ -280,7 +282,7 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
         __syncthreads();
 
         // ---- phase 2: flocking every second step (BaseAviary.py:454-455, 1352-1400) -------------
-        const bool flock = (scA % 2) == 0;
+        const bool flock = (scA % 2) == 0 && !(p.phase_mask & 2);
         if (valid && flock && t < p.M) {
             const R C2A = R(2 * 1.7320508075688772), C2B = R(2 * 4.47213595499958), C1G = R(5),
                     C2G = R(0.2 * 2.23606797749979);
@@ -337,7 +339,8 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
         if (valid && flock && t < p.M) { S.cvx[t] = cvx; S.cvy[t] = cvy; }
 
         // ---- phase 3: per-drone reward terms (lane i) and per-cow herded flags (lane j) -----------
-        if (valid && t < n) {
+        const bool task = !(p.phase_mask & 4);
+        if (valid && task && t < n) {
             const int i = t;
             R m1 = R(INFINITY), m2 = R(INFINITY);
             uint8_t fl = 0;
@@ -364,7 +367,7 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
             S.scat[i] = cattle_spacing(best);
             neighbour_obs(S, i, n);
         }
-        if (valid && t < p.M) {
+        if (valid && task && t < p.M) {
             // evaluate_herding_effectiveness (evaluation.py:100-138)
             R px = S.cx[t], py = S.cy[t];
             int wn = 0;
@@ -380,7 +383,7 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
         __syncthreads();
 
         // ---- phase 4: order-dependent task bookkeeping on lane 0 ----------------------------------
-        if (valid && t == 0) {
+        if (valid && task && t == 0) {
             R scx = 0, scy = 0, sdx = 0, sdy = 0;
             int herded = 0;
             for (int j = 0; j < p.M; ++j) { scx += S.cx[j]; scy += S.cy[j]; herded += S.herded[j]; }
@@ -592,7 +595,7 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
     __syncthreads();
 
     // ---- observation + scalars back to HBM --------------------------------------------------
-    const bool write = valid && (!RESET_ONLY || do_reset);
+    const bool write = valid && (!RESET_ONLY || do_reset) && !(p.phase_mask & 8);
     if (write) write_obs(p.obs + (long long)e * p.rows * 86, p.rows, S, t, m_obs, cat_off);
     if (write && t == 0) {
         p.envi[0 * E + e] = n; p.envi[1 * E + e] = sc; p.envi[2 * E + e] = scA; p.envi[3 * E + e] = has_prev;

@@ -1,0 +1,42 @@
+"""Diagnostics: per-launch kernel time of the fused step with phases disabled (time attribution)."""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "rl-cattle-herding_amd"))
+import torch  # noqa: E402
+from cattleherd import _lib  # noqa: E402
+from cattleherd.env import HerdBatch  # noqa: E402
+
+
+def time_launches(b, k=200):
+    for _ in range(20):
+        b.step(random_actions=True, autoreset=True, terminal_obs=False)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(k):
+        b.step(random_actions=True, autoreset=True, terminal_obs=False)
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / k * 1000.0
+
+
+def main():
+    configs = [("ctde", 4096, 4, 16), ("ctde", 4096, 2, 8), ("marl", 4096, 4, 32)]
+    masks = [(0, "full"), (1, "-drones"), (2, "-flock"), (4, "-task"), (8, "-obs"), (1 | 2 | 4 | 8, "loads/stores only")]
+    for prec in ("f64", "f32"):
+        for mode, E, n, m in configs:
+            b = HerdBatch(E, n, m, mode=mode, precision=prec)
+            b.reset()
+            row = []
+            for mask, name in masks:
+                _lib.lib().ch__set_phase_mask(b.handle, mask)
+                row.append(f"{name}={time_launches(b):.1f}us")
+            print(prec, mode, E, n, m, " ".join(row), flush=True)
+            b.close()
+
+
+if __name__ == "__main__":
+    main()
