@@ -253,6 +253,21 @@ __device__ __forceinline__ void pair_terms(R qix, R qiy, R pix, R piy, R qjx, R 
     cy += b * (pjy - piy);
 }
 
+// same as pair_terms with the neighbour offset z = qj - qi and its norm already at hand
+template <class R>
+__device__ __forceinline__ void pair_terms_n(R n, R zx, R zy, R pix, R piy, R pjx, R pjy, R ra, R da, R& gx, R& gy,
+                                             R& cx, R& cy) {
+    R den = sqrt(R(1) + R(kEps) * (n * n));
+    R sn = (den - R(1)) / R(kEps);
+    R b = bump(sn / ra);
+    R zz = sn - da;
+    R ph = b * ((R(5.0 + 5.0) * sigma_1(zz + R(0.0)) + R(5.0 - 5.0)) / R(2));
+    gx += ph * (zx / den);
+    gy += ph * (zy / den);
+    cx += b * (pjx - pix);
+    cy += b * (pjy - piy);
+}
+
 // ---- spacing rewards: CattleAviary.py:572-679 -------------------------------------------------
 template <class R> __device__ __forceinline__ R simple_spacing(R r, const Level& L) {
     R desired = R(L.desired), tol = desired * R(L.tol);

@@ -34,10 +34,9 @@ template <class R>
 __device__ __forceinline__ R ld(const R* base, int comp, long long stride, long long idx) { return base[comp * stride + idx]; }
 
 // observation element f of an env block (BaseRLAviary.py:272-342 / BaseMARLAviary.py:253-303)
+// observation element (row, col) of an env block (BaseRLAviary.py:272-342 / BaseMARLAviary.py:253-303)
 template <class R, int TEAM>
-__device__ __forceinline__ float obs_val(const Slot<R, TEAM>& S, int f, int n, int m_obs, int cat_off) {
-    int row = f / 86;
-    int col = f - row * 86;
+__device__ __forceinline__ float obs_val(const Slot<R, TEAM>& S, int row, int col, int n, int m_obs, int cat_off) {
     if (row >= n) return 0.0f;
     if (col < 10) return S.own[row][col];
     if (col < 14) return S.nbr[row][col - 10];
@@ -47,24 +46,31 @@ __device__ __forceinline__ float obs_val(const Slot<R, TEAM>& S, int f, int n, i
     return (col & 1) ? (float)(S.cy[k] - S.dy[row]) : (float)(S.cx[k] - S.dx[row]);
 }
 
+// the env's [rows][86] block with 16-byte (or 8-byte) coalesced stores; (row, col) advance
+// incrementally so no division sits in the loop
+template <int W, class R, int TEAM>
+__device__ __forceinline__ void write_obs_w(float* out, int rows, const Slot<R, TEAM>& S, int t, int m_obs, int cat_off) {
+    const int n = S.n, F = rows * 86;
+    int f0 = t * W, row = f0 / 86, col = f0 - row * 86;
+    for (int q = t; q < F / W; q += TEAM) {
+        float v[W];
+        int r = row, c = col;
+#pragma unroll
+        for (int u = 0; u < W; ++u) {
+            v[u] = obs_val(S, r, c, n, m_obs, cat_off);
+            if (++c == 86) { c = 0; ++r; }
+        }
+        if constexpr (W == 4) reinterpret_cast<float4*>(out)[q] = make_float4(v[0], v[1], v[2], v[3]);
+        else reinterpret_cast<float2*>(out)[q] = make_float2(v[0], v[1]);
+        col += W * TEAM;
+        while (col >= 86) { col -= 86; ++row; }
+    }
+}
+
 template <class R, int TEAM>
 __device__ __forceinline__ void write_obs(float* out, int rows, const Slot<R, TEAM>& S, int t, int m_obs, int cat_off) {
-    const int F = rows * 86;
-    const int n = S.n;
-    if ((F & 3) == 0) {
-        float4* o4 = reinterpret_cast<float4*>(out);
-        for (int q = t; q < (F >> 2); q += TEAM) {
-            int f = q << 2;
-            o4[q] = make_float4(obs_val(S, f, n, m_obs, cat_off), obs_val(S, f + 1, n, m_obs, cat_off),
-                                obs_val(S, f + 2, n, m_obs, cat_off), obs_val(S, f + 3, n, m_obs, cat_off));
-        }
-    } else {
-        float2* o2 = reinterpret_cast<float2*>(out);
-        for (int q = t; q < (F >> 1); q += TEAM) {
-            int f = q << 1;
-            o2[q] = make_float2(obs_val(S, f, n, m_obs, cat_off), obs_val(S, f + 1, n, m_obs, cat_off));
-        }
-    }
+    if (((rows * 86) & 3) == 0) write_obs_w<4>(out, rows, S, t, m_obs, cat_off);
+    else write_obs_w<2>(out, rows, S, t, m_obs, cat_off);
 }
 
 // own-state block and nearest-two neighbour block of drone i (needs S.dx/S.dy of all drones)
@@ -215,6 +221,12 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
         prev = p.envr[0 * E + e]; clock = p.envr[1 * E + e];
     }
     if (t == 0) { S.done = 0; S.reset = 0; S.n = n; }
+    // metric accumulators are fetched now so their latency hides behind the physics
+    double mt[kMetricRows];
+    if (!RESET_ONLY && valid && t == 0) {
+#pragma unroll
+        for (int r = 0; r < kMetricRows; ++r) mt[r] = p.metrics[r * E + e];
+    }
 
     R own_z = 0;
     R rpy[3] = {0, 0, 0}, dv[3] = {0, 0, 0}, dw[3] = {0, 0, 0};
@@ -290,40 +302,45 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
             const R qix = S.cx[t], qiy = S.cy[t], pix = cvx, piy = cvy;
             R ux = 0, uy = 0, gx = 0, gy = 0, cxx = 0, cyy = 0;
             int nb = 0;
+            // alpha term over the herd (flockUtils.py:237-258); |qj - qi| of the adjacency test is the
+            // same number the gradient term needs, so it is computed once
+#pragma unroll 4
             for (int j = 0; j < p.M; ++j) {
                 if (j == t) continue;
-                if (!(norm2(qix - S.cx[j], qiy - S.cy[j]) <= R(999))) continue;
+                const R zx = S.cx[j] - qix, zy = S.cy[j] - qiy;
+                const R nrm = sqrt(zx * zx + zy * zy);
+                if (!(nrm <= R(999))) continue;
                 ++nb;
-                pair_terms(qix, qiy, pix, piy, S.cx[j], S.cy[j], S.cvx[j], S.cvy[j], ra_a, da_a, gx, gy, cxx, cyy);
+                pair_terms_n(nrm, zx, zy, pix, piy, S.cvx[j], S.cvy[j], ra_a, da_a, gx, gy, cxx, cyy);
             }
             if (nb > 0) { ux = C2A * gx + C2A * cxx; uy = C2A * gy + C2A * cyy; }
-            R ddx = 0, ddy = 0;
+            // delta (shepherd) term (271-317) and predator avoidance (343-348) share |y_k - q_i|
+            R ddx = 0, ddy = 0, sx = 0, sy = 0;
             gx = gy = cxx = cyy = 0;
             nb = 0;
+#pragma unroll 4
             for (int k = 0; k < n; ++k) {
-                R yx = S.dx[k], yy = S.dy[k];
-                if (!(norm2(yx - qix, yy - qiy) <= R(999 + 2))) continue;
-                ++nb;
-                R difx = qix - yx, dify = qiy - yy;
-                R d = norm2(difx, dify) + R(1e-6);
-                R mu = d / R(1.0) < R(1.0) ? d / R(1.0) : R(1.0);
-                R akx = difx / d, aky = dify / d;
-                R P00 = R(1) - akx * akx, P01 = R(0) - akx * aky, P10 = R(0) - aky * akx, P11 = R(1) - aky * aky;
-                R qkx = mu * qix + (R(1) - mu) * yx, qky = mu * qiy + (R(1) - mu) * yy;
-                R pkx = mu * (P00 * pix + P01 * piy), pky = mu * (P10 * pix + P11 * piy);
-                pair_terms(qix, qiy, pix, piy, qkx, qky, pkx, pky, ra_b, da_b, gx, gy, cxx, cyy);
-            }
-            if (nb > 0) { ddx = C2B * gx + C2B * cxx; ddy = C2B * gy + C2B * cyy; }
-            R sx = 0, sy = 0;
-            for (int k = 0; k < n; ++k) {
-                R ex = S.dx[k] - qix, ey = S.dy[k] - qiy;
-                R dn = norm2(ex, ey);
+                const R yx = S.dx[k], yy = S.dy[k];
+                const R ex = yx - qix, ey = yy - qiy;
+                const R dn = sqrt(ex * ex + ey * ey);
+                if (dn <= R(999 + 2)) {
+                    ++nb;
+                    R difx = qix - yx, dify = qiy - yy;
+                    R d = dn + R(1e-6);
+                    R mu = d / R(1.0) < R(1.0) ? d / R(1.0) : R(1.0);
+                    R akx = difx / d, aky = dify / d;
+                    R P00 = R(1) - akx * akx, P01 = R(0) - akx * aky, P10 = R(0) - aky * akx, P11 = R(1) - aky * aky;
+                    R qkx = mu * qix + (R(1) - mu) * yx, qky = mu * qiy + (R(1) - mu) * yy;
+                    R pkx = mu * (P00 * pix + P01 * piy), pky = mu * (P10 * pix + P11 * piy);
+                    pair_terms(qix, qiy, pix, piy, qkx, qky, pkx, pky, ra_b, da_b, gx, gy, cxx, cyy);
+                }
                 if (dn <= R(1.1)) {
                     R d3 = pow(dn, R(3.0));
                     sx += R(-650000.0) * ex / d3;
                     sy += R(-650000.0) * ey / d3;
                 }
             }
+            if (nb > 0) { ddx = C2B * gx + C2B * cxx; ddy = C2B * gy + C2B * cyy; }
             ddx += sx; ddy += sy;
             R gmx = -C1G * sigma_1(qix - R(1)) - C2G * pix, gmy = -C1G * sigma_1(qiy - R(1)) - C2G * piy;
             R qx = (ux + ddx) + gmx, qy = (uy + ddy) + gmy;
@@ -345,6 +362,7 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
             R m1 = R(INFINITY), m2 = R(INFINITY);
             uint8_t fl = 0;
             bool iso = true;
+#pragma unroll 4
             for (int j = 0; j < n; ++j) {
                 if (j == i) continue;
                 R d = norm2(S.dx[j] - S.dx[i], S.dy[j] - S.dy[i]);
@@ -356,6 +374,7 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
             if (iso) fl |= F_ISO;
             if (fabs(own_z - R(kTargetAlt)) > R(kTargetAlt * 0.6)) fl |= F_ALT;
             R best = R(INFINITY);
+#pragma unroll 4
             for (int j = 0; j < p.M; ++j) {
                 R d = norm2(S.cx[j] - S.dx[i], S.cy[j] - S.dy[i]);
                 if (d < best) best = d;
@@ -386,7 +405,9 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
         if (valid && task && t == 0) {
             R scx = 0, scy = 0, sdx = 0, sdy = 0;
             int herded = 0;
+#pragma unroll 8
             for (int j = 0; j < p.M; ++j) { scx += S.cx[j]; scy += S.cy[j]; herded += S.herded[j]; }
+#pragma unroll 4
             for (int i = 0; i < n; ++i) { sdx += S.dx[i]; sdy += S.dy[i]; }
             scx /= R(p.M); scy /= R(p.M); sdx /= R(n); sdy /= R(n);
             R ex = sdx - scx, ey = sdy - scy;
@@ -534,21 +555,22 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
             }
             sc += marl ? 1 : p.substeps;
             // metrics (rank-local accumulators; bench.py all-reduces them)
-            double* MT = p.metrics;
-            MT[CH_METRIC_STEPS * E + e] += 1;
-            MT[CH_METRIC_TERMINATED * E + e] += n_term;
-            MT[CH_METRIC_TRUNCATED * E + e] += n_trunc;
-            MT[CH_METRIC_NAN_REWARDS * E + e] += n_nan;
-            MT[CH_METRIC_EFFECTIVENESS_SUM * E + e] += (double)eff;
-            MT[kMetricCurReturn * E + e] += ret;
-            MT[kMetricCurLen * E + e] += 1;
+            mt[CH_METRIC_STEPS] += 1;
+            mt[CH_METRIC_TERMINATED] += n_term;
+            mt[CH_METRIC_TRUNCATED] += n_trunc;
+            mt[CH_METRIC_NAN_REWARDS] += n_nan;
+            mt[CH_METRIC_EFFECTIVENESS_SUM] += (double)eff;
+            mt[kMetricCurReturn] += ret;
+            mt[kMetricCurLen] += 1;
             if (done) {
-                MT[CH_METRIC_EPISODES * E + e] += 1;
-                MT[CH_METRIC_RETURN_SUM * E + e] += MT[kMetricCurReturn * E + e];
-                MT[CH_METRIC_LENGTH_SUM * E + e] += MT[kMetricCurLen * E + e];
-                MT[kMetricCurReturn * E + e] = 0;
-                MT[kMetricCurLen * E + e] = 0;
+                mt[CH_METRIC_EPISODES] += 1;
+                mt[CH_METRIC_RETURN_SUM] += mt[kMetricCurReturn];
+                mt[CH_METRIC_LENGTH_SUM] += mt[kMetricCurLen];
+                mt[kMetricCurReturn] = 0;
+                mt[kMetricCurLen] = 0;
             }
+#pragma unroll
+            for (int r = 0; r < kMetricRows; ++r) p.metrics[r * E + e] = mt[r];
             S.done = done;
             S.reset = done && (p.flags & CH_STEP_AUTORESET);
         }
