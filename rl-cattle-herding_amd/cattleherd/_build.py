@@ -30,25 +30,26 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=False):
-    if not force and not _stale():
+def build(force=False, verbose=False, extra_flags=(), out=None):
+    lib_out = out or LIB
+    if not force and out is None and not _stale():
         return LIB
     os.makedirs(BUILD, exist_ok=True)
     objs = []
     for src in SOURCES:
-        obj = os.path.join(BUILD, src + ".o")
-        cmd = [HIPCC, *FLAGS, "-c", os.path.join(CSRC, src), "-o", obj]
+        obj = os.path.join(BUILD, src + ("".join(extra_flags).replace("-", "_") if extra_flags else "") + ".o")
+        cmd = [HIPCC, *FLAGS, *extra_flags, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
         objs.append(obj)
-    tmp = LIB + ".tmp"
+    tmp = lib_out + ".tmp"
     cmd = [HIPCC, *FLAGS, "-shared", *objs, "-o", tmp]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib_out)
+    return lib_out
 
 
 if __name__ == "__main__":

@@ -7,7 +7,7 @@ import ctypes
 import os
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "libcattleherd.so")
+LIB_PATH = os.environ.get("CH_LIB_PATH") or os.path.join(_PKG, "libcattleherd.so")  # override: A/B diagnostics
 
 CH_OK, CH_ERR_INVALID, CH_ERR_DEVICE, CH_ERR_NOMEM, CH_ERR_UNSUPPORTED = 0, -1, -2, -3, -4
 CH_MODE_CTDE, CH_MODE_MARL = 0, 1

@@ -40,6 +40,21 @@ __constant__ static const Level kLevels[8] = {
     {0.8, 0.3, 15, 0.2, 50, 0.0, 0.0, 4, 12, 80, 0.0, 0.0, -0.0, 1, 1, 0.0, 600},
 };
 
+// Heavy libm entry points go through one out-of-line copy each (CH_NOINLINE_MATH) instead of being
+// inlined at every call site: the fused step kernel is otherwise ~11k instructions and thrashes the
+// shared instruction cache.
+#ifdef CH_NOINLINE_MATH
+#define CH_MATH_ATTR __device__ __noinline__
+#else
+#define CH_MATH_ATTR __device__ __forceinline__
+#endif
+template <class R> CH_MATH_ATTR R m_atan2(R y, R x) { return atan2(y, x); }
+template <class R> CH_MATH_ATTR R m_asin(R x) { return asin(x); }
+template <class R> CH_MATH_ATTR R m_exp(R x) { return exp(x); }
+template <class R> CH_MATH_ATTR R m_cos(R x) { return cos(x); }
+template <class R> CH_MATH_ATTR R m_sin(R x) { return sin(x); }
+template <class R> CH_MATH_ATTR R m_pow(R x, R y) { return pow(x, y); }
+
 template <class R> __device__ __forceinline__ R clip(R x, R lo, R hi) { return x < lo ? lo : (x > hi ? hi : x); }
 template <class R> __device__ __forceinline__ R norm2(R x, R y) { return sqrt(x * x + y * y); }
 
@@ -60,13 +75,13 @@ template <class R> __device__ __forceinline__ void quat_to_euler(const R q[4], R
     R sqx = x * x, sqy = y * y, sqz = z * z, squ = w * w;
     R sarg = R(-2.0) * (x * z - w * y);
     if (sarg <= R(-0.99999)) {
-        rpy[0] = 0; rpy[1] = R(-0.5 * kPi); rpy[2] = R(2) * atan2(x, -y);
+        rpy[0] = 0; rpy[1] = R(-0.5 * kPi); rpy[2] = R(2) * m_atan2(x, -y);
     } else if (sarg >= R(0.99999)) {
-        rpy[0] = 0; rpy[1] = R(0.5 * kPi); rpy[2] = R(2) * atan2(-x, y);
+        rpy[0] = 0; rpy[1] = R(0.5 * kPi); rpy[2] = R(2) * m_atan2(-x, y);
     } else {
-        rpy[0] = atan2(R(2) * (y * z + w * x), squ - sqx - sqy + sqz);
-        rpy[1] = asin(sarg);
-        rpy[2] = atan2(R(2) * (x * y + w * z), squ + sqx - sqy - sqz);
+        rpy[0] = m_atan2(R(2) * (y * z + w * x), squ - sqx - sqy + sqz);
+        rpy[1] = m_asin(sarg);
+        rpy[2] = m_atan2(R(2) * (x * y + w * z), squ + sqx - sqy - sqz);
     }
 }
 
@@ -106,7 +121,7 @@ __device__ __forceinline__ void pid_vel(const R pos[3], const R q[4], const R ve
     R thrust = (sqrt(scalar / (R(4) * R(kKF))) - R(kPwmConst)) / R(kPwmScale);
     R tn = sqrt(T[0] * T[0] + T[1] * T[1] + T[2] * T[2]);
     R z[3] = {T[0] / tn, T[1] / tn, T[2] / tn};
-    R xc[3] = {cos(yaw), sin(yaw), R(0)};
+    R xc[3] = {m_cos(yaw), m_sin(yaw), R(0)};
     R yt[3] = {z[1] * xc[2] - z[2] * xc[1], z[2] * xc[0] - z[0] * xc[2], z[0] * xc[1] - z[1] * xc[0]};
     R yn = sqrt(yt[0] * yt[0] + yt[1] * yt[1] + yt[2] * yt[2]);
     R y[3] = {yt[0] / yn, yt[1] / yn, yt[2] / yn};
@@ -213,8 +228,8 @@ __device__ __forceinline__ void drone_substep(R p[3], R q[4], R v[3], R w[3], co
     if (fang * dt > R(0.5 * (0.5 * kPi))) fang = R(0.5 * (0.5 * kPi)) / dt;
     R s;
     if (fang < R(0.001)) s = R(0.5) * dt - (dt * dt * dt) * R(0.020833333333) * fang * fang;
-    else s = sin(R(0.5) * fang * dt) / fang;
-    R a[4] = {w[0] * s, w[1] * s, w[2] * s, cos(fang * dt * R(0.5))};
+    else s = m_sin(R(0.5) * fang * dt) / fang;
+    R a[4] = {w[0] * s, w[1] * s, w[2] * s, m_cos(fang * dt * R(0.5))};
     R o[4] = {a[3] * q[0] + a[0] * q[3] + a[1] * q[2] - a[2] * q[1],
               a[3] * q[1] + a[1] * q[3] + a[2] * q[0] - a[0] * q[2],
               a[3] * q[2] + a[2] * q[3] + a[0] * q[1] - a[1] * q[0],
@@ -230,7 +245,7 @@ template <class R> __device__ __forceinline__ R sigma_norm_n(R n) { return (sqrt
 template <class R> __device__ __forceinline__ R bump(R z) {
     if (z < R(0)) return R(0);
     if (z < R(kH)) return R(1);
-    if (z <= R(1)) return (R(1) + cos(R(kPi) * (z - R(kH)) / (R(1) - R(kH)))) / R(2);
+    if (z <= R(1)) return (R(1) + m_cos(R(kPi) * (z - R(kH)) / (R(1) - R(kH)))) / R(2);
     return R(0);
 }
 template <class R> __device__ __forceinline__ R sigma_1(R z) { return z / sqrt(R(1) + z * z); }
@@ -280,7 +295,7 @@ template <class R> __device__ __forceinline__ R simple_spacing(R r, const Level&
 template <class R> __device__ __forceinline__ R complex_spacing(R r, const Level& L) {
     R ds = R(L.desired);
     R t = (r - ds) / R(0.4 + 1e-9);
-    R gauss = exp(R(-0.5) * (t * t));
+    R gauss = m_exp(R(-0.5) * (t * t));
     R coll = r < R(0.3) ? R(-1.0) * (R(1.0) - (r / R(0.3 + 1e-9))) : R(0.0);
     R pull = r > R(1.5) ? R(-0.3) * (r - R(1.5)) / R(5.0 - 1.5) : R(0.0);
     R rew = gauss + coll + pull;
@@ -290,10 +305,10 @@ template <class R> __device__ __forceinline__ R complex_spacing(R r, const Level
 template <class R> __device__ __forceinline__ R cattle_spacing(R r) {
     const double A = 1.2, B = 2.1, C = 3.3, K = 0.2, D = -1, R0 = 1.3, LAM = 0.8;
     if (r <= R(R0))
-        return R(A) * exp(-((r - R(D)) * (r - R(D))) / R(2 * (C * C))) - R(B) * exp(-(r * r) / R(2 * (K * K)));
-    R fr0 = R(A) * exp(-(R(R0 - D) * R(R0 - D)) / R(2 * (C * C))) - R(B) * exp(-(R(R0) * R(R0)) / R(2 * (K * K)));
-    R Cc = fr0 / exp(R(-LAM) * R(R0));
-    return Cc * exp(R(-LAM) * r);
+        return R(A) * m_exp(-((r - R(D)) * (r - R(D))) / R(2 * (C * C))) - R(B) * m_exp(-(r * r) / R(2 * (K * K)));
+    R fr0 = R(A) * m_exp(-(R(R0 - D) * R(R0 - D)) / R(2 * (C * C))) - R(B) * m_exp(-(R(R0) * R(R0)) / R(2 * (K * K)));
+    R Cc = fr0 / m_exp(R(-LAM) * R(R0));
+    return Cc * m_exp(R(-LAM) * r);
 }
 
 // ---- Philox4x32-10 (Random123) ------------------------------------------------------------------

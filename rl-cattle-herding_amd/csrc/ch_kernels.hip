@@ -169,7 +169,7 @@ __device__ __forceinline__ void reset_env(const StepParams<R>& p, Slot<R, TEAM>&
         R x = R(tab[0]), y = R(tab[1]);
         double u = philox_uniform53(p.k0, p.k1, episode, 1 + t, (uint32_t)env_id);
         double ang = kPi * (2 * u - 1);
-        R vx = R(kMaxVelCattle * cos(ang)), vy = R(kMaxVelCattle * sin(ang));
+        R vx = R(kMaxVelCattle * m_cos(ang)), vy = R(kMaxVelCattle * m_sin(ang));
         const long long ci = (long long)e * p.M + t;
         p.cattle[0 * CS + ci] = x; p.cattle[1 * CS + ci] = y; p.cattle[2 * CS + ci] = vx; p.cattle[3 * CS + ci] = vy;
         S.cx[t] = x; S.cy[t] = y; S.cvx[t] = vx; S.cvy[t] = vy;
@@ -197,7 +197,7 @@ __device__ __forceinline__ void reset_scalars(const StepParams<R>& p, int e, int
     episode += 1;
 }
 
-template <class R, int TEAM, bool RESET_ONLY>
+template <class R, int TEAM, bool RESET_ONLY, int MODE>
 __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
     constexpr int EPB = 64 / TEAM;
     __shared__ Slot<R, TEAM> slots[EPB];
@@ -207,7 +207,7 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
     Slot<R, TEAM>& S = slots[slot];
     const long long E = p.E;
     const long long DS = E * p.NC, CS = E * p.M;
-    const bool marl = p.mode == 1;
+    constexpr bool marl = MODE == 1;   // CTDE and MARL are separate instantiations (smaller code)
     const int m_obs = p.M < 16 ? p.M : 16;
     const int cat_off = marl ? 18 : 34;
 
@@ -304,7 +304,6 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
             int nb = 0;
             // alpha term over the herd (flockUtils.py:237-258); |qj - qi| of the adjacency test is the
             // same number the gradient term needs, so it is computed once
-#pragma unroll 4
             for (int j = 0; j < p.M; ++j) {
                 if (j == t) continue;
                 const R zx = S.cx[j] - qix, zy = S.cy[j] - qiy;
@@ -318,7 +317,6 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
             R ddx = 0, ddy = 0, sx = 0, sy = 0;
             gx = gy = cxx = cyy = 0;
             nb = 0;
-#pragma unroll 4
             for (int k = 0; k < n; ++k) {
                 const R yx = S.dx[k], yy = S.dy[k];
                 const R ex = yx - qix, ey = yy - qiy;
@@ -335,7 +333,7 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
                     pair_terms(qix, qiy, pix, piy, qkx, qky, pkx, pky, ra_b, da_b, gx, gy, cxx, cyy);
                 }
                 if (dn <= R(1.1)) {
-                    R d3 = pow(dn, R(3.0));
+                    R d3 = m_pow(dn, R(3.0));
                     sx += R(-650000.0) * ex / d3;
                     sy += R(-650000.0) * ey / d3;
                 }
@@ -427,7 +425,7 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
             int done = 0;
             double ret = 0;
             int n_term = 0, n_trunc = 0, n_nan = 0;
-            if (!marl) {
+            if constexpr (!marl) {
                 // CattleAviary._computeReward (CattleAviary.py:213-332)
                 const Level& L = kLevels[level];
                 R sp_simple = 0, sp_complex = 0, per_sp[kNMax], msp = 0, mcat = 0, cat = 0;
@@ -630,15 +628,21 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
 // ---------------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------------
-template <class R, bool RESET_ONLY>
-static hipError_t launch_team(const StepParams<R>& p, int team, hipStream_t st) {
+template <class R, bool RESET_ONLY, int MODE>
+static void launch_mode(const StepParams<R>& p, int team, hipStream_t st) {
     int epb = 64 / team;
     dim3 grid((p.E + epb - 1) / epb), block(64);
     switch (team) {
-        case 16: hipLaunchKernelGGL((k_env<R, 16, RESET_ONLY>), grid, block, 0, st, p); break;
-        case 32: hipLaunchKernelGGL((k_env<R, 32, RESET_ONLY>), grid, block, 0, st, p); break;
-        default: hipLaunchKernelGGL((k_env<R, 64, RESET_ONLY>), grid, block, 0, st, p); break;
+        case 16: hipLaunchKernelGGL((k_env<R, 16, RESET_ONLY, MODE>), grid, block, 0, st, p); break;
+        case 32: hipLaunchKernelGGL((k_env<R, 32, RESET_ONLY, MODE>), grid, block, 0, st, p); break;
+        default: hipLaunchKernelGGL((k_env<R, 64, RESET_ONLY, MODE>), grid, block, 0, st, p); break;
     }
+}
+
+template <class R, bool RESET_ONLY>
+static hipError_t launch_team(const StepParams<R>& p, int team, hipStream_t st) {
+    if (p.mode == 1) launch_mode<R, RESET_ONLY, 1>(p, team, st);
+    else launch_mode<R, RESET_ONLY, 0>(p, team, st);
     return hipGetLastError();
 }
 
