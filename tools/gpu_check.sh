@@ -17,7 +17,7 @@ step() {  # name timeout cmd...
 }
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
-  step pytest_gpu ${TEST_TIMEOUT:-900} python -m pytest tests -m gpu -q -rf ${PYTEST_ARGS:-}
+  step pytest_gpu ${TEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -v -rf --timeout 300 --timeout-method thread ${PYTEST_ARGS:-}
   rc=$?
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 fi
