@@ -74,46 +74,35 @@ def main():
     args = ap.parse_args()
 
     import torch
-    import torch.distributed as dist
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from cattleherd import distributed as D
+    from cattleherd.env import HerdBatch
+    rank, world, local = D.world_info()
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        D.init("nccl")          # RCCL over xGMI; one process per GPU
     else:
         torch.cuda.set_device(0)
-    from cattleherd.env import HerdBatch
 
     mode, E, n, m, desc = WORKLOADS[args.workload]
     if args.envs:
         E = args.envs
-    b = HerdBatch(E, n, m, mode=mode, precision=args.precision, env_id_offset=rank * E)
+    b = HerdBatch(E, n, m, mode=mode, precision=args.precision, env_id_offset=D.env_offset(rank, E))
     b.reset()
     stream = torch.cuda.current_stream()
     for _ in range(args.warmup):
         b.step(random_actions=True, autoreset=True, terminal_obs=False)
     b.metrics(reset=True)
 
-    def barrier():
-        if world > 1:
-            dist.barrier()
-
-    barrier()
+    D.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         b.step(random_actions=True, autoreset=True, terminal_obs=False)
-    met = torch.tensor(b.metrics(reset=True), dtype=torch.float64, device=b.device)  # end-of-rollout metrics
-    if world > 1:
-        dist.all_reduce(met)   # RCCL over xGMI: the only collective of the rollout
+    # end-of-rollout metrics: RCCL all-reduce over xGMI, the only collective of the rollout
+    mv, _ = D.reduce_rollout(torch.tensor(b.metrics(reset=True), dtype=torch.float64), 0.0, device=b.device)
     torch.cuda.synchronize()
-    barrier()
+    D.barrier()
     dt = time.perf_counter() - t0
-    dt_t = torch.tensor([dt], dtype=torch.float64, device=b.device)
-    if world > 1:
-        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
-    dt = float(dt_t.item())
+    _, dt = D.reduce_rollout([0.0], dt, device=b.device)   # max over ranks
 
     # live per-launch kernel timing with HIP events on the launch stream (roofline)
     nk = min(200, args.steps)
@@ -131,7 +120,6 @@ def main():
     out = None
     if rank == 0:
         value = E * world * args.steps / dt
-        mv = met.cpu().numpy()
         out = {
             "metric": "env-steps/sec (agent-steps/sec) at 4096 envs/GPU, 1/2/4/8 MI355X",
             "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -152,8 +140,7 @@ def main():
         elif world == 1:
             out["cpu_baseline"] = None
     b.close()
-    if world > 1:
-        dist.destroy_process_group()
+    D.shutdown()
     if out is not None:
         print(json.dumps(out), flush=True)
 

@@ -1,0 +1,84 @@
+"""Multi-rank host logic on CPU (gloo, world_size 2): env sharding by env_id_offset and the single
+end-of-rollout metric all-reduce (cattleherd.distributed, used by bench.py).
+
+Each rank steps its shard of oracle envs (the CPU checker stands in for the GPU here) with the same
+Philox action stream the kernel draws; the all-reduced metric vector must equal a single-process run
+over all envs, and the reported time must be the max over ranks.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+E_TOTAL, T, N, M = 8, 90, 4, 16
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rollout(env_ids, table):
+    """steps, episodes, return_sum, terminated, truncated of random-action rollouts with auto-reset."""
+    import oracle as O
+    met = np.zeros(5)
+    for gid in env_ids:
+        env = O.Env(0, N, M, table, env_id=gid, start_level=2)
+        env.reset()
+        for t in range(T):
+            o, r, te, tr, done, _ = env.step(env.random_actions(t), autoreset=True)
+            met += [1, float(done), r[0], te[0], tr[0]]
+    return met
+
+
+def _worker(rank, world, port, table, out):
+    for p in (ROOT, os.path.join(ROOT, "rl-cattle-herding_amd"), os.path.join(ROOT, "oracle")):
+        sys.path.insert(0, p)
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from cattleherd import distributed as D
+    r, w, _ = D.init("gloo")
+    per = E_TOTAL // w
+    off = D.env_offset(r, per)
+    met = _rollout(range(off, off + per), table)
+    sums, tmax = D.reduce_rollout(met, elapsed=1.0 + r)
+    out[rank] = (sums, tmax, off)
+    D.shutdown()
+
+
+def test_sharded_rollout_metrics_equal_single_process():
+    from cattleherd._lib import spawn_table
+    table = spawn_table(M)
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    out = mgr.dict()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, table, out)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+        assert p.exitcode == 0
+    single = _rollout(range(E_TOTAL), table)
+    for r in range(world):
+        sums, tmax, off = out[r]
+        assert off == r * (E_TOTAL // world)
+        assert np.allclose(sums, single, rtol=1e-12, atol=0)
+        assert tmax == 2.0
+    assert single[1] > 0, "the rollout should finish episodes (level 2 terminates on approach)"
+
+
+def test_env_offset_and_world_defaults(monkeypatch):
+    from cattleherd import distributed as D
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    assert D.world_info() == (0, 1, 0)
+    assert D.env_offset(3, 4096) == 3 * 4096
+    sums, t = D.reduce_rollout(np.arange(4.0), 2.5)   # no process group: identity
+    assert np.array_equal(sums, np.arange(4.0)) and t == 2.5
