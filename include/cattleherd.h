@@ -130,7 +130,7 @@ int ch_step(ch_handle* h, const ch_step_io* io, void* stream);
  *   doubles: drone[22][E][N] (px py pz qx qy qz qw vx vy vz wx wy wz pid_last_rpy[3]
  *            pid_int_pos[3] pid_int_rpy[3]), cattle[4][E][M] (x y vx vy), env[2][E] (prev_cent clock)
  *   int32:   env[10][E] (n, step_counter, step_counter_A, has_prev, level, tally, spawn_index,
- *            active_mask, episode, reserved) */
+ *            active_mask, episode, step_index = ch_step calls so far = the Philox action counter) */
 int ch_state_size(const ch_handle* h, int64_t* n_doubles, int64_t* n_ints);
 int ch_get_state(ch_handle* h, double* host_doubles, int32_t* host_ints, void* stream);
 int ch_set_state(ch_handle* h, const double* host_doubles, const int32_t* host_ints, void* stream);

@@ -17,7 +17,7 @@ from . import _lib as L
 DRONE_COMPS = 22
 CATTLE_COMPS = 4
 ENV_INTS = ("n", "step_counter", "step_counter_A", "has_prev", "level", "tally", "spawn_index", "active_mask",
-            "episode", "reserved")
+            "episode", "step_index")
 
 
 class HerdBatch:
@@ -70,10 +70,26 @@ class HerdBatch:
         self.agent_active = torch.zeros((self.n_envs, num_drones), dtype=torch.uint8, **z)
         self.reset_happened = torch.zeros(self.n_envs, dtype=torch.uint8, **z)
         self.actions = torch.zeros((self.n_envs, num_drones, 4), dtype=torch.float32, **z)
+        # the step io block: output pointers are fixed for the life of the batch, so a step only
+        # rewrites the action pointers and flags (keeps the per-step host cost to one ctypes call)
         self._io = L.ChStepIO()
+        self._io.obs = self.obs.data_ptr()
+        self._io.reward = self.reward.data_ptr()
+        self._io.terminated = self.terminated.data_ptr()
+        self._io.truncated = self.truncated.data_ptr()
+        self._io.agent_active = self.agent_active.data_ptr()
+        self._io.reset_happened = self.reset_happened.data_ptr()
+        self._io_ref = ctypes.byref(self._io)
+        self._ch_step = L.lib().ch_step
+        self._raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+        self._dev_index = dev_index
+        self._actions_ptr = self.actions.data_ptr()
+        self._terminal_ptr = self.terminal_obs.data_ptr()
 
     # ------------------------------------------------------------------------------------------
     def _stream(self):
+        if self._raw_stream is not None:
+            return ctypes.c_void_p(self._raw_stream(self._dev_index))
         return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
 
     def reset(self, mask=None):
@@ -91,7 +107,7 @@ class HerdBatch:
         flags = (L.CH_STEP_AUTORESET if autoreset else 0) | (L.CH_STEP_RANDOM_ACTIONS if random_actions else 0)
         if random_actions:
             io.actions = None
-            io.actions_out = self.actions.data_ptr()
+            io.actions_out = self._actions_ptr
         else:
             if actions is None:
                 actions = self.actions
@@ -102,15 +118,11 @@ class HerdBatch:
             self._keep = actions
             io.actions = actions.data_ptr()
             io.actions_out = None
-        io.obs = self.obs.data_ptr()
-        io.reward = self.reward.data_ptr()
-        io.terminated = self.terminated.data_ptr()
-        io.truncated = self.truncated.data_ptr()
-        io.terminal_obs = self.terminal_obs.data_ptr() if (terminal_obs and autoreset) else None
-        io.agent_active = self.agent_active.data_ptr()
-        io.reset_happened = self.reset_happened.data_ptr()
+        io.terminal_obs = self._terminal_ptr if (terminal_obs and autoreset) else None
         io.flags = flags
-        L.check(L.lib().ch_step(self.handle, ctypes.byref(io), self._stream()), self.handle)
+        rc = self._ch_step(self.handle, self._io_ref, self._stream())
+        if rc:
+            L.check(rc, self.handle)
         return self.obs, self.reward, self.terminated, self.truncated
 
     # ------------------------------------------------------------------------------------------

@@ -33,9 +33,14 @@ struct ch_handle {
     double* metrics = nullptr;
     double* spawn = nullptr;
     int n_scen = 0, n_cows = 0;
-    int64_t step_index = 0;
     double* debug = nullptr;
     int phase_mask = 0;
+    // v2 step kernel (ch_step.hip): envs per workgroup, block size, dynamic LDS, cow-pair list
+    int kernel = 2;
+    long long* tstamp = nullptr;
+    int G = 1, block = 64, P = 0;
+    size_t lds = 0;
+    uint16_t* pairs = nullptr;
     std::string err;
 };
 
@@ -106,6 +111,15 @@ static std::vector<double> make_spawn_table(int cows) {
     return t;
 }
 
+// CattleSpacingRewardFunction (CattleAviary.py:572-592), r > r0 branch: C = f(r0) / exp(-lambda r0) is the
+// same number on every call; evaluated once here with the reference's expression.
+static double cattle_spacing_cc() {
+    const double A = 1.2, B = 2.1, C = 3.3, K = 0.2, D = -1, R0 = 1.3, LAM = 0.8;
+    volatile double r0 = R0;   // evaluate at run time with the host libm, as the reference (and the oracle) do
+    double fr0 = A * std::exp(-((r0 - D) * (r0 - D)) / (2 * (C * C))) - B * std::exp(-(r0 * r0) / (2 * (K * K)));
+    return fr0 / std::exp(-LAM * r0);
+}
+
 template <class R>
 static StepParams<R> params(ch_handle* h) {
     StepParams<R> p{};
@@ -117,11 +131,14 @@ static StepParams<R> params(ch_handle* h) {
     p.episode_len = h->episode_len; p.damping = c.damping;
     p.dt_ctrl = 1.0 / c.ctrl_freq; p.dt = 1.0 / c.pyb_freq;
     p.k0 = (uint32_t)c.seed; p.k1 = (uint32_t)(c.seed >> 32);
-    p.env_off = c.env_id_offset; p.step_index = h->step_index;
+    p.env_off = c.env_id_offset;
+    p.cs_cc = cattle_spacing_cc();
     p.drone = (R*)h->drone; p.cattle = (R*)h->cattle; p.envr = (R*)h->envr; p.envi = h->envi;
     p.metrics = h->metrics; p.spawn = h->spawn; p.n_scen = h->n_scen; p.n_cows = h->n_cows;
     p.debug = h->debug;
     p.phase_mask = h->phase_mask;
+    p.G = h->G; p.P = h->P; p.pairs = h->pairs;
+    p.tstamp = h->tstamp;
     return p;
 }
 
@@ -170,7 +187,7 @@ int ch_default_config(ch_config* c, int32_t mode, int32_t num_drones, int32_t nu
 const char* ch_last_error(const ch_handle* h) { return h ? h->err.c_str() : g_create_err.c_str(); }
 
 static void free_all(ch_handle* h) {
-    void* ptrs[] = {h->drone, h->cattle, h->envr, h->envi, h->metrics, h->spawn};
+    void* ptrs[] = {h->drone, h->cattle, h->envr, h->envi, h->metrics, h->spawn, h->pairs};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
 }
@@ -226,6 +243,7 @@ int ch_create(const ch_config* c, int64_t n_envs, int32_t device, ch_handle** ou
     h->start_level = level;
     h->episode_len = kEpisodeLen[level];
     h->rsize = c->precision == CH_PREC_F64 ? sizeof(double) : sizeof(float);
+    h->P = h->M * (h->M - 1) / 2;
     (void)kLevelMin; (void)kLevelMax;
 
     auto cleanup = [&](int code) { free_all(h); std::string m = h->err; delete h; g_create_err = m; return code; };
@@ -256,6 +274,32 @@ int ch_create(const ch_config* c, int64_t n_envs, int32_t device, ch_handle** ou
         h->n_cows = std::max(h->M, (int)CH_SPAWN_COWS);
     }
     CTRY(hipMalloc(&h->spawn, table.size() * sizeof(double)));
+    {
+        // v2 geometry: G envs per workgroup with all G*N drone chains in wave 0, the LDS
+        // carve within the per-CU budget, and at least one workgroup per CU when E allows it.
+        int cus = 256, lds_max = 64 * 1024;
+        CTRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+        if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, device) != hipSuccess)
+            lds_max = 64 * 1024;
+        const size_t budget = std::min<size_t>((size_t)lds_max, 150 * 1024);
+        // a drone wave (G*N <= 64 drone chains) plus three cow waves (G*M cows, one per lane when it fits)
+        int G = std::max(1, std::min(64 / h->NC, 192 / h->M));
+        G = (int)std::min<int64_t>(G, std::max<int64_t>(1, E / std::max(cus, 1)));
+        while (G & (G - 1)) G &= G - 1;   // power of two: whole workgroups per CU at E = 2^k
+        while (G > 1 && V2Layout(G, h->NC, h->M, h->P, c->mode, (int)h->rsize).bytes() > budget) --G;
+        h->G = G;
+        h->lds = V2Layout(G, h->NC, h->M, h->P, c->mode, (int)h->rsize).bytes();
+        h->block = 256;
+        // measured (tools/geom_sweep.py, MI355X): the dataflow kernel wins for CTDE with up to 8 drones;
+        // MARL and the 9..12-drone CTDE configs are still faster on the team-per-env kernel
+        if (c->mode == CH_MODE_MARL || h->NC > 8) h->kernel = 1;
+        if (h->lds > budget) h->kernel = 1;   // one env's pair table alone exceeds the budget
+        std::vector<uint16_t> pl((size_t)std::max(h->P, 1));
+        for (int i = 0, r = 0; i < h->M; ++i)
+            for (int j = i + 1; j < h->M; ++j) pl[r++] = (uint16_t)(i | (j << 8));
+        CTRY(hipMalloc(&h->pairs, pl.size() * sizeof(uint16_t)));
+        CTRY(hipMemcpy(h->pairs, pl.data(), pl.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+    }
     CTRY(hipMemcpy(h->spawn, table.data(), table.size() * sizeof(double), hipMemcpyHostToDevice));
 
     // initial state = what the constructors leave behind before the first reset():
@@ -348,14 +392,13 @@ int ch_step(ch_handle* h, const ch_step_io* io, void* stream) {
     if (h->rsize == sizeof(double)) {
         StepParams<double> p = params<double>(h);
         fill(p);
-        e = launch_step(p, h->team, st);
+        e = h->kernel == 2 ? launch_step_v2(p, h->block, h->lds, st) : launch_step(p, h->team, st);
     } else {
         StepParams<float> p = params<float>(h);
         fill(p);
-        e = launch_step(p, h->team, st);
+        e = h->kernel == 2 ? launch_step_v2(p, h->block, h->lds, st) : launch_step(p, h->team, st);
     }
     if (e != hipSuccess) return fail(h, CH_ERR_DEVICE, std::string("ch_step launch: ") + hipGetErrorString(e));
-    h->step_index += 1;
     return CH_OK;
 }
 
@@ -417,6 +460,40 @@ int ch_set_state(ch_handle* h, const double* hd, const int32_t* hi, void* stream
 int ch__set_debug(ch_handle* h, double* dev) {
     if (!h) return CH_ERR_INVALID;
     h->debug = dev;
+    return CH_OK;
+}
+
+/* Internal diagnostics: step kernel version (1 = team-per-env ch_kernels.hip, 2 = role-split ch_step.hip). */
+int ch__set_kernel(ch_handle* h, int32_t version) {
+    if (!h || (version != 1 && version != 2)) return CH_ERR_INVALID;
+    if (version == 2 && h->lds > 150 * 1024) return CH_ERR_UNSUPPORTED;
+    h->kernel = version;
+    return CH_OK;
+}
+
+/* Internal diagnostics: device buffer [grid][16] of per-workgroup timestamps written by the v2 kernel. */
+int ch__set_tstamp(ch_handle* h, long long* dev) {
+    if (!h) return CH_ERR_INVALID;
+    h->tstamp = dev;
+    return CH_OK;
+}
+
+/* Internal diagnostics: override the v2 geometry (envs per workgroup, block size) for sweeps. */
+int ch__set_geometry(ch_handle* h, int32_t G, int32_t block) {
+    if (!h || G < 1 || G > 64 || G * h->NC > 64 || block < 128 || block > 256 || block % 64) return CH_ERR_INVALID;
+    const size_t lds = V2Layout(G, h->NC, h->M, h->P, h->cfg.mode, (int)h->rsize).bytes();
+    if (lds > 150 * 1024) return CH_ERR_UNSUPPORTED;
+    h->G = G; h->block = block; h->lds = lds;
+    return CH_OK;
+}
+
+/* Internal diagnostics: v2 geometry (envs per workgroup, block size, dynamic LDS bytes). */
+int ch__geometry(const ch_handle* h, int32_t* G, int32_t* block, int64_t* lds, int32_t* kernel) {
+    if (!h) return CH_ERR_INVALID;
+    if (G) *G = h->G;
+    if (block) *block = h->block;
+    if (lds) *lds = (int64_t)h->lds;
+    if (kernel) *kernel = h->kernel;
     return CH_OK;
 }
 

@@ -1,0 +1,135 @@
+// ch_common.h — per-env task bookkeeping and reset pieces shared by the step kernels.
+//
+// Restates the order-dependent parts of the reference's env.step(): curriculum tally
+// (curriculum_learning.py:200-219), _computeTerminated (CattleAviary.py:422-492,
+// MARLCattleAviary.py:246-321) and the reset bookkeeping of BaseAviary.reset / _housekeeping
+// (BaseAviary.py:280-331, 547-700).  Paths relative to gym_pybullet_drones/.
+#pragma once
+#include "ch_device.h"
+#include "ch_internal.h"
+
+namespace ch {
+
+// curriculum_learning.py:200-219
+__device__ __forceinline__ void curriculum_success(const Level* LT, int& level, int& tally) {
+    tally += 1;
+    if (tally >= LT[level].required_tally) {
+        tally = 0;
+        level += 1;
+        if (level >= 8) level = 7;
+    }
+}
+
+// _computeTerminated (CattleAviary.py:422-492; MARLCattleAviary.py:246-321)
+template <class R>
+__device__ __forceinline__ bool term_call(const Level* LT, int level, R& clock, R clock_inc, R min_spacing, R cent, R eff) {
+    const Level& L = LT[level];
+    if (level == 0 || level == 1) {
+        R up = R(L.desired) + R(L.desired) * R(L.tol), lo = R(L.desired) - R(L.desired) * R(L.tol);
+        if (min_spacing < up && min_spacing > lo) {
+            clock += clock_inc;
+            if (clock >= R(L.hold)) return true;
+        } else {
+            clock = 0;
+        }
+    } else if (level == 2 || level == 3) {
+        if (cent < R(L.approach_min)) return true;
+    } else if (level == 4 || level == 6) {
+        if (eff > R(L.min_eff)) return true;
+    } else if (level == 5) {
+        if (eff > R(L.min_eff)) {
+            R up = R(L.cattle_desired) + R(L.cattle_desired) * R(L.cattle_tol);
+            R lo = R(L.cattle_desired) - R(L.cattle_desired) * R(L.cattle_tol);
+            if (min_spacing < up && min_spacing > lo) return true;
+        }
+    }
+    return false;
+}
+
+// env-scalar part of a reset: NUM_DRONES draw (BaseAviary.py:307), counters (306, 557), spawn index
+// advanced before use (600-606); prev_cent_dists / spacing clock persist in compat mode (CattleAviary.py:89)
+template <class R>
+__device__ __forceinline__ void reset_scalars(const StepParams<R>& p, int e, int& n, int& sc, int& scA, int& spawn,
+                                              int& episode, int& active, int& has_prev, R& prev, R& clock) {
+    const long long env_id = p.env_off + e;
+    int span = p.max_drones - p.min_drones + 1;
+    int nn = p.min_drones;
+    if (span > 1) {
+        double u = philox_uniform53(p.k0, p.k1, (uint32_t)episode, 0, (uint32_t)env_id);
+        nn = p.min_drones + (int)(u * span);
+        if (nn > p.max_drones) nn = p.max_drones;
+    }
+    n = nn;
+    sc = 0; scA = 0;
+    spawn += 1;
+    if (spawn >= p.n_scen) spawn = 0;
+    active = (1 << nn) - 1;
+    if (!p.compat) { has_prev = 0; prev = 0; clock = 0; }
+    episode += 1;
+}
+
+// initial pose of constructor drone k (initialize_drone_positions, BaseAviary.py:251-277): written to
+// the SoA state; returns x, y, z.  PID state persists across resets in compat mode (the reference's
+// DSLPIDControl objects are created once, BaseRLAviary.py:80).
+template <class R>
+__device__ __forceinline__ void reset_drone(const StepParams<R>& p, long long di, int k, int n_new, R& x, R& y, R& z) {
+    const long long DS = (long long)p.E * p.NC;
+    x = 0; y = 0; z = 0;
+    if (k < n_new) {
+        if (n_new <= 4) { x = R(k * 1.75); y = 0; }
+        else {
+            int r1 = n_new / 2;
+            if (k < r1) { x = R(k * 1.75); y = 0; } else { x = R((k - r1) * 1.75); y = R(1.75); }
+        }
+        z = R(kTargetAlt);
+    }
+    R* D = p.drone;
+    D[0 * DS + di] = x; D[1 * DS + di] = y; D[2 * DS + di] = z;
+    D[3 * DS + di] = 0; D[4 * DS + di] = 0; D[5 * DS + di] = 0; D[6 * DS + di] = 1;
+#pragma unroll
+    for (int c = 7; c < 13; ++c) D[c * DS + di] = 0;
+    if (!p.compat) {
+#pragma unroll
+        for (int c = 13; c < 22; ++c) D[c * DS + di] = 0;
+    }
+}
+
+// cow j of a reset env: YAML scenario position, yaw/velocity angle pi(2U-1) (BaseAviary.py:600-637),
+// U from Philox keyed (seed, env id, episode, 1 + j)
+template <class R>
+__device__ __forceinline__ void reset_cow(const StepParams<R>& p, long long ci, long long env_id, int j, int spawn,
+                                          uint32_t episode, R& x, R& y, R& vx, R& vy) {
+    const long long CS = (long long)p.E * p.M;
+    const double* tab = p.spawn + ((long long)spawn * p.n_cows + j) * 2;
+    x = R(tab[0]); y = R(tab[1]);
+    double u = philox_uniform53(p.k0, p.k1, episode, 1 + j, (uint32_t)env_id);
+    double ang = kPi * (2 * u - 1);
+    vx = R(kMaxVelCattle * m_cos(ang)); vy = R(kMaxVelCattle * m_sin(ang));
+    p.cattle[0 * CS + ci] = x; p.cattle[1 * CS + ci] = y; p.cattle[2 * CS + ci] = vx; p.cattle[3 * CS + ci] = vy;
+}
+
+// end-of-episode bonus of MARLCattleAviary._endOfEpisodeReward (MARLCattleAviary.py:183-241)
+template <class R>
+__device__ __forceinline__ R marl_end_of_episode(const Level* LT, int level, R a, R b, R cent, R eff, R dist_to_herd,
+                                                int n) {
+    const Level& L2 = LT[level];
+    R eor = 0;
+    if (level == 0 || level == 1) {
+        R up = R(L2.desired) + R(L2.desired) * R(L2.tol), lo = R(L2.desired) - R(L2.desired) * R(L2.tol);
+        if (a >= lo && a <= up && b >= lo && b <= up) eor += R(50.0) / R(n);
+    } else if (level == 2 || level == 3) {
+        if (cent < R(L2.approach_min)) eor += R(50.0);
+    } else if (level == 4 || level == 6) {
+        R wgt = clip(R(1.0) - dist_to_herd / R(10.0), R(0), R(1));
+        eor += eff * R(2) * wgt;
+    } else if (level == 5) {
+        if (eff > R(L2.min_eff)) {
+            R up = R(L2.cattle_desired) + R(L2.cattle_desired) * R(L2.cattle_tol);
+            R lo = R(L2.cattle_desired) - R(L2.cattle_desired) * R(L2.cattle_tol);
+            if (a >= lo && a <= up && b >= lo && b <= up) eor += R(50.0) / R(n);
+        }
+    }
+    return eor;
+}
+
+}  // namespace ch

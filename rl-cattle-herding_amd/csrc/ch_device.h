@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "ch_internal.h"
+
 namespace ch {
 
 // ---- constants: assets/cf2x.urdf:5-12, BaseAviary.py:97-173, DSLPIDControl.py:37-53 ----------
@@ -22,13 +24,6 @@ constexpr double kMissionBoundary = 15, kMaxFormation = 8, kCollision = 0.2;  //
 constexpr double kPi = 3.14159265358979323846;
 
 // curriculum_learning.py:10-194
-struct Level {
-    double desired, tol, hold, approach_min, min_eff, cattle_desired, cattle_tol;
-    int min_drones, max_drones;
-    double episode_len;
-    double w_simple, w_complex, w_survival, w_approach, w_eff, w_cattle;
-    int required_tally;
-};
 __constant__ static const Level kLevels[8] = {
     {0.8, 0.3, 10, 0.0, 0, 0.0, 0.0, 3, 3, 40, 1, 0, 0, 0, 0, 0.0, 100},
     {0.8, 0.2, 25, 0.0, 0, 0.0, 0.0, 4, 4, 40, 0, 1, -0.5, 0, 0, 0.0, 300},
@@ -302,13 +297,13 @@ template <class R> __device__ __forceinline__ R complex_spacing(R r, const Level
     rew += R(0.1) * (R(1) - fabs(r - ds));
     return rew;
 }
-template <class R> __device__ __forceinline__ R cattle_spacing(R r) {
+// cc = the continuation constant fr0 / exp(-lambda r0) of the r > r0 branch, evaluated once on the host
+// (ch_api.cpp: cattle_spacing_cc) with the same expression the reference evaluates per call
+template <class R> __device__ __forceinline__ R cattle_spacing(R r, R cc) {
     const double A = 1.2, B = 2.1, C = 3.3, K = 0.2, D = -1, R0 = 1.3, LAM = 0.8;
     if (r <= R(R0))
         return R(A) * m_exp(-((r - R(D)) * (r - R(D))) / R(2 * (C * C))) - R(B) * m_exp(-(r * r) / R(2 * (K * K)));
-    R fr0 = R(A) * m_exp(-(R(R0 - D) * R(R0 - D)) / R(2 * (C * C))) - R(B) * m_exp(-(R(R0) * R(R0)) / R(2 * (K * K)));
-    R Cc = fr0 / m_exp(R(-LAM) * R(R0));
-    return Cc * m_exp(R(-LAM) * r);
+    return cc * m_exp(R(-LAM) * r);
 }
 
 // ---- Philox4x32-10 (Random123) ------------------------------------------------------------------

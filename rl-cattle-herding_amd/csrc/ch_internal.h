@@ -12,7 +12,7 @@ constexpr int kMMax = 64;          // cattle per env supported by the team mappi
 constexpr int kDroneComps = 22;    // px py pz qx qy qz qw vx vy vz wx wy wz pid[9]
 constexpr int kCattleComps = 4;    // x y vx vy
 constexpr int kEnvReal = 2;        // prev_cent, clock
-constexpr int kEnvInt = 10;        // n sc scA has_prev level tally spawn active episode reserved
+constexpr int kEnvInt = 10;        // n sc scA has_prev level tally spawn active episode step_index
 constexpr int kMetricCurReturn = CH_METRIC_COUNT;      // running episode return
 constexpr int kMetricCurLen = CH_METRIC_COUNT + 1;     // running episode length
 constexpr int kMetricRows = CH_METRIC_COUNT + 2;
@@ -23,7 +23,8 @@ struct StepParams {
     int min_drones, max_drones, ctrl_freq, substeps, compat, torque_world, gyro, marl_wrapper;
     double episode_len, damping, dt_ctrl, dt;
     uint32_t k0, k1;
-    long long env_off, step_index;
+    long long env_off;
+    double cs_cc;   // CattleSpacingRewardFunction continuation constant (host-evaluated)
     R* drone;       // [22][E][NC]
     R* cattle;      // [4][E][M]
     R* envr;        // [2][E]
@@ -44,9 +45,48 @@ struct StepParams {
     uint32_t flags;
     double* debug;  // optional [E][NC][16] per-drone intermediates (diagnostics only)
     int phase_mask; // diagnostics only: skip phases (1 drones, 2 flock, 4 task, 8 obs) for time attribution
+    int G, P;                 // v2: envs per workgroup, cow pairs per env
+    const uint16_t* pairs;    // v2: [P] unordered cow pairs (i | j << 8) in tri() order
+    long long* tstamp;        // diagnostics only: [grid][16] per-workgroup phase timestamps (ch__set_tstamp)
+};
+
+// one curriculum level (curriculum_learning.py:10-194); the table kLevels lives in ch_device.h
+struct Level {
+    double desired, tol, hold, approach_min, min_eff, cattle_desired, cattle_tol;
+    int min_drones, max_drones;
+    double episode_len;
+    double w_simple, w_complex, w_survival, w_approach, w_eff, w_cattle;
+    int required_tally;
+};
+
+// LDS carve of one v2 step workgroup (ch_step.hip); identical on host (size) and device (offsets).
+constexpr int kV2EnvInts = 11;
+constexpr int kV2Flags = 6;          // LDS hand-off counters between the drone wave and the cow waves
+struct V2Layout {
+    enum { CX = 0, DRONE, DCOW, ENVR, PAIRS, MET, IMG, EI, LEVELS, BYTES, NOFF };
+    int G, N, M, P, rows;
+    size_t off[NOFF + 1];
+    static __host__ __device__ size_t al(size_t x) { return (x + 15) & ~size_t(15); }
+    __host__ __device__ V2Layout(int G_, int N_, int M_, int P_, int mode, int rb) : G(G_), N(N_), M(M_), P(P_) {
+        rows = mode == CH_MODE_CTDE ? 12 : N;
+        size_t o = 0;
+        off[CX] = o;     o = al(o + 6 * (size_t)G * M * rb);         // cx cy cvx cvy aux auy
+        off[DRONE] = o;  o = al(o + 12 * (size_t)G * N * rb);        // dx dy dz pa pb sa sb ca cb scat psp mrew
+        off[DCOW] = o;   o = al(o + (size_t)G * N * M * rb);         // cow-drone distances
+        off[ENVR] = o;   o = al(o + 2 * (size_t)G * rb);             // prev clock
+        off[PAIRS] = o;  o = al(o + 4 * (size_t)G * P * rb);         // alpha pair table
+        off[MET] = o;    o = al(o + (size_t)kMetricRows * G * 8);
+        off[IMG] = o;    o = al(o + (size_t)G * rows * 86 * 4);      // the workgroup's observation image
+        off[EI] = o;     o = al(o + ((size_t)kV2EnvInts * G + G + 2 + kV2Flags) * 4);
+        off[LEVELS] = o; o = al(o + 8 * sizeof(Level));              // curriculum table
+        off[BYTES] = o;  o = al(o + (size_t)G * P + 3 * (size_t)G * N + (size_t)G * M);
+        off[NOFF] = o;
+    }
+    __host__ __device__ size_t bytes() const { return off[NOFF]; }
 };
 
 template <class R> hipError_t launch_step(const StepParams<R>& p, int team, hipStream_t st);
 template <class R> hipError_t launch_reset(const StepParams<R>& p, int team, hipStream_t st);
+template <class R> hipError_t launch_step_v2(const StepParams<R>& p, int block, size_t lds, hipStream_t st);
 
 }  // namespace ch

@@ -12,6 +12,7 @@
 
 #include "ch_device.h"
 #include "ch_internal.h"
+#include "ch_common.h"
 
 namespace ch {
 
@@ -100,101 +101,21 @@ __device__ __forceinline__ void neighbour_obs(Slot<R, TEAM>& S, int i, int n) {
     S.nbr[i][3] = i2 >= 0 ? (float)(S.dy[i2] - S.dy[i]) : 0.0f;
 }
 
-// curriculum_learning.py:200-219
-__device__ __forceinline__ void curriculum_success(int& level, int& tally) {
-    tally += 1;
-    if (tally >= kLevels[level].required_tally) {
-        tally = 0;
-        level += 1;
-        if (level >= 8) level = 7;
-    }
-}
-
-// _computeTerminated (CattleAviary.py:422-492; MARLCattleAviary.py:246-321)
-template <class R>
-__device__ __forceinline__ bool term_call(int level, R& clock, R clock_inc, R min_spacing, R cent, R eff) {
-    const Level& L = kLevels[level];
-    if (level == 0 || level == 1) {
-        R up = R(L.desired) + R(L.desired) * R(L.tol), lo = R(L.desired) - R(L.desired) * R(L.tol);
-        if (min_spacing < up && min_spacing > lo) {
-            clock += clock_inc;
-            if (clock >= R(L.hold)) return true;
-        } else {
-            clock = 0;
-        }
-    } else if (level == 2 || level == 3) {
-        if (cent < R(L.approach_min)) return true;
-    } else if (level == 4 || level == 6) {
-        if (eff > R(L.min_eff)) return true;
-    } else if (level == 5) {
-        if (eff > R(L.min_eff)) {
-            R up = R(L.cattle_desired) + R(L.cattle_desired) * R(L.cattle_tol);
-            R lo = R(L.cattle_desired) - R(L.cattle_desired) * R(L.cattle_tol);
-            if (min_spacing < up && min_spacing > lo) return true;
-        }
-    }
-    return false;
-}
-
 template <class R, int TEAM>
 __device__ __forceinline__ void reset_env(const StepParams<R>& p, Slot<R, TEAM>& S, int e, int t, int n_new, int spawn,
                                           uint32_t episode, R* own_z) {
-    const long long DS = (long long)p.E * p.NC, CS = (long long)p.E * p.M;
     const long long env_id = p.env_off + e;
     if (t < p.NC) {
-        R x = 0, y = 0, z = 0;
-        if (t < n_new) {
-            if (n_new <= 4) { x = R(t * 1.75); y = 0; }
-            else {
-                int r1 = n_new / 2;
-                if (t < r1) { x = R(t * 1.75); y = 0; } else { x = R((t - r1) * 1.75); y = R(1.75); }
-            }
-            z = R(kTargetAlt);
-        }
-        const long long di = (long long)e * p.NC + t;
-        R* D = p.drone;
-        D[0 * DS + di] = x; D[1 * DS + di] = y; D[2 * DS + di] = z;
-        D[3 * DS + di] = 0; D[4 * DS + di] = 0; D[5 * DS + di] = 0; D[6 * DS + di] = 1;
-#pragma unroll
-        for (int c = 7; c < 13; ++c) D[c * DS + di] = 0;
-        if (!p.compat) {
-#pragma unroll
-            for (int c = 13; c < 22; ++c) D[c * DS + di] = 0;
-        }
+        R x, y, z;
+        reset_drone(p, (long long)e * p.NC + t, t, n_new, x, y, z);
         S.dx[t] = x; S.dy[t] = y;
         *own_z = z;
     }
     if (t < p.M) {
-        const double* tab = p.spawn + ((long long)spawn * p.n_cows + t) * 2;
-        R x = R(tab[0]), y = R(tab[1]);
-        double u = philox_uniform53(p.k0, p.k1, episode, 1 + t, (uint32_t)env_id);
-        double ang = kPi * (2 * u - 1);
-        R vx = R(kMaxVelCattle * m_cos(ang)), vy = R(kMaxVelCattle * m_sin(ang));
-        const long long ci = (long long)e * p.M + t;
-        p.cattle[0 * CS + ci] = x; p.cattle[1 * CS + ci] = y; p.cattle[2 * CS + ci] = vx; p.cattle[3 * CS + ci] = vy;
+        R x, y, vx, vy;
+        reset_cow(p, (long long)e * p.M + t, env_id, t, spawn, episode, x, y, vx, vy);
         S.cx[t] = x; S.cy[t] = y; S.cvx[t] = vx; S.cvy[t] = vy;
     }
-}
-
-// lane-0 part of a reset: NUM_DRONES draw, counters, spawn index (BaseAviary.py:280-331, 600-606)
-template <class R>
-__device__ __forceinline__ void reset_scalars(const StepParams<R>& p, int e, int& n, int& sc, int& scA, int& spawn,
-                                              int& episode, int& active, int& has_prev, R& prev, R& clock) {
-    const long long env_id = p.env_off + e;
-    int span = p.max_drones - p.min_drones + 1;
-    int nn = p.min_drones;
-    if (span > 1) {
-        double u = philox_uniform53(p.k0, p.k1, (uint32_t)episode, 0, (uint32_t)env_id);
-        nn = p.min_drones + (int)(u * span);
-        if (nn > p.max_drones) nn = p.max_drones;
-    }
-    n = nn;
-    sc = 0; scA = 0;
-    spawn += 1;
-    if (spawn >= p.n_scen) spawn = 0;
-    active = (1 << nn) - 1;
-    if (!p.compat) { has_prev = 0; prev = 0; clock = 0; }
-    episode += 1;
 }
 
 template <class R, int TEAM, bool RESET_ONLY, int MODE>
@@ -212,12 +133,12 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
     const int cat_off = marl ? 18 : 34;
 
     // ---- env scalars (broadcast loads) -------------------------------------------------------
-    int n = 0, sc = 0, scA = 0, has_prev = 0, level = 0, tally = 0, spawn = 0, active = 0, episode = 0;
+    int n = 0, sc = 0, scA = 0, has_prev = 0, level = 0, tally = 0, spawn = 0, active = 0, episode = 0, stepi = 0;
     R prev = 0, clock = 0;
     if (valid) {
         n = p.envi[0 * E + e]; sc = p.envi[1 * E + e]; scA = p.envi[2 * E + e]; has_prev = p.envi[3 * E + e];
         level = p.envi[4 * E + e]; tally = p.envi[5 * E + e]; spawn = p.envi[6 * E + e]; active = p.envi[7 * E + e];
-        episode = p.envi[8 * E + e];
+        episode = p.envi[8 * E + e]; stepi = p.envi[9 * E + e];
         prev = p.envr[0 * E + e]; clock = p.envr[1 * E + e];
     }
     if (t == 0) { S.done = 0; S.reset = 0; S.n = n; }
@@ -246,8 +167,7 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
             for (int c = 0; c < 9; ++c) pid[c] = ld(p.drone, 13 + c, DS, di);
             float a[4];
             if (p.flags & CH_STEP_RANDOM_ACTIONS) {
-                uint32_t c4[4] = {(uint32_t)p.step_index, (uint32_t)((unsigned long long)p.step_index >> 32), (uint32_t)t,
-                                  (uint32_t)(p.env_off + e)};
+                uint32_t c4[4] = {(uint32_t)stepi, 0u, (uint32_t)t, (uint32_t)(p.env_off + e)};
                 philox(c4, p.k0, p.k1);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) a[k] = (float)(c4[k] >> 8) * (1.0f / 16777216.0f) * 2.0f - 1.0f;
@@ -381,7 +301,7 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
             const Level& L = kLevels[level];
             S.sa[i] = simple_spacing(m1, L); S.sb[i] = simple_spacing(m2, L);
             S.ca[i] = complex_spacing(m1, L); S.cb[i] = complex_spacing(m2, L);
-            S.scat[i] = cattle_spacing(best);
+            S.scat[i] = cattle_spacing(best, R(p.cs_cc));
             neighbour_obs(S, i, n);
         }
         if (valid && task && t < p.M) {
@@ -451,9 +371,9 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
                 for (int i = 0; i < n; ++i) tot += rg + R(0.5) * ((per_sp[i] - msp) + (S.scat[i] - mcat));
                 R rew = tot / R(n);
                 const R inc = R(1.0 / 240);
-                bool te = term_call(level, clock, inc, ms, cent, eff);
-                if (te) curriculum_success(level, tally);
-                bool te2 = term_call(level, clock, inc, ms, cent, eff);
+                bool te = term_call(kLevels, level, clock, inc, ms, cent, eff);
+                if (te) curriculum_success(kLevels, level, tally);
+                bool te2 = term_call(kLevels, level, clock, inc, ms, cent, eff);
                 bool tr = any_alt || any_coll || any_iso || cent > R(kMissionBoundary) || time_up;
                 p.reward[e] = (float)rew;
                 p.term[e] = te2; p.trunc[e] = tr;
@@ -490,28 +410,11 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
                     r += clip((change / (max_step + R(1e-6))) * R(5), R(-1.0), R(1.0)) * R(L.w_approach);
                     r += (eff / R(100)) * R(L.w_eff);
                     r += S.scat[i] * R(L.w_cattle);
-                    if (term_call(level, clock, inc, ms, cent, eff)) {
+                    if (term_call(kLevels, level, clock, inc, ms, cent, eff)) {
                         // _endOfEpisodeReward (MARLCattleAviary.py:183-241)
-                        const Level& L2 = kLevels[level];
-                        R eor = 0;
-                        if (level == 0 || level == 1) {
-                            R up = R(L2.desired) + R(L2.desired) * R(L2.tol), lo = R(L2.desired) - R(L2.desired) * R(L2.tol);
-                            if (a >= lo && a <= up && b >= lo && b <= up) eor += R(50.0) / R(n);
-                        } else if (level == 2 || level == 3) {
-                            if (cent < R(L2.approach_min)) eor += R(50.0);
-                        } else if (level == 4 || level == 6) {
-                            R dd = norm2(scx - S.dx[i], scy - S.dy[i]);
-                            R wgt = clip(R(1.0) - dd / R(10.0), R(0), R(1));
-                            eor += eff * R(2) * wgt;
-                        } else if (level == 5) {
-                            if (eff > R(L2.min_eff)) {
-                                R up = R(L2.cattle_desired) + R(L2.cattle_desired) * R(L2.cattle_tol);
-                                R lo = R(L2.cattle_desired) - R(L2.cattle_desired) * R(L2.cattle_tol);
-                                if (a >= lo && a <= up && b >= lo && b <= up) eor += R(50.0) / R(n);
-                            }
-                        }
+                        R eor = marl_end_of_episode(kLevels, level, a, b, cent, eff, norm2(scx - S.dx[i], scy - S.dy[i]), n);
                         r += eor;
-                        curriculum_success(level, tally);
+                        curriculum_success(kLevels, level, tally);
                     } else if (trunc_i(i)) {
                         r -= R(50);
                     }
@@ -520,13 +423,13 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
                 R r1[kNMax];
                 uint8_t d1[kNMax];
                 for (int i = 0; i < n; ++i) r1[i] = reward_i(i);
-                for (int i = 0; i < n; ++i) d1[i] = term_call(level, clock, inc, ms, cent, eff);
+                for (int i = 0; i < n; ++i) d1[i] = term_call(kLevels, level, clock, inc, ms, cent, eff);
                 for (int i = 0; i < p.NC; ++i) { rout[i] = R(NAN); tout[i] = 0; trout[i] = 0; }
                 if (p.marl_wrapper) {
                     for (int i = 0; i < n; ++i) {
                         if (!((active >> i) & 1)) continue;
                         rout[i] = reward_i(i);
-                        tout[i] = term_call(level, clock, inc, ms, cent, eff);
+                        tout[i] = term_call(kLevels, level, clock, inc, ms, cent, eff);
                         trout[i] = trunc_i(i);
                     }
                     int live = 0;
@@ -621,6 +524,7 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
         p.envi[0 * E + e] = n; p.envi[1 * E + e] = sc; p.envi[2 * E + e] = scA; p.envi[3 * E + e] = has_prev;
         p.envi[4 * E + e] = level; p.envi[5 * E + e] = tally; p.envi[6 * E + e] = spawn; p.envi[7 * E + e] = active;
         p.envi[8 * E + e] = episode;
+        if (!RESET_ONLY) p.envi[9 * E + e] = stepi + 1;   // ch_step calls on this env (Philox action counter)
         p.envr[0 * E + e] = prev; p.envr[1 * E + e] = clock;
     }
 }

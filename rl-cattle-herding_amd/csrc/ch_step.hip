@@ -1,0 +1,811 @@
+// ch_step.hip — the fused env-step kernel, v2: a drone wave and cow waves in dataflow (gfx950 / MI355X).
+//
+// One launch advances every environment by one control step (reference: BaseAviary.step,
+// sb3_envs/BaseAviary.py:335-465; rllib_envs/BaseAviary.py:320-438 + marl_wrapper.py:77-119).
+//
+// Every piece of this step is a long dependent fp64 chain (PID, rigid-body substeps, libm sequences),
+// so the kernel is organised around latency rather than lanes.  A workgroup holds G environments
+// (G*N <= 64) in 2..4 waves:
+//   wave 0 ("drone wave"), the critical path:
+//       Philox action -> PID -> 4 physics substeps -> state, LDS positions      [signal D]
+//       per-drone reward terms + nearest-neighbour observation entries         [signal T]
+//       (wait H) closest cow from the cow waves' distance table -> cattle term
+//       per-env reward / terminated / truncated / curriculum / metrics bookkeeping
+//   waves 1.. ("cow waves"), concurrently on the other SIMDs:
+//       flock alpha term as a table of the M(M-1)/2 unordered cow pairs      [A: all cow waves]
+//       per-cow alpha row sums in the reference's neighbour order (each pair quantity is symmetric and
+//       the two directed contributions are exact negations: bit-identical to the ordered loop)
+//       (wait D) cow-drone distances, herded winding number, cattle observation entries   [signal H]
+//       shepherd / predator / gamma terms and the velocity update (flockUtils.py:271-348)
+//       (wait T, all H) copy of the workgroup's observation image to HBM (16-byte stores)
+// The hand-offs are LDS counters (release/acquire at workgroup scope, LDS only); the two workgroup
+// barriers are LDS-only too, so no wave ever waits for its own global stores to drain.  Auto-resets
+// (rare) run after the second barrier.  The SoA state layout is shared with ch_kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include "ch_common.h"
+#include "ch_device.h"
+#include "ch_internal.h"
+
+namespace ch {
+
+// per-env integer scalars kept in LDS (index I * G + g)
+enum { I_N = 0, I_SC, I_SCA, I_HASPREV, I_LEVEL, I_TALLY, I_SPAWN, I_ACTIVE, I_EPISODE, I_FLOCK, I_RESET, I_COUNT };
+static_assert(I_COUNT == kV2EnvInts, "LDS env-int rows");
+enum { F_D = 0, F_T, F_H, F_A, F_E, F_Z };   // hand-off counters
+
+// index of unordered pair (i, j), i < j, in row-major upper-triangle order
+__device__ __forceinline__ int tri(int i, int j, int M) { return i * M - ((i * (i + 1)) >> 1) + (j - i - 1); }
+
+// q / d for 0 <= q < 2^22 without an integer divide
+__device__ __forceinline__ int qdiv(int q, int d, float rd) {
+    int r = (int)((float)q * rd);
+    int rem = q - r * d;
+    if (rem < 0) --r;
+    else if (rem >= d) ++r;
+    return r;
+}
+
+// workgroup barrier that orders LDS only (no wait for outstanding global stores)
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+// LDS writes of this wave visible to its other lanes
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+}
+// called convergently by a whole wave: its LDS writes are published, then the counter is bumped once
+__device__ __forceinline__ void lds_signal(int* f) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(f, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// spin until *f >= target (bounded: a broken hand-off ends the kernel with wrong data, never a hang)
+__device__ __forceinline__ void lds_wait(int* f, int target) {
+    int spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target && ++spins < (1 << 22))
+        __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// diagnostics: per-workgroup timestamps (slots: 0/1 wall clock at start/end, 2 shader clock at start,
+// 3 after the first barrier, 4 drone chain done, 5 reward terms done, 6 herded flags received,
+// 7 bookkeeping done, 8 cow waves: alpha rows done, 9 drone positions received, 10 velocity update
+// done, 11 obs copy done, 12 CU id, 13 second barrier, 14 end)
+#define TS(slot, val) do { if (p.tstamp) p.tstamp[(long long)blockIdx.x * 16 + (slot)] = (val); } while (0)
+
+template <class R>
+struct V2Smem {
+    R *cx, *cy, *cvx, *cvy, *aux, *auy;              // [G*M] positions after integration, pre-flock velocities, alpha
+    R *dx, *dy, *dz;                                 // [G*N] drone position after physics
+    R *pa, *pb, *sa, *sb, *ca, *cb, *scat, *psp;     // [G*N] per-drone reward terms
+    R* mrew;                                         // [G*N] MARL per-agent reward scratch
+    R* dcow;                                         // [G*N*M] cow-drone distances, (g*N + k)*M + j
+    R *prev, *clock;                                 // [G]
+    R *tgx, *tgy, *tcx, *tcy;                        // [G*P] alpha pair table
+    double* met;                                     // [kMetricRows*G]
+    float* img;                                      // [G][rows][86] observation image (output layout)
+    int* ei;                                         // [I_COUNT*G] + list [G] + 2 + flags
+    int* flags;
+    Level* LT;                                       // curriculum table (curriculum_learning.py:10-194)
+    uint8_t *pflag, *dflags, *herded, *md1, *md2;    // [G*P], [G*N], [G*M], [G*N], [G*N]
+
+    __device__ V2Smem(unsigned char* base, const V2Layout& L) {
+        const int GM = L.G * L.M, GN = L.G * L.N, GP = L.G * L.P;
+        cx = (R*)(base + L.off[V2Layout::CX]); cy = cx + GM; cvx = cy + GM; cvy = cvx + GM; aux = cvy + GM; auy = aux + GM;
+        dx = (R*)(base + L.off[V2Layout::DRONE]); dy = dx + GN; dz = dy + GN;
+        pa = dz + GN; pb = pa + GN; sa = pb + GN; sb = sa + GN; ca = sb + GN; cb = ca + GN; scat = cb + GN;
+        psp = scat + GN; mrew = psp + GN;
+        dcow = (R*)(base + L.off[V2Layout::DCOW]);
+        prev = (R*)(base + L.off[V2Layout::ENVR]); clock = prev + L.G;
+        tgx = (R*)(base + L.off[V2Layout::PAIRS]); tgy = tgx + GP; tcx = tgy + GP; tcy = tcx + GP;
+        met = (double*)(base + L.off[V2Layout::MET]);
+        img = (float*)(base + L.off[V2Layout::IMG]);
+        ei = (int*)(base + L.off[V2Layout::EI]);
+        flags = ei + I_COUNT * L.G + L.G + 2;
+        LT = (Level*)(base + L.off[V2Layout::LEVELS]);
+        pflag = base + L.off[V2Layout::BYTES]; dflags = pflag + GP; herded = dflags + GN; md1 = herded + GM;
+        md2 = md1 + GN;
+    }
+};
+
+// Copy the observation image of envs [0, Gv) (same layout as the output region) to HBM.
+__device__ __forceinline__ void copy_obs(float* out, const float* img, int Gv, int RW, int t0, int stride, bool vec4) {
+    const int total = Gv * RW;
+    if (vec4) {
+        const float4* s = reinterpret_cast<const float4*>(img);
+        float4* d = reinterpret_cast<float4*>(out);
+        for (int q = t0; q < (total >> 2); q += stride) d[q] = s[q];
+    } else {
+        const float2* s = reinterpret_cast<const float2*>(img);
+        float2* d = reinterpret_cast<float2*>(out);
+        for (int q = t0; q < (total >> 1); q += stride) d[q] = s[q];
+    }
+}
+
+// Copy (or clear, with out == nullptr) the images of the envs listed in rl[0..nr) between LDS and the
+// output; one env's block is RW floats at offset g*RW in both.  16-byte units when RW % 4 == 0 (then
+// every env block is 16-byte aligned), 8-byte units otherwise (86 is even).
+__device__ __forceinline__ void env_list_obs(float* out, float* img, const int* rl, int nr, int RW, int t0, int stride) {
+    if ((RW & 3) == 0) {
+        const int RW4 = RW >> 2;
+        const float rR = 1.0f / (float)RW4;
+        for (int q = t0; q < nr * RW4; q += stride) {
+            const int k = qdiv(q, RW4, rR), g = rl[k], o = g * RW4 + (q - k * RW4);
+            if (out) reinterpret_cast<float4*>(out)[o] = reinterpret_cast<const float4*>(img)[o];
+            else reinterpret_cast<float4*>(img)[o] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        }
+    } else {
+        const int RW2 = RW >> 1;
+        const float rR = 1.0f / (float)RW2;
+        for (int q = t0; q < nr * RW2; q += stride) {
+            const int k = qdiv(q, RW2, rR), g = rl[k], o = g * RW2 + (q - k * RW2);
+            if (out) reinterpret_cast<float2*>(out)[o] = reinterpret_cast<const float2*>(img)[o];
+            else reinterpret_cast<float2*>(img)[o] = make_float2(0.0f, 0.0f);
+        }
+    }
+}
+
+// own-state observation entries of drone row `row` of env g (BaseRLAviary.py:289-295)
+template <class R>
+__device__ __forceinline__ void img_own(float* img, int g, int rows, int row, R z, const R rpy[3], const R v[3],
+                                        const R w[3]) {
+    float* t = img + (g * rows + row) * 86;
+    reinterpret_cast<float2*>(t)[0] = make_float2((float)z, (float)rpy[0]);
+    reinterpret_cast<float2*>(t)[1] = make_float2((float)rpy[1], (float)rpy[2]);
+    reinterpret_cast<float2*>(t)[2] = make_float2((float)v[0], (float)v[1]);
+    reinterpret_cast<float2*>(t)[3] = make_float2((float)v[2], (float)w[0]);
+    reinterpret_cast<float2*>(t)[4] = make_float2((float)w[1], (float)w[2]);
+}
+
+// nearest-neighbour observation entries (columns 10..13) from the two nearest drones i1, i2
+template <class R>
+__device__ __forceinline__ void img_nbr(float* img, const R* dx, const R* dy, int g, int N, int rows, int i, int i1,
+                                        int i2) {
+    const int b0 = g * N;
+    const R xi = dx[b0 + i], yi = dy[b0 + i];
+    float2* t = reinterpret_cast<float2*>(img + (g * rows + i) * 86 + 10);
+    t[0] = i1 >= 0 ? make_float2((float)(dx[b0 + i1] - xi), (float)(dy[b0 + i1] - yi)) : make_float2(0.0f, 0.0f);
+    t[1] = i2 >= 0 ? make_float2((float)(dx[b0 + i2] - xi), (float)(dy[b0 + i2] - yi)) : make_float2(0.0f, 0.0f);
+}
+
+// two nearest drones of drone i in the reference's stable order (BaseRLAviary.py:303-317)
+template <class R>
+__device__ __forceinline__ void nearest_two(const R* dx, const R* dy, int b0, int i, int n, int& i1, int& i2) {
+    const R xi = dx[b0 + i], yi = dy[b0 + i];
+    R b1 = 0, b2 = 0;
+    i1 = -1; i2 = -1;
+    for (int j = 0; j < n; ++j) {
+        if (j == i) continue;
+        const R d = norm2(dx[b0 + j] - xi, dy[b0 + j] - yi);
+        if (i1 < 0 || d < b1) { i2 = i1; b2 = b1; i1 = j; b1 = d; }
+        else if (i2 < 0 || d < b2) { i2 = j; b2 = d; }
+    }
+}
+
+// cattle-relative observation entries of cow j for every live drone row (BaseRLAviary.py:319-331)
+template <class R>
+__device__ __forceinline__ void img_cattle(float* img, const R* dx, const R* dy, int g, int N, int rows, int j, int n,
+                                           int cat_off, R qx, R qy) {
+    const int b0 = g * N;
+    for (int r = 0; r < n; ++r)
+        reinterpret_cast<float2*>(img + (g * rows + r) * 86 + cat_off + 2 * j)[0] =
+            make_float2((float)(qx - dx[b0 + r]), (float)(qy - dy[b0 + r]));
+}
+
+// flock alpha term, pair form, for every flocking env (flockUtils.py:237-258, 327-337; MathUtils 11-58).
+// l = lane rank among the A lanes that share the table.
+template <class R>
+__device__ __forceinline__ void alpha_pairs(const StepParams<R>& p, V2Smem<R>& S, int G, int M, int P, int l, int A) {
+    const int nf = S.ei[I_COUNT * G + G];
+    const int* flist = S.ei + I_COUNT * G;
+    const R ra = sigma_norm_n(R(1.2)), da = ra;
+    const int tot = nf * P;
+    const float rP = 1.0f / (float)P;
+    auto one = [&](int q) {
+        const int f = qdiv(q, P, rP), r = q - f * P, g = flist[f];
+        const uint32_t pr = p.pairs[r];
+        const int bi = g * M + (pr & 0xff), bj = g * M + (pr >> 8);
+        const R zx = S.cx[bj] - S.cx[bi], zy = S.cy[bj] - S.cy[bi];
+        const R nrm = sqrt(zx * zx + zy * zy);
+        const int idx = g * P + r;
+        const bool in = nrm <= R(999);
+        S.pflag[idx] = in;
+        R gx = 0, gy = 0, cx = 0, cy = 0;
+        if (in) pair_terms_n(nrm, zx, zy, S.cvx[bi], S.cvy[bi], S.cvx[bj], S.cvy[bj], ra, da, gx, gy, cx, cy);
+        S.tgx[idx] = gx; S.tgy[idx] = gy; S.tcx[idx] = cx; S.tcy[idx] = cy;
+    };
+    for (int q = l; q < tot; q += 2 * A) {   // two independent pairs per iteration (instruction-level parallelism)
+        one(q);
+        if (q + A < tot) one(q + A);
+    }
+}
+
+// alpha row of cow u = g*M + j in neighbour order, scaled by c2_alpha (flockUtils.py:237-258)
+template <class R>
+__device__ __forceinline__ void alpha_row(V2Smem<R>& S, int M, int P, int u, int g, int j) {
+    const R C2A = R(2 * 1.7320508075688772);
+    R gx = 0, gy = 0, cxx = 0, cyy = 0, ux = 0, uy = 0;
+    int nb = 0;
+    const int pb = g * P;
+    for (int k = 0; k < M; ++k) {
+        if (k == j) continue;
+        const bool fwd = j < k;
+        const int idx = pb + (fwd ? tri(j, k, M) : tri(k, j, M));
+        if (!S.pflag[idx]) continue;
+        ++nb;
+        const R tgx = S.tgx[idx], tgy = S.tgy[idx], tcx = S.tcx[idx], tcy = S.tcy[idx];
+        gx += fwd ? tgx : -tgx; gy += fwd ? tgy : -tgy;
+        cxx += fwd ? tcx : -tcx; cyy += fwd ? tcy : -tcy;
+    }
+    if (nb > 0) { ux = C2A * gx + C2A * cxx; uy = C2A * gy + C2A * cyy; }
+    S.aux[u] = ux; S.auy[u] = uy;
+}
+
+// shepherd (delta, flockUtils.py:271-317), predator (343-348) and gamma (150-160, 340-341) terms and the
+// velocity update with the speed clip (BaseAviary.py:1384-1400) of cow u; |y_k - q_i| from the
+// distance table.  Four drones per batch, evaluated independently and accumulated in drone order.
+template <class R>
+__device__ __forceinline__ void cow_flock(const StepParams<R>& p, V2Smem<R>& S, int N, int M, int e0, int u, int g,
+                                          int j, int n) {
+    const long long CS = (long long)p.E * M;
+    const R C2B = R(2 * 4.47213595499958), C1G = R(5), C2G = R(0.2 * 2.23606797749979);
+    const R ra_b = sigma_norm_n(R(1.0)), da_b = ra_b;
+    const int b0 = g * N;
+    const R qix = S.cx[u], qiy = S.cy[u], pix = S.cvx[u], piy = S.cvy[u];
+    R ddx = 0, ddy = 0, sx = 0, sy = 0, gx = 0, gy = 0, cxx = 0, cyy = 0;
+    int nb = 0;
+    for (int k0 = 0; k0 < n; k0 += 4) {
+        R t[4][6];
+        bool in[4], pr[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const int k = min(k0 + v, n - 1);
+            const R yx = S.dx[b0 + k], yy = S.dy[b0 + k];
+            const R ex = yx - qix, ey = yy - qiy;
+            const R dn = S.dcow[(b0 + k) * M + j];   // = sqrt(ex * ex + ey * ey)
+            in[v] = dn <= R(999 + 2);
+            pr[v] = dn <= R(1.1);
+            t[v][0] = t[v][1] = t[v][2] = t[v][3] = t[v][4] = t[v][5] = 0;
+            if (in[v]) {
+                R difx = qix - yx, dify = qiy - yy;
+                R d = dn + R(1e-6);
+                R mu = d / R(1.0) < R(1.0) ? d / R(1.0) : R(1.0);
+                R akx = difx / d, aky = dify / d;
+                R P00 = R(1) - akx * akx, P01 = R(0) - akx * aky, P10 = R(0) - aky * akx, P11 = R(1) - aky * aky;
+                R qkx = mu * qix + (R(1) - mu) * yx, qky = mu * qiy + (R(1) - mu) * yy;
+                R pkx = mu * (P00 * pix + P01 * piy), pky = mu * (P10 * pix + P11 * piy);
+                pair_terms(qix, qiy, pix, piy, qkx, qky, pkx, pky, ra_b, da_b, t[v][0], t[v][1], t[v][2], t[v][3]);
+            }
+            if (pr[v]) {
+                R d3 = m_pow(dn, R(3.0));
+                t[v][4] = R(-650000.0) * ex / d3;
+                t[v][5] = R(-650000.0) * ey / d3;
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            if (k0 + v >= n) break;
+            if (in[v]) { ++nb; gx += t[v][0]; gy += t[v][1]; cxx += t[v][2]; cyy += t[v][3]; }
+            if (pr[v]) { sx += t[v][4]; sy += t[v][5]; }
+        }
+    }
+    if (nb > 0) { ddx = C2B * gx + C2B * cxx; ddy = C2B * gy + C2B * cyy; }
+    ddx += sx; ddy += sy;
+    R gmx = -C1G * sigma_1(qix - R(1)) - C2G * pix, gmy = -C1G * sigma_1(qiy - R(1)) - C2G * piy;
+    R qx = (S.aux[u] + ddx) + gmx, qy = (S.auy[u] + ddy) + gmy;
+    const R dt_sqr = R(0.05 * 0.05);
+    R vx = pix + qx * dt_sqr, vy = piy + qy * dt_sqr;
+    R sp = norm2(vx, vy);
+    if (sp > R(kMaxVelCattle)) { R f = R(kMaxVelCattle) / sp; vx *= f; vy *= f; }
+    const long long ci = (long long)e0 * M + u;
+    p.cattle[2 * CS + ci] = vx; p.cattle[3 * CS + ci] = vy;
+}
+
+// GT/NT/MT > 0 specialise the kernel for one geometry (envs per workgroup, drones, cattle): the LDS
+// carve and all index arithmetic then fold to immediates, which keeps the kernel within the SGPR file.
+template <class R, int MODE, int GT, int NT, int MT>
+__global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    constexpr bool marl = MODE == 1;
+    const int G = GT ? GT : p.G, N = NT ? NT : p.NC, M = MT ? MT : p.M, P = MT ? MT * (MT - 1) / 2 : p.P;
+    const int rows = marl ? N : 12;
+    const V2Layout L(G, N, M, P, MODE, (int)sizeof(R));
+    V2Smem<R> S(smem, L);
+    const int BS = blockDim.x, tid = threadIdx.x;
+    const int e0 = blockIdx.x * G;
+    const int Gv = min(G, p.E - e0);
+    const long long E = p.E, DS = E * N, CS = E * M;
+    const int m_obs = M < 16 ? M : 16, cat_off = marl ? 18 : 34, RW = rows * 86;
+    const bool task = !(p.phase_mask & 4);
+    const int W1 = (BS >> 6) - 1;   // cow waves (host guarantees BS >= 128)
+    const int ct = tid - 64, CW = BS - 64;
+    int* ei = S.ei;
+    int* fl = S.flags;
+    const Level* LT = S.LT;
+    if (tid == 0) { TS(0, (long long)wall_clock64()); TS(2, (long long)clock64()); TS(12, (long long)__smid()); }
+    if (tid < kV2Flags) fl[tid] = 0;
+    lds_barrier();   // hand-off counters cleared before anyone signals
+
+    // ---- phase 0: env scalars, drone prefetch (wave 0); cattle integration, image zero-fill (cow waves)
+    const int nd = Gv * N;
+    const bool dlane = tid < nd;
+    const int dg = dlane ? tid / N : 0, dk = tid - dg * N;
+    const long long di = (long long)e0 * N + tid;
+    R pos[3], q[4], v[3], w[3], pid[9];
+    int stepi = 0;
+    if (tid < 64) {
+        __builtin_amdgcn_s_setprio(3);   // the drone wave is the critical path: it wins issue on a shared SIMD
+        if (dlane) {
+            pos[0] = p.drone[0 * DS + di]; pos[1] = p.drone[1 * DS + di]; pos[2] = p.drone[2 * DS + di];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) q[c] = p.drone[(3 + c) * DS + di];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) { v[c] = p.drone[(7 + c) * DS + di]; w[c] = p.drone[(10 + c) * DS + di]; }
+#pragma unroll
+            for (int c = 0; c < 9; ++c) pid[c] = p.drone[(13 + c) * DS + di];
+            stepi = p.envi[9 * E + e0 + dg];   // ch_step calls on this env so far: the Philox action counter
+        }
+        for (int k = tid; k < (int)(sizeof(kLevels) / 4); k += 64)
+            reinterpret_cast<uint32_t*>(S.LT)[k] = reinterpret_cast<const uint32_t*>(kLevels)[k];
+        const int g = tid;
+        bool flk = false;
+        if (g < Gv) {
+            const int e = e0 + g;
+            const int scA = p.envi[2 * E + e] + 1;
+            flk = (scA % 2) == 0 && !(p.phase_mask & 2);
+            ei[I_N * G + g] = p.envi[0 * E + e]; ei[I_SC * G + g] = p.envi[1 * E + e]; ei[I_SCA * G + g] = scA;
+            ei[I_HASPREV * G + g] = p.envi[3 * E + e]; ei[I_LEVEL * G + g] = p.envi[4 * E + e];
+            ei[I_TALLY * G + g] = p.envi[5 * E + e]; ei[I_SPAWN * G + g] = p.envi[6 * E + e];
+            ei[I_ACTIVE * G + g] = p.envi[7 * E + e]; ei[I_EPISODE * G + g] = p.envi[8 * E + e];
+            ei[I_FLOCK * G + g] = flk; ei[I_RESET * G + g] = 0;
+            S.prev[g] = p.envr[e]; S.clock[g] = p.envr[E + e];
+#pragma unroll
+            for (int r = 0; r < kMetricRows; ++r) S.met[r * G + g] = p.metrics[r * E + e];
+        }
+        // compact list of flocking envs (BaseAviary.py:454: every second step_counter_A)
+        const unsigned long long bal = __ballot(flk);
+        if (flk) ei[I_COUNT * G + __popcll(bal & ((1ull << tid) - 1ull))] = g;
+        if (tid == 0) { ei[I_COUNT * G + G] = __popcll(bal); ei[I_COUNT * G + G + 1] = 0; }
+        lds_signal(fl + F_E);
+    } else {
+        for (int u = ct; u < Gv * M; u += CW) {
+            const long long ci = (long long)e0 * M + u;   // the workgroup's cows are contiguous per component
+            R x = p.cattle[0 * CS + ci], y = p.cattle[1 * CS + ci];
+            const R vx = p.cattle[2 * CS + ci], vy = p.cattle[3 * CS + ci];
+            const R dt = R(p.dt);
+            for (int s = 0; s < p.substeps; ++s) { x += vx * dt; y += vy * dt; }   // frictionless cube (trace-pinned)
+            p.cattle[0 * CS + ci] = x; p.cattle[1 * CS + ci] = y;
+            S.cx[u] = x; S.cy[u] = y; S.cvx[u] = vx; S.cvy[u] = vy;
+        }
+        float4* z4 = reinterpret_cast<float4*>(S.img);
+        const int n4 = (G * RW + 3) >> 2;
+        for (int k = ct; k < n4; k += CW) z4[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        lds_signal(fl + F_Z);
+        lds_wait(fl + F_E, 1);   // env scalars and the flocking list from the drone wave
+    }
+    if (tid == 0) TS(3, (long long)clock64());
+
+    const bool wobs = !(p.phase_mask & 8);
+    float* obs_wg = p.obs + (long long)e0 * RW;
+    const bool vec4 = (((long long)e0 * RW) & 3) == 0 && ((Gv * RW) & 3) == 0;
+
+    if (tid < 64) {
+        // ============ drone wave: the critical path ============================================
+        wave_sync();   // this wave's env scalars
+        const int n = dlane ? ei[I_N * G + dg] : 0;
+        const bool live = dlane && dk < n;
+        R rpy_out[3] = {0, 0, 0};
+        if (live) {
+            const int e = e0 + dg;
+            float a[4];
+            if (p.flags & CH_STEP_RANDOM_ACTIONS) {
+                uint32_t c4[4] = {(uint32_t)stepi, 0u, (uint32_t)dk, (uint32_t)(p.env_off + e)};
+                philox(c4, p.k0, p.k1);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) a[k] = (float)(c4[k] >> 8) * (1.0f / 16777216.0f) * 2.0f - 1.0f;
+                if (p.actions_out) reinterpret_cast<float4*>(p.actions_out)[di] = make_float4(a[0], a[1], a[2], a[3]);
+            } else {
+                float4 a4 = reinterpret_cast<const float4*>(p.actions)[di];
+                a[0] = a4.x; a[1] = a4.y; a[2] = a4.z; a[3] = a4.w;
+            }
+            if (marl && !((ei[I_ACTIVE * G + dg] >> dk) & 1)) { a[0] = a[1] = a[2] = a[3] = 0.0f; }  // marl_wrapper.py:80-84
+            R Rm[9], rpy[3];
+            quat_to_mat(q, Rm);
+            quat_to_euler(q, rpy);
+            if (!(p.phase_mask & 1)) {
+                R rpm[4];
+                pid_vel(pos, q, v, Rm, rpy, a, R(p.dt_ctrl), pid, rpm, p.debug ? p.debug + di * 16 : nullptr);
+                for (int s = 0; s < p.substeps; ++s)
+                    drone_substep(pos, q, v, w, rpm, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0);
+            }
+            R* D = p.drone;
+            D[0 * DS + di] = pos[0]; D[1 * DS + di] = pos[1]; D[2 * DS + di] = pos[2];
+            D[3 * DS + di] = q[0]; D[4 * DS + di] = q[1]; D[5 * DS + di] = q[2]; D[6 * DS + di] = q[3];
+            D[7 * DS + di] = v[0]; D[8 * DS + di] = v[1]; D[9 * DS + di] = v[2];
+            D[10 * DS + di] = w[0]; D[11 * DS + di] = w[1]; D[12 * DS + di] = w[2];
+#pragma unroll
+            for (int c = 0; c < 9; ++c) D[(13 + c) * DS + di] = pid[c];
+            quat_to_euler(q, rpy_out);
+            S.dx[tid] = pos[0]; S.dy[tid] = pos[1]; S.dz[tid] = pos[2];
+        }
+        lds_wait(fl + F_Z, W1);   // the cow waves have integrated the herd and zeroed the image
+        if (live) img_own(S.img, dg, rows, dk, pos[2], rpy_out, v, w);
+        wave_sync();
+        lds_signal(fl + F_D);
+        if (tid == 0) TS(4, (long long)clock64());
+
+        // per-drone reward terms (CattleAviary.py:230-246, 572-679) and neighbour obs (BaseRLAviary.py:303-317)
+        if (live && task) {
+            const int i = dk, b0 = dg * N;
+            const R xi = pos[0], yi = pos[1];
+            R m1 = R(INFINITY), m2 = R(INFINITY), b1 = 0, b2 = 0;
+            int i1 = -1, i2 = -1;
+            uint8_t f = 0;
+            bool iso = true;
+            for (int j = 0; j < n; ++j) {
+                if (j == i) continue;
+                const R d = norm2(S.dx[b0 + j] - xi, S.dy[b0 + j] - yi);
+                if (d != d) f |= 8;
+                if (d < m1) { m2 = m1; m1 = d; } else if (d < m2) m2 = d;
+                if (d < R(kCollision)) f |= 2;
+                if (!(d > R(kMaxFormation))) iso = false;
+                if (i1 < 0 || d < b1) { i2 = i1; b2 = b1; i1 = j; b1 = d; }
+                else if (i2 < 0 || d < b2) { i2 = j; b2 = d; }
+            }
+            if (iso) f |= 4;
+            if (fabs(pos[2] - R(kTargetAlt)) > R(kTargetAlt * 0.6)) f |= 1;
+            const Level& Lv = LT[ei[I_LEVEL * G + dg]];
+            const R sa = simple_spacing(m1, Lv), sb = simple_spacing(m2, Lv);
+            const R ca = complex_spacing(m1, Lv), cb = complex_spacing(m2, Lv);
+            R ps = 0;   // per-drone spacing reward (CattleAviary.py:238-246)
+            if (p.compat || m1 < R(INFINITY)) ps += (ca + sa) / R(2.0);
+            if (p.compat || m2 < R(INFINITY)) ps += (cb + sb) / R(2.0);
+            S.pa[tid] = m1; S.pb[tid] = m2; S.dflags[tid] = f;
+            S.sa[tid] = sa; S.sb[tid] = sb; S.ca[tid] = ca; S.cb[tid] = cb; S.psp[tid] = ps;
+            img_nbr(S.img, S.dx, S.dy, dg, N, rows, i, i1, i2);
+        }
+        lds_signal(fl + F_T);
+        if (tid == 0) TS(5, (long long)clock64());
+        lds_wait(fl + F_H, W1);
+        if (tid == 0) TS(6, (long long)clock64());
+        if (live && task) {
+            // closest cow (CattleAviary.py:248-252) from the cow waves' distance table -> cattle term
+            const R* dc = S.dcow + tid * M;
+            R best = R(INFINITY);
+            for (int j = 0; j < M; ++j) {
+                const R d = dc[j];
+                if (d < best) best = d;
+            }
+            S.scat[tid] = cattle_spacing(best, R(p.cs_cc));
+        }
+        wave_sync();
+
+        // per-env bookkeeping, one env per lane, in the reference's call order
+        const int g = tid;
+        if (g < Gv && task) {
+            const int e = e0 + g, n = ei[I_N * G + g], b0 = g * N, c0 = g * M;
+            int sc = ei[I_SC * G + g], has_prev = ei[I_HASPREV * G + g], level = ei[I_LEVEL * G + g];
+            int tally = ei[I_TALLY * G + g], active = ei[I_ACTIVE * G + g];
+            R prev = S.prev[g], clock = S.clock[g];
+            R scx = 0, scy = 0, sdx = 0, sdy = 0;
+            int herded = 0;
+            for (int j = 0; j < M; ++j) { scx += S.cx[c0 + j]; scy += S.cy[c0 + j]; herded += S.herded[c0 + j]; }
+            for (int i = 0; i < n; ++i) { sdx += S.dx[b0 + i]; sdy += S.dy[b0 + i]; }
+            scx /= R(M); scy /= R(M); sdx /= R(n); sdy /= R(n);
+            R ex = sdx - scx, ey = sdy - scy;
+            const R cent = sqrt(ex * ex + ey * ey + R(0) * R(0));   // HerdCentroid/DroneCentroid, z = 0.95 both
+            const R eff = R((double)herded / M * 100);
+            R ms = R(INFINITY);
+            bool anynan = false;
+            uint8_t any = 0;
+            for (int i = 0; i < n; ++i) {
+                if (S.pa[b0 + i] < ms) ms = S.pa[b0 + i];
+                anynan |= (S.dflags[b0 + i] & 8) != 0;
+                any |= S.dflags[b0 + i];
+            }
+            if (anynan) ms = R(NAN);
+            const R max_step = R(0.3 * kMaxSpeedKmh * (1000.0 / 3600.0)) / R(p.ctrl_freq);
+            const bool time_up = (double)sc / p.ctrl_freq > p.episode_len;
+            int done = 0;
+            double ret = 0;
+            int n_term = 0, n_trunc = 0, n_nan = 0;
+            if constexpr (!marl) {
+                // CattleAviary._computeReward (CattleAviary.py:213-332) then terminated / truncated twice
+                const Level& Lv = LT[level];
+                R sp_simple = 0, sp_complex = 0, msp = 0, mcat = 0, cat = 0;
+                for (int i = 0; i < n; ++i) {
+                    if (p.compat || S.pa[b0 + i] < R(INFINITY)) { sp_complex += S.ca[b0 + i]; sp_simple += S.sa[b0 + i]; }
+                    if (p.compat || S.pb[b0 + i] < R(INFINITY)) { sp_complex += S.cb[b0 + i]; sp_simple += S.sb[b0 + i]; }
+                }
+                sp_complex /= R(n * 2.0); sp_simple /= R(n * 2.0);
+                R approach = 0;
+                if (has_prev) approach = clip(((prev - cent) / (max_step + R(1e-6))) * R(5), R(-1.0), R(1.0));
+                prev = cent; has_prev = 1;
+                for (int i = 0; i < n; ++i) cat += S.scat[b0 + i];
+                cat /= R(n);
+                R rg = sp_simple * R(Lv.w_simple) + sp_complex * R(Lv.w_complex) + R(0.1) * R(Lv.w_survival) +
+                       approach * R(Lv.w_approach) + (eff / R(100)) * R(Lv.w_eff) + cat * R(Lv.w_cattle);
+                for (int i = 0; i < n; ++i) { msp += S.psp[b0 + i]; mcat += S.scat[b0 + i]; }
+                msp /= R(n); mcat /= R(n);
+                R tot = 0;
+                for (int i = 0; i < n; ++i) tot += rg + R(0.5) * ((S.psp[b0 + i] - msp) + (S.scat[b0 + i] - mcat));
+                R rew = tot / R(n);
+                const R inc = R(1.0 / 240);
+                bool te = term_call(LT, level, clock, inc, ms, cent, eff);
+                if (te) curriculum_success(LT, level, tally);
+                bool te2 = term_call(LT, level, clock, inc, ms, cent, eff);
+                bool tr = (any & 7) || cent > R(kMissionBoundary) || time_up;
+                p.reward[e] = (float)rew;
+                p.term[e] = te2; p.trunc[e] = tr;
+                done = te2 || tr;
+                ret = (double)rew;
+                n_term = te2; n_trunc = tr; n_nan = rew != rew;
+            } else {
+                // MARLCattleAviary reward / terminated / truncated in the order env.step
+                // (rllib_envs/BaseAviary.py:425-431) and the wrapper (marl_wrapper.py:104-113) call them
+                const R inc = R(1.0) / R(p.ctrl_freq);
+                const int lvl0 = level;
+                auto trunc_i = [&](int i) -> bool {
+                    return (S.dflags[b0 + i] & 7) || cent > R(kMissionBoundary) || time_up;
+                };
+                auto reward_i = [&](int i) -> R {
+                    const Level& Lv = LT[level];
+                    R a = S.pa[b0 + i], b = S.pb[b0 + i];
+                    R sa, sb, ca, cb;
+                    if (level == lvl0) { sa = S.sa[b0 + i]; sb = S.sb[b0 + i]; ca = S.ca[b0 + i]; cb = S.cb[b0 + i]; }
+                    else { sa = simple_spacing(a, Lv); sb = simple_spacing(b, Lv); ca = complex_spacing(a, Lv); cb = complex_spacing(b, Lv); }
+                    R simple = (sa + sb) / R(2), cplx = (ca + cb) / R(2);
+                    if (!p.compat) {
+                        if (!(b < R(INFINITY))) { simple = sa; cplx = ca; }
+                        if (!(a < R(INFINITY))) { simple = 0; cplx = 0; }
+                    }
+                    R r = 0;
+                    r += simple * R(Lv.w_simple);
+                    r += cplx * R(Lv.w_complex);
+                    r += R(0.1) * R(Lv.w_survival);
+                    R change = has_prev ? prev - cent : R(0.0);
+                    prev = cent; has_prev = 1;
+                    r += clip((change / (max_step + R(1e-6))) * R(5), R(-1.0), R(1.0)) * R(Lv.w_approach);
+                    r += (eff / R(100)) * R(Lv.w_eff);
+                    r += S.scat[b0 + i] * R(Lv.w_cattle);
+                    if (term_call(LT, level, clock, inc, ms, cent, eff)) {
+                        r += marl_end_of_episode(LT, level, a, b, cent, eff, norm2(scx - S.dx[b0 + i], scy - S.dy[b0 + i]), n);
+                        curriculum_success(LT, level, tally);
+                    } else if (trunc_i(i)) {
+                        r -= R(50);
+                    }
+                    return r;
+                };
+                // env.step's own dicts (rllib_envs/BaseAviary.py:425-431)
+                for (int i = 0; i < n; ++i) S.mrew[b0 + i] = reward_i(i);
+                for (int i = 0; i < n; ++i) S.md1[b0 + i] = term_call(LT, level, clock, inc, ms, cent, eff);
+                const int act0 = active;
+                if (p.marl_wrapper) {
+                    // the wrapper recomputes everything per live agent (marl_wrapper.py:104-110)
+                    done = 1;
+                    for (int i = 0; i < N; ++i) {
+                        R rr = R(NAN);
+                        uint8_t tt = 0, trr = 0;
+                        if (i < n && ((act0 >> i) & 1)) {
+                            rr = reward_i(i);
+                            tt = term_call(LT, level, clock, inc, ms, cent, eff);
+                            trr = trunc_i(i);
+                        }
+                        p.reward[(long long)e * N + i] = (float)rr;
+                        p.term[(long long)e * N + i] = tt;
+                        p.trunc[(long long)e * N + i] = trr;
+                        if (i < n && rr == rr) ret += (double)rr;
+                        n_term += tt; n_trunc += trr;
+                        if (i < n && (((act0 >> i) & 1) || tt) && rr != rr) n_nan += 1;
+                        if (i < n && ((act0 >> i) & 1) && tt) active &= ~(1 << i);   // finished agents drop out
+                    }
+                    for (int i = 0; i < n; ++i)
+                        if ((active >> i) & 1) done = 0;   // __all__: every agent terminated (marl_wrapper.py:113-117)
+                } else {
+                    done = 1;   // bare env.step dicts: __all__ = all(done.values())
+                    for (int i = 0; i < N; ++i) {
+                        R rr = R(NAN);
+                        uint8_t tt = 0, trr = 0;
+                        if (i < n) { rr = S.mrew[b0 + i]; tt = S.md1[b0 + i]; trr = trunc_i(i); done &= tt; }
+                        p.reward[(long long)e * N + i] = (float)rr;
+                        p.term[(long long)e * N + i] = tt;
+                        p.trunc[(long long)e * N + i] = trr;
+                        if (i < n && rr == rr) ret += (double)rr;
+                        n_term += tt; n_trunc += trr;
+                        if (i < n && (((act0 >> i) & 1) || tt) && rr != rr) n_nan += 1;
+                    }
+                }
+            }
+            sc += marl ? 1 : p.substeps;
+            // metric accumulators (rank-local; bench.py all-reduces them)
+            const double* mt = S.met;
+            double o[kMetricRows];
+#pragma unroll
+            for (int r = 0; r < kMetricRows; ++r) o[r] = mt[r * G + g];
+            o[CH_METRIC_STEPS] += 1;
+            o[CH_METRIC_TERMINATED] += n_term;
+            o[CH_METRIC_TRUNCATED] += n_trunc;
+            o[CH_METRIC_NAN_REWARDS] += n_nan;
+            o[CH_METRIC_EFFECTIVENESS_SUM] += (double)eff;
+            o[kMetricCurReturn] += ret;
+            o[kMetricCurLen] += 1;
+            if (done) {
+                o[CH_METRIC_EPISODES] += 1;
+                o[CH_METRIC_RETURN_SUM] += o[kMetricCurReturn];
+                o[CH_METRIC_LENGTH_SUM] += o[kMetricCurLen];
+                o[kMetricCurReturn] = 0;
+                o[kMetricCurLen] = 0;
+            }
+#pragma unroll
+            for (int r = 0; r < kMetricRows; ++r) p.metrics[r * E + e] = o[r];
+            const int rs = done && (p.flags & CH_STEP_AUTORESET);
+            ei[I_SC * G + g] = sc; ei[I_HASPREV * G + g] = has_prev; ei[I_LEVEL * G + g] = level;
+            ei[I_TALLY * G + g] = tally; ei[I_ACTIVE * G + g] = active; ei[I_RESET * G + g] = rs;
+            S.prev[g] = prev; S.clock[g] = clock;
+            if (p.reset_happened) p.reset_happened[e] = rs;
+            if (p.agent_active && !rs)
+                for (int i = 0; i < N; ++i) p.agent_active[(long long)e * N + i] = (active >> i) & 1;
+        } else if (g < Gv && p.reset_happened) {
+            p.reset_happened[e0 + g] = 0;
+        }
+        // compact list of the envs that auto-reset in this launch (the reset phase walks only these)
+        const bool rs_lane = g < Gv && ei[I_RESET * G + g];
+        const unsigned long long rbal = __ballot(rs_lane);
+        if (rs_lane) ei[I_COUNT * G + __popcll(rbal & ((1ull << g) - 1ull))] = g;
+        if (tid == 0) ei[I_COUNT * G + G + 1] = __popcll(rbal);
+        if (tid == 0) TS(7, (long long)clock64());
+    } else {
+        // ============ cow waves ================================================================
+        alpha_pairs(p, S, G, M, P, ct, CW);
+        lds_signal(fl + F_A);
+        lds_wait(fl + F_A, W1);
+        const float rM = 1.0f / (float)M;
+        for (int u = ct; u < Gv * M; u += CW) {
+            const int g = qdiv(u, M, rM);
+            if (ei[I_FLOCK * G + g]) alpha_row(S, M, P, u, g, u - g * M);
+        }
+        if (ct == 0) TS(8, (long long)clock64());
+        lds_wait(fl + F_D, 1);
+        if (ct == 0) TS(9, (long long)clock64());
+        for (int u = ct; u < Gv * M; u += CW) {
+            const int g = qdiv(u, M, rM), j = u - g * M;
+            const int n = ei[I_N * G + g], b0 = g * N;
+            const R qix = S.cx[u], qiy = S.cy[u];
+            for (int k = 0; k < n; ++k) {   // |y_k - q_j| for the shepherd term and the closest-cow search
+                const R ex = S.dx[b0 + k] - qix, ey = S.dy[b0 + k] - qiy;
+                S.dcow[(b0 + k) * M + j] = sqrt(ex * ex + ey * ey);
+            }
+            if (task) {
+                // evaluate_herding_effectiveness winding number (evaluation.py:100-138)
+                int wn = 0;
+                for (int i = 0; i < n; ++i) {
+                    int i2 = (i + 1 == n) ? 0 : i + 1;
+                    R x1 = S.dx[b0 + i], y1 = S.dy[b0 + i], x2 = S.dx[b0 + i2], y2 = S.dy[b0 + i2];
+                    R il = (x2 - x1) * (qiy - y1) - (qix - x1) * (y2 - y1);
+                    if (y1 <= qiy) { if (y2 > qiy && il > R(0)) wn += 1; }
+                    else { if (y2 <= qiy && il < R(0)) wn -= 1; }
+                }
+                S.herded[u] = wn != 0;
+            }
+            if (j < m_obs) img_cattle(S.img, S.dx, S.dy, g, N, rows, j, n, cat_off, qix, qiy);
+        }
+        lds_signal(fl + F_H);
+        for (int u = ct; u < Gv * M; u += CW) {
+            const int g = qdiv(u, M, rM);
+            if (ei[I_FLOCK * G + g]) cow_flock(p, S, N, M, e0, u, g, u - g * M, ei[I_N * G + g]);
+        }
+        if (ct == 0) TS(10, (long long)clock64());
+        lds_wait(fl + F_T, 1);    // neighbour entries of the drone wave
+        lds_wait(fl + F_H, W1);   // cattle entries of every cow wave
+        if (wobs) copy_obs(obs_wg, S.img, Gv, RW, ct, CW, vec4);
+        if (ct == 0) TS(11, (long long)clock64());
+    }
+    lds_barrier();
+    if (tid == 0) TS(13, (long long)clock64());
+
+    // ---- auto-reset of finished envs (SB3 VecEnv semantics) --------------------------------------
+    const int nr = ei[I_COUNT * G + G + 1];
+    if (nr) {   // uniform: read after the barrier
+        const int* rl = ei + I_COUNT * G;
+        if (p.terminal_obs)   // info["terminal_observation"]: the pre-reset observation
+            env_list_obs(p.terminal_obs + (long long)e0 * RW, S.img, rl, nr, RW, tid, BS);
+        if (tid < nr) {
+            const int g = rl[tid], e = e0 + g;
+            int n = ei[I_N * G + g], sc = ei[I_SC * G + g], scA = ei[I_SCA * G + g], spawn = ei[I_SPAWN * G + g];
+            int episode = ei[I_EPISODE * G + g], active = ei[I_ACTIVE * G + g], has_prev = ei[I_HASPREV * G + g];
+            R prev = S.prev[g], clock = S.clock[g];
+            reset_scalars(p, e, n, sc, scA, spawn, episode, active, has_prev, prev, clock);
+            ei[I_N * G + g] = n; ei[I_SC * G + g] = sc; ei[I_SCA * G + g] = scA; ei[I_SPAWN * G + g] = spawn;
+            ei[I_EPISODE * G + g] = episode; ei[I_ACTIVE * G + g] = active; ei[I_HASPREV * G + g] = has_prev;
+            S.prev[g] = prev; S.clock[g] = clock;
+            if (p.agent_active)
+                for (int i = 0; i < N; ++i) p.agent_active[(long long)e * N + i] = (active >> i) & 1;
+        }
+        lds_barrier();
+        env_list_obs(nullptr, S.img, rl, nr, RW, tid, BS);   // clear the images of the envs being reset
+        const float rN = 1.0f / (float)N, rM = 1.0f / (float)M;
+        for (int u = tid; u < nr * N; u += BS) {
+            const int k0 = qdiv(u, N, rN), g = rl[k0], k = u - k0 * N, ud = g * N + k;
+            const int n = ei[I_N * G + g];
+            R x, y, z;
+            reset_drone(p, (long long)e0 * N + ud, k, n, x, y, z);
+            S.dx[ud] = x; S.dy[ud] = y; S.dz[ud] = z;
+        }
+        for (int u = tid; u < nr * M; u += BS) {
+            const int k0 = qdiv(u, M, rM), g = rl[k0], j = u - k0 * M, uc = g * M + j;
+            R x, y, vx, vy;
+            reset_cow(p, (long long)e0 * M + uc, p.env_off + e0 + g, j, ei[I_SPAWN * G + g],
+                      (uint32_t)(ei[I_EPISODE * G + g] - 1), x, y, vx, vy);
+            S.cx[uc] = x; S.cy[uc] = y;
+        }
+        lds_barrier();
+        for (int u = tid; u < nr * N; u += BS) {
+            const int k0 = qdiv(u, N, rN), g = rl[k0], i = u - k0 * N, ud = g * N + i;
+            const int n = ei[I_N * G + g];
+            if (i >= n) continue;
+            // identity quaternion (getEulerFromQuaternion -> 0), zero velocities
+            const R qid[4] = {0, 0, 0, 1}, zero3[3] = {0, 0, 0};
+            R rpy0[3];
+            quat_to_euler(qid, rpy0);
+            img_own(S.img, g, rows, i, S.dz[ud], rpy0, zero3, zero3);
+            int i1, i2;
+            nearest_two(S.dx, S.dy, g * N, i, n, i1, i2);
+            img_nbr(S.img, S.dx, S.dy, g, N, rows, i, i1, i2);
+        }
+        for (int u = tid; u < nr * M; u += BS) {
+            const int k0 = qdiv(u, M, rM), g = rl[k0], j = u - k0 * M, uc = g * M + j;
+            if (j < m_obs) img_cattle(S.img, S.dx, S.dy, g, N, rows, j, ei[I_N * G + g], cat_off, S.cx[uc], S.cy[uc]);
+        }
+        lds_barrier();
+        if (wobs) env_list_obs(obs_wg, S.img, rl, nr, RW, tid, BS);
+    }
+
+    // ---- env scalars back to HBM -----------------------------------------------------------------
+    if (tid < Gv && wobs) {
+        const int g = tid, e = e0 + g;
+        p.envi[0 * E + e] = ei[I_N * G + g]; p.envi[1 * E + e] = ei[I_SC * G + g]; p.envi[2 * E + e] = ei[I_SCA * G + g];
+        p.envi[3 * E + e] = ei[I_HASPREV * G + g]; p.envi[4 * E + e] = ei[I_LEVEL * G + g];
+        p.envi[5 * E + e] = ei[I_TALLY * G + g]; p.envi[6 * E + e] = ei[I_SPAWN * G + g];
+        p.envi[7 * E + e] = ei[I_ACTIVE * G + g]; p.envi[8 * E + e] = ei[I_EPISODE * G + g];
+        p.envi[9 * E + e] += 1;   // ch_step calls on this env
+        p.envr[0 * E + e] = S.prev[g]; p.envr[1 * E + e] = S.clock[g];
+    }
+    if (tid == 0) { TS(14, (long long)clock64()); TS(1, (long long)wall_clock64()); }
+}
+
+template <class R, int MODE, int GT, int NT, int MT>
+static hipError_t launch_v2_kernel(const StepParams<R>& p, int block, size_t lds, hipStream_t st) {
+    static bool attr_set = false;   // one-time opt-in to > 64 KiB of dynamic LDS
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_step2<R, MODE, GT, NT, MT>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    dim3 grid((p.E + p.G - 1) / p.G);
+    hipLaunchKernelGGL((k_step2<R, MODE, GT, NT, MT>), grid, dim3(block), lds, st, p);
+    return hipGetLastError();
+}
+
+// geometry specialisations: the BASELINE configs at their default geometry (ch_api.cpp)
+template <class R>
+hipError_t launch_step_v2(const StepParams<R>& p, int block, size_t lds, hipStream_t st) {
+    const int G = p.G, N = p.NC, M = p.M;
+    if (p.mode == 1) {
+        if (G == 4 && N == 4 && M == 32) return launch_v2_kernel<R, 1, 4, 4, 32>(p, block, lds, st);     // configs[4]
+        return launch_v2_kernel<R, 1, 0, 0, 0>(p, block, lds, st);
+    }
+    if (G == 8 && N == 4 && M == 16) return launch_v2_kernel<R, 0, 8, 4, 16>(p, block, lds, st);          // configs[3]
+    if (G == 16 && N == 2 && M == 8) return launch_v2_kernel<R, 0, 16, 2, 8>(p, block, lds, st);          // configs[2]
+    if (G == 4 && N == 2 && M == 8) return launch_v2_kernel<R, 0, 4, 2, 8>(p, block, lds, st);            // configs[1]
+    return launch_v2_kernel<R, 0, 0, 0, 0>(p, block, lds, st);
+}
+
+template hipError_t launch_step_v2<double>(const StepParams<double>&, int, size_t, hipStream_t);
+template hipError_t launch_step_v2<float>(const StepParams<float>&, int, size_t, hipStream_t);
+
+}  // namespace ch

@@ -24,18 +24,25 @@ def time_launches(b, k=200):
 
 
 def main():
-    configs = [("ctde", 4096, 4, 16), ("ctde", 4096, 2, 8), ("marl", 4096, 4, 32)]
+    import ctypes
+    configs = [("ctde", 4096, 4, 16), ("ctde", 4096, 2, 8), ("marl", 4096, 4, 32), ("ctde", 1024, 2, 8)]
     masks = [(0, "full"), (1, "-drones"), (2, "-flock"), (4, "-task"), (8, "-obs"), (1 | 2 | 4 | 8, "loads/stores only")]
     for prec in ("f64", "f32"):
         for mode, E, n, m in configs:
-            b = HerdBatch(E, n, m, mode=mode, precision=prec)
-            b.reset()
-            row = []
-            for mask, name in masks:
-                _lib.lib().ch__set_phase_mask(b.handle, mask)
-                row.append(f"{name}={time_launches(b):.1f}us")
-            print(prec, mode, E, n, m, " ".join(row), flush=True)
-            b.close()
+            for kern in (1, 2):
+                b = HerdBatch(E, n, m, mode=mode, precision=prec)
+                if _lib.lib().ch__set_kernel(b.handle, ctypes.c_int32(kern)) != 0:
+                    continue
+                g, blk, lds, kv = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int32()
+                _lib.lib().ch__geometry(b.handle, ctypes.byref(g), ctypes.byref(blk), ctypes.byref(lds), ctypes.byref(kv))
+                b.reset()
+                row = []
+                for mask, name in masks:
+                    _lib.lib().ch__set_phase_mask(b.handle, mask)
+                    row.append(f"{name}={time_launches(b):.1f}us")
+                print(f"v{kern}", prec, mode, E, n, m, f"G={g.value} block={blk.value} lds={lds.value}", " ".join(row),
+                      flush=True)
+                b.close()
 
 
 if __name__ == "__main__":

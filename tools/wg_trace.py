@@ -1,0 +1,118 @@
+"""Diagnostics: per-workgroup phase timestamps of the v2 step kernel (ch__set_tstamp).
+
+For a few consecutive steps: kernel span on the 100 MHz wall clock, spread of workgroup start times
+(dispatch), per-workgroup duration, and mean shader cycles per phase."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "rl-cattle-herding_amd"))
+import torch  # noqa: E402
+from cattleherd import _lib  # noqa: E402
+from cattleherd.env import HerdBatch  # noqa: E402
+
+
+def trace(mode, E, n, m, prec, G=None, B=None, steps=4):
+    L = _lib.lib()
+    b = HerdBatch(E, n, m, mode=mode, precision=prec)
+    if G is not None:
+        assert L.ch__set_geometry(b.handle, ctypes.c_int32(G), ctypes.c_int32(B)) == 0
+    g, blk, lds, kv = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int32()
+    L.ch__geometry(b.handle, ctypes.byref(g), ctypes.byref(blk), ctypes.byref(lds), ctypes.byref(kv))
+    grid = (E + g.value - 1) // g.value
+    ts = torch.zeros((grid, 16), dtype=torch.int64, device=b.device)
+    b.reset()
+    for _ in range(250):   # steady state: resets have desynchronised the flocking parity
+        b.step(random_actions=True, autoreset=True, terminal_obs=False)
+    L.ch__set_tstamp(b.handle, ctypes.c_void_p(ts.data_ptr()))
+    print(f"== {prec} {mode} E={E} N={n} M={m} G={g.value} block={blk.value} lds={lds.value} grid={grid}")
+    for s in range(steps):
+        ts.zero_()
+        torch.cuda.synchronize()
+        b.step(random_actions=True, autoreset=True, terminal_obs=False)
+        torch.cuda.synchronize()
+        t = ts.cpu().numpy()
+        w0, w1 = t[:, 0], t[:, 1]
+        span_us = (w1.max() - w0.min()) / 100.0
+        start = (w0 - w0.min()) / 100.0
+        dur = (w1 - w0) / 100.0
+        cyc = t[:, 14] - t[:, 2]
+        clk = (cyc / np.maximum(dur, 1e-3)).mean() / 1e3
+        cus = len(np.unique(t[:, 12]))
+        rel = lambda k: (t[:, k] - t[:, 2]).mean()  # noqa: E731
+        print(f" step {s}: span {span_us:.1f}us | WG start q50/q90/max {np.percentile(start, 50):.1f}/"
+              f"{np.percentile(start, 90):.1f}/{start.max():.1f}us | WG dur mean/max {dur.mean():.1f}/{dur.max():.1f}us"
+              f" | ~{clk:.2f} GHz | CUs {cus}")
+        print(f"   drone wave (cycles from start): B0 {rel(3):.0f} chain {rel(4):.0f} terms {rel(5):.0f} "
+              f"H {rel(6):.0f} book {rel(7):.0f} | cow waves: alpha {rel(8):.0f} D {rel(9):.0f} flock {rel(10):.0f} "
+              f"copy {rel(11):.0f} | B1 {rel(13):.0f} end {rel(14):.0f}")
+    L.ch__set_tstamp(b.handle, None)
+    b.close()
+
+
+def main():
+    precs = sys.argv[1:] or ["f64"]
+    for prec in precs:
+        trace("ctde", 4096, 4, 16, prec)
+        trace("ctde", 4096, 4, 16, prec, 4, 128)
+        trace("ctde", 4096, 4, 16, prec, 8, 256)
+        trace("ctde", 4096, 4, 16, prec, 4, 256)
+        trace("ctde", 4096, 2, 8, prec, 4, 128)
+
+
+
+def host_rate(mode="ctde", E=4096, n=4, m=16, prec="f64", k=500):
+    """Host submission cost per step (loop without sync) vs. the synchronised per-step time."""
+    import time
+    b = HerdBatch(E, n, m, mode=mode, precision=prec)
+    b.reset()
+    for _ in range(50):
+        b.step(random_actions=True, autoreset=True, terminal_obs=False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(k):
+        b.step(random_actions=True, autoreset=True, terminal_obs=False)
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    print(f"host submit {1e6 * (t1 - t0) / k:.1f} us/step, synchronised {1e6 * (t2 - t0) / k:.1f} us/step")
+    b.close()
+
+
+
+def back_to_back(mode="ctde", E=4096, n=4, m=16, prec="f64", k=12):
+    """Timestamps of k back-to-back launches: per-kernel span and the gap to the previous kernel."""
+    L = _lib.lib()
+    b = HerdBatch(E, n, m, mode=mode, precision=prec)
+    g, blk, lds, kv = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int32()
+    L.ch__geometry(b.handle, ctypes.byref(g), ctypes.byref(blk), ctypes.byref(lds), ctypes.byref(kv))
+    grid = (E + g.value - 1) // g.value
+    ts = torch.zeros((k, grid, 16), dtype=torch.int64, device=b.device)
+    b.reset()
+    for _ in range(250):
+        b.step(random_actions=True, autoreset=True, terminal_obs=False)
+    torch.cuda.synchronize()
+    for i in range(k):
+        L.ch__set_tstamp(b.handle, ctypes.c_void_p(ts[i].data_ptr()))
+        b.step(random_actions=True, autoreset=True, terminal_obs=False)
+    torch.cuda.synchronize()
+    L.ch__set_tstamp(b.handle, None)
+    t = ts.cpu().numpy()
+    prev_end = None
+    for i in range(k):
+        w0, w1 = t[i, :, 0].min(), t[i, :, 1].max()
+        gap = "" if prev_end is None else f" gap {(w0 - prev_end) / 100.0:.1f}us"
+        nres = int((t[i, :, 6] != 0).sum())
+        print(f" kernel {i}: span {(w1 - w0) / 100.0:.1f}us{gap} | WG dur max {(t[i, :, 1] - t[i, :, 0]).max() / 100.0:.1f}us")
+        prev_end = w1
+    b.close()
+
+
+if __name__ == "__main__":
+    host_rate()
+    back_to_back()
+    if len(sys.argv) > 1:
+        main()
