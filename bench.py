@@ -28,6 +28,7 @@ WORKLOADS = {
     "c5": ("marl", 4096, 4, 32, "BASELINE configs[4]: 4096 envs x (4 drones, 32 cattle), MARL per-agent obs (4,86)"),
 }
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PROFILES = os.path.join(ROOT, "profiles")
 
 
 def algorithmic_bytes(mode, n, m, rows, real_bytes):
@@ -41,6 +42,29 @@ def algorithmic_bytes(mode, n, m, rows, real_bytes):
     k = 1 if mode == "ctde" else n
     flags = 4 * k + 2 * k + n + 1                     # reward, terminated, truncated, agent_active, reset flag
     return drone + actions + cattle + env + metrics + obs + flags
+
+
+def pmc_traffic(workload, dtype):
+    """HBM bytes per launch of the step kernel from the newest committed rocprofv3 --pmc pass
+    (profiles/rNN/traffic_<workload>_<dtype>.json, written by tools/parse_pmc.py), or None."""
+    import glob
+    hits = sorted(glob.glob(os.path.join(PROFILES, "r*", f"traffic_{workload}_{dtype}.json")))
+    if not hits:
+        return None, None
+    with open(hits[-1]) as fh:
+        d = json.load(fh)
+    return d.get("traffic_bytes_per_launch"), os.path.relpath(hits[-1], ROOT)
+
+
+def kernel_name(b):
+    """Which step kernel the handle launches (internal diagnostics entry point)."""
+    import ctypes
+    from cattleherd import _lib
+    g, blk, lds, kv = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int32()
+    _lib.lib().ch__geometry(b.handle, ctypes.byref(g), ctypes.byref(blk), ctypes.byref(lds), ctypes.byref(kv))
+    if kv.value == 2:
+        return f"ch::k_step2 (drone wave + cow waves; {g.value} envs/workgroup, {blk.value} threads, {lds.value} B LDS)"
+    return "ch::k_env (team per env)"
 
 
 def cpu_baseline(mode, n, m, seconds=12.0):
@@ -116,6 +140,8 @@ def main():
     rb = 8 if args.precision == "f64" else 4
     bytes_step = algorithmic_bytes(mode, n, m, b.obs_rows, rb)
     achieved = bytes_step * E / (kern_us * 1e-6) / 1e9
+    traffic, traffic_src = pmc_traffic(args.workload, args.precision) if E == WORKLOADS[args.workload][1] else (None, None)
+    kname = kernel_name(b)
 
     out = None
     if rank == 0:
@@ -129,9 +155,9 @@ def main():
             "config": {"workload": desc, "envs_per_gpu": E, "num_drones": n, "num_cattle": m, "mode": mode,
                        "parallelism": f"env-sharded x{world} (no per-step collective)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "ch::k_env<R,TEAM,false> (fused step)", "kernel_us": kern_us,
-                         "bytes_per_env_step": bytes_step},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": traffic_src, "algorithmic_bytes_per_launch": bytes_step * E,
+                         "kernel": kname, "kernel_us": kern_us, "bytes_per_env_step": bytes_step},
             "rollout_metrics": {"episodes": mv[1], "mean_return": (mv[2] / mv[1]) if mv[1] else None,
                                 "nan_rewards": mv[6], "terminated": mv[4], "truncated": mv[5]},
         }

@@ -1,13 +1,12 @@
 #!/bin/bash
-# Counter collection: one rocprofv3 --pmc pass per counter group (no tracing domains combined).
-# Stops at the first crash/timeout; an unknown counter (rc 1) just skips that group.
+# Counter collection for the step kernel: one rocprofv3 --pmc pass per counter group (no tracing
+# domains combined), then tools/parse_pmc.py.  Stops at the first crash/timeout.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${TAG:-prof}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
-WORK="python bench.py --steps ${STEPS:-40} --warmup 10 --no-cpu-baseline ${BENCH_ARGS:-}"
+WORK="python bench.py --steps ${STEPS:-60} --warmup 200 --no-cpu-baseline ${BENCH_ARGS:-}"
 i=0
 while read -r group; do
   [ -z "$group" ] && continue
@@ -18,4 +17,5 @@ while read -r group; do
   echo "=== pmc$i rc=$rc" | tee -a "$OUT/steps.log"
   if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then exit $rc; fi
 done < "${GROUPS_FILE:-tools/pmc_groups.txt}"
+python tools/parse_pmc.py "$OUT" --json "$OUT/traffic.json" --workload "${WORKLOAD:-c4}" --dtype "${DTYPE:-f64}" > "$OUT/pmc_summary.txt"
 echo ALL_DONE | tee -a "$OUT/steps.log"

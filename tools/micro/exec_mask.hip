@@ -25,6 +25,35 @@ __global__ void sincos_chain(T* out, int iters, int active) {
     out[blockIdx.x * blockDim.x + threadIdx.x] = x;
 }
 
+// 8 independent dependency chains, unrolled: the single-wave issue interval of the FMA
+template <class T>
+__global__ void ilp8(T* out, int iters) {
+    T x[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = (T)threadIdx.x * (T)1e-3 + (T)k;
+    const T b = (T)0.999999, c = (T)1e-7;
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) x[k] = __builtin_fma(x[k], b, c);
+    }
+    T s = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += x[k];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+template <class T>
+__global__ void dep1(T* out, int iters) {
+    T x = (T)threadIdx.x * (T)1e-3;
+    const T b = (T)0.999999, c = (T)1e-7;
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int r = 0; r < 64; ++r) x = __builtin_fma(x, b, c);
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+}
+
 int main() {
     double* d;
     hipMalloc(&d, 1 << 24);
@@ -56,6 +85,29 @@ int main() {
                 float ms; hipEventElapsedTime(&ms, s, e);
                 if (rep) printf("%s sin+cos chain active=%2d: %.3f ms -> %.1f ns per iteration\n", prec ? "f32" : "f64", act, ms,
                                 ms * 1e6 / 2000);
+            }
+        }
+    for (int waves : {1024, 2048, 4096})
+        for (int prec = 0; prec < 2; ++prec) {
+            for (int kind = 0; kind < 2; ++kind) {
+                float best = 1e9;
+                for (int rep = 0; rep < 3; ++rep) {
+                    hipEventRecord(s);
+                    if (kind == 0) {
+                        if (prec == 0) hipLaunchKernelGGL(ilp8<double>, dim3(waves), dim3(64), 0, 0, d, 2000);
+                        else hipLaunchKernelGGL(ilp8<float>, dim3(waves), dim3(64), 0, 0, (float*)d, 2000);
+                    } else {
+                        if (prec == 0) hipLaunchKernelGGL(dep1<double>, dim3(waves), dim3(64), 0, 0, d, 2000);
+                        else hipLaunchKernelGGL(dep1<float>, dim3(waves), dim3(64), 0, 0, (float*)d, 2000);
+                    }
+                    hipEventRecord(e);
+                    hipEventSynchronize(e);
+                    float ms; hipEventElapsedTime(&ms, s, e);
+                    if (ms < best) best = ms;
+                }
+                printf("%s %s waves=%d (%d/SIMD): %.3f ms -> %.2f ns per wave-FMA (per wave)\n", prec ? "f32" : "f64",
+                       kind == 0 ? "8 independent" : "1 dependent  ", waves, waves / 1024, best,
+                       best * 1e6 / (2000.0 * 64));
             }
         }
     // two waves per SIMD: 2048 blocks
