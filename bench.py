@@ -95,6 +95,8 @@ def main():
     ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--graph", type=int, default=0,
+                    help="steps per captured HIP graph in the timed loop (0 = one host launch per step)")
     args = ap.parse_args()
 
     import torch
@@ -114,13 +116,27 @@ def main():
     stream = torch.cuda.current_stream()
     for _ in range(args.warmup):
         b.step(random_actions=True, autoreset=True, terminal_obs=False)
+    # the timed loop: K steps as whole graph replays of `chunk` steps (plus single launches for the rest)
+    chunk = args.graph if args.graph > 0 and args.steps >= args.graph else 0
+    graph = b.capture_rollout(chunk) if chunk else None
+    if graph is not None:   # capture launched one real step; keep warm-up semantics
+        torch.cuda.synchronize()
     b.metrics(reset=True)
+
+    def run(k):
+        done = 0
+        if graph is not None:
+            while done + chunk <= k:
+                graph.replay()
+                done += chunk
+        while done < k:
+            b.step(random_actions=True, autoreset=True, terminal_obs=False)
+            done += 1
 
     D.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        b.step(random_actions=True, autoreset=True, terminal_obs=False)
+    run(args.steps)
     # end-of-rollout metrics: RCCL all-reduce over xGMI, the only collective of the rollout
     mv, _ = D.reduce_rollout(torch.tensor(b.metrics(reset=True), dtype=torch.float64), 0.0, device=b.device)
     torch.cuda.synchronize()
@@ -152,6 +168,7 @@ def main():
             "ms_per_step": dt / args.steps * 1000.0, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": args.precision, "agent_steps_per_s": value * n,
             "data": "synthetic: Philox4x32 random VEL actions in-kernel, spawn table from config/cattle_positions.yaml",
+            "launch": f"HIP graph of {chunk} steps per replay" if graph is not None else "one host launch per step",
             "config": {"workload": desc, "envs_per_gpu": E, "num_drones": n, "num_cattle": m, "mode": mode,
                        "parallelism": f"env-sharded x{world} (no per-step collective)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -102,7 +102,12 @@ class HerdBatch:
         return self.obs
 
     def step(self, actions=None, autoreset=True, random_actions=False, terminal_obs=True, step_io=None):
-        """BaseAviary.step for every env.  ``actions``: float32 [E, num_drones, 4] device tensor."""
+        """BaseAviary.step for every env.  ``actions``: float32 [E, num_drones, 4] device tensor.
+
+        ``self.obs`` is overwritten in place and is read-only to the caller: the step kernel stores only
+        the entries that change (own state, neighbours, cattle), the constant-zero bytes of each block
+        (rows >= NUM_DRONES, the action-buffer block) stay from the last full write.  After writing
+        into ``self.obs``, call ``invalidate_obs()`` so the next step rewrites every block in full."""
         io = self._io
         flags = (L.CH_STEP_AUTORESET if autoreset else 0) | (L.CH_STEP_RANDOM_ACTIONS if random_actions else 0)
         if random_actions:
@@ -124,6 +129,28 @@ class HerdBatch:
         if rc:
             L.check(rc, self.handle)
         return self.obs, self.reward, self.terminated, self.truncated
+
+    def invalidate_obs(self):
+        """The caller modified ``self.obs``: the next step writes every observation block in full."""
+        L.check(L.lib().ch__obs_invalidate(self.handle), self.handle)
+
+    def capture_rollout(self, steps, autoreset=True, terminal_obs=False):
+        """Capture ``steps`` random-action steps into a HIP graph (torch.cuda.CUDAGraph); ``replay()``
+        then runs them with one launch from the host.  Every launch parameter is constant across steps
+        (the Philox counter lives in the env state), so a replay is exactly ``steps`` calls of
+        ``step(random_actions=True)``.  Used by bench.py to take the host out of the step loop."""
+        torch = self.torch
+        side = torch.cuda.Stream(device=self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(side):
+            self.step(random_actions=True, autoreset=autoreset, terminal_obs=terminal_obs)   # first launch: attrs
+            torch.cuda.synchronize(self.device)
+            with torch.cuda.graph(graph, stream=side):
+                for _ in range(steps):
+                    self.step(random_actions=True, autoreset=autoreset, terminal_obs=terminal_obs)
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        return graph
 
     # ------------------------------------------------------------------------------------------
     def state_size(self):

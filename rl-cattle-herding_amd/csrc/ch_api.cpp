@@ -35,6 +35,10 @@ struct ch_handle {
     int n_scen = 0, n_cows = 0;
     double* debug = nullptr;
     int phase_mask = 0;
+    // The obs buffer whose constant-zero bytes (rows >= NUM_DRONES, the action-buffer block, padding)
+    // are known to hold zeros: the last one a full-block writer (v1 step, full ch_reset, v2 step with
+    // obs_full) wrote.  The v2 step then stores only the entries that change.
+    const float* obs_zero_ptr = nullptr;
     // v2 step kernel (ch_step.hip): envs per workgroup, block size, dynamic LDS, cow-pair list
     int kernel = 2;
     long long* tstamp = nullptr;
@@ -366,6 +370,8 @@ int ch_reset(ch_handle* h, const uint8_t* mask_dev, float* obs_dev, void* stream
         e = launch_reset(p, h->team, st);
     }
     if (e != hipSuccess) return fail(h, CH_ERR_DEVICE, std::string("ch_reset launch: ") + hipGetErrorString(e));
+    if (!mask_dev) h->obs_zero_ptr = obs_dev;                    // every block written in full
+    else if (h->obs_zero_ptr != obs_dev) h->obs_zero_ptr = nullptr;   // some blocks of obs_dev unknown
     return CH_OK;
 }
 
@@ -388,6 +394,7 @@ int ch_step(ch_handle* h, const ch_step_io* io, void* stream) {
         p.actions = io->actions; p.actions_out = io->actions_out; p.obs = io->obs; p.reward = io->reward;
         p.term = io->terminated; p.trunc = io->truncated; p.terminal_obs = io->terminal_obs;
         p.agent_active = io->agent_active; p.reset_happened = io->reset_happened; p.flags = io->flags;
+        p.obs_full = io->obs != h->obs_zero_ptr;
     };
     if (h->rsize == sizeof(double)) {
         StepParams<double> p = params<double>(h);
@@ -399,6 +406,7 @@ int ch_step(ch_handle* h, const ch_step_io* io, void* stream) {
         e = h->kernel == 2 ? launch_step_v2(p, h->block, h->lds, st) : launch_step(p, h->team, st);
     }
     if (e != hipSuccess) return fail(h, CH_ERR_DEVICE, std::string("ch_step launch: ") + hipGetErrorString(e));
+    h->obs_zero_ptr = (h->phase_mask & 8) ? nullptr : io->obs;
     return CH_OK;
 }
 
@@ -438,6 +446,7 @@ int ch_set_state(ch_handle* h, const double* hd, const int32_t* hi, void* stream
     HIP_TRY(h, hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
     HIP_TRY(h, hipStreamSynchronize(st));
+    h->obs_zero_ptr = nullptr;   // NUM_DRONES may change: the next step writes every obs block in full
     const size_t nd = (size_t)kDroneComps * h->E * h->NC, nc = (size_t)kCattleComps * h->E * h->M,
                  nr = (size_t)kEnvReal * h->E;
     if (hd) {
@@ -498,6 +507,14 @@ int ch__geometry(const ch_handle* h, int32_t* G, int32_t* block, int64_t* lds, i
 }
 
 /* Internal diagnostics: skip kernel phases (1 drones, 2 flock, 4 task, 8 obs) to attribute time. */
+/* Internal: forget which obs buffer holds valid constant-zero bytes (the caller wrote into it); the
+ * next ch_step writes every obs block in full. */
+int ch__obs_invalidate(ch_handle* h) {
+    if (!h) return CH_ERR_INVALID;
+    h->obs_zero_ptr = nullptr;
+    return CH_OK;
+}
+
 int ch__set_phase_mask(ch_handle* h, int32_t mask) {
     if (!h) return CH_ERR_INVALID;
     h->phase_mask = mask;

@@ -46,12 +46,10 @@ __device__ __forceinline__ bool term_call(const Level* LT, int level, R& clock, 
     return false;
 }
 
-// env-scalar part of a reset: NUM_DRONES draw (BaseAviary.py:307), counters (306, 557), spawn index
-// advanced before use (600-606); prev_cent_dists / spacing clock persist in compat mode (CattleAviary.py:89)
+// NUM_DRONES of the episode that starts after `episode` resets (BaseAviary.py:307: random.randint over
+// the curriculum's [min, max]); U from Philox keyed (seed, env id, episode, 0)
 template <class R>
-__device__ __forceinline__ void reset_scalars(const StepParams<R>& p, int e, int& n, int& sc, int& scA, int& spawn,
-                                              int& episode, int& active, int& has_prev, R& prev, R& clock) {
-    const long long env_id = p.env_off + e;
+__device__ __forceinline__ int reset_draw_n(const StepParams<R>& p, int episode, long long env_id) {
     int span = p.max_drones - p.min_drones + 1;
     int nn = p.min_drones;
     if (span > 1) {
@@ -59,6 +57,15 @@ __device__ __forceinline__ void reset_scalars(const StepParams<R>& p, int e, int
         nn = p.min_drones + (int)(u * span);
         if (nn > p.max_drones) nn = p.max_drones;
     }
+    return nn;
+}
+
+// env-scalar part of a reset: NUM_DRONES draw (BaseAviary.py:307), counters (306, 557), spawn index
+// advanced before use (600-606); prev_cent_dists / spacing clock persist in compat mode (CattleAviary.py:89)
+template <class R>
+__device__ __forceinline__ void reset_scalars(const StepParams<R>& p, int e, int& n, int& sc, int& scA, int& spawn,
+                                              int& episode, int& active, int& has_prev, R& prev, R& clock) {
+    const int nn = reset_draw_n(p, episode, p.env_off + e);
     n = nn;
     sc = 0; scA = 0;
     spawn += 1;
@@ -94,19 +101,29 @@ __device__ __forceinline__ void reset_drone(const StepParams<R>& p, long long di
     }
 }
 
+// cow j of a reset env at spawn position (x0, y0) (already looked up in the scenario table)
+template <class R>
+__device__ __forceinline__ void reset_cow_at(const StepParams<R>& p, long long ci, long long env_id, int j, R x0, R y0,
+                                             uint32_t episode, R& x, R& y, R& vx, R& vy) {
+    const long long CS = (long long)p.E * p.M;
+    x = x0; y = y0;
+    double u = philox_uniform53(p.k0, p.k1, episode, 1 + j, (uint32_t)env_id);
+    double ang = kPi * (2 * u - 1);
+    double sa, ca;
+    sincos(ang, &sa, &ca);
+    vx = R(kMaxVelCattle * ca); vy = R(kMaxVelCattle * sa);
+    p.cattle[0 * CS + ci] = x; p.cattle[1 * CS + ci] = y; p.cattle[2 * CS + ci] = vx; p.cattle[3 * CS + ci] = vy;
+}
+
 // cow j of a reset env: YAML scenario position, yaw/velocity angle pi(2U-1) (BaseAviary.py:600-637),
 // U from Philox keyed (seed, env id, episode, 1 + j)
 template <class R>
 __device__ __forceinline__ void reset_cow(const StepParams<R>& p, long long ci, long long env_id, int j, int spawn,
                                           uint32_t episode, R& x, R& y, R& vx, R& vy) {
-    const long long CS = (long long)p.E * p.M;
     const double* tab = p.spawn + ((long long)spawn * p.n_cows + j) * 2;
-    x = R(tab[0]); y = R(tab[1]);
-    double u = philox_uniform53(p.k0, p.k1, episode, 1 + j, (uint32_t)env_id);
-    double ang = kPi * (2 * u - 1);
-    vx = R(kMaxVelCattle * m_cos(ang)); vy = R(kMaxVelCattle * m_sin(ang));
-    p.cattle[0 * CS + ci] = x; p.cattle[1 * CS + ci] = y; p.cattle[2 * CS + ci] = vx; p.cattle[3 * CS + ci] = vy;
+    reset_cow_at(p, ci, env_id, j, R(tab[0]), R(tab[1]), episode, x, y, vx, vy);
 }
+
 
 // end-of-episode bonus of MARLCattleAviary._endOfEpisodeReward (MARLCattleAviary.py:183-241)
 template <class R>

@@ -44,6 +44,7 @@ struct StepParams {
     const uint8_t* reset_mask;
     uint32_t flags;
     double* debug;  // optional [E][NC][16] per-drone intermediates (diagnostics only)
+    int obs_full;   // v2: also store the constant-zero bytes of every obs block (ch_api.cpp: obs_zero_ptr)
     int phase_mask; // diagnostics only: skip phases (1 drones, 2 flock, 4 task, 8 obs) for time attribution
     int G, P;                 // v2: envs per workgroup, cow pairs per env
     const uint16_t* pairs;    // v2: [P] unordered cow pairs (i | j << 8) in tri() order
@@ -60,8 +61,8 @@ struct Level {
 };
 
 // LDS carve of one v2 step workgroup (ch_step.hip); identical on host (size) and device (offsets).
-constexpr int kV2EnvInts = 11;
-constexpr int kV2Flags = 6;          // LDS hand-off counters between the drone wave and the cow waves
+constexpr int kV2EnvInts = 12;
+constexpr int kV2Flags = 9;          // LDS hand-off counters between the drone wave and the cow waves
 struct V2Layout {
     enum { CX = 0, DRONE, DCOW, ENVR, PAIRS, MET, IMG, EI, LEVELS, BYTES, NOFF };
     int G, N, M, P, rows;
@@ -70,14 +71,14 @@ struct V2Layout {
     __host__ __device__ V2Layout(int G_, int N_, int M_, int P_, int mode, int rb) : G(G_), N(N_), M(M_), P(P_) {
         rows = mode == CH_MODE_CTDE ? 12 : N;
         size_t o = 0;
-        off[CX] = o;     o = al(o + 6 * (size_t)G * M * rb);         // cx cy cvx cvy aux auy
+        off[CX] = o;     o = al(o + 8 * (size_t)G * M * rb);         // cx cy cvx cvy aux auy spx spy
         off[DRONE] = o;  o = al(o + 12 * (size_t)G * N * rb);        // dx dy dz pa pb sa sb ca cb scat psp mrew
         off[DCOW] = o;   o = al(o + (size_t)G * N * M * rb);         // cow-drone distances
         off[ENVR] = o;   o = al(o + 2 * (size_t)G * rb);             // prev clock
         off[PAIRS] = o;  o = al(o + 4 * (size_t)G * P * rb);         // alpha pair table
         off[MET] = o;    o = al(o + (size_t)kMetricRows * G * 8);
-        off[IMG] = o;    o = al(o + (size_t)G * rows * 86 * 4);      // the workgroup's observation image
-        off[EI] = o;     o = al(o + ((size_t)kV2EnvInts * G + G + 2 + kV2Flags) * 4);
+        off[IMG] = o;                                                // (observations go straight to HBM)
+        off[EI] = o;     o = al(o + ((size_t)kV2EnvInts * G + 2 * G + 2 + kV2Flags) * 4);   // + flock/reset lists
         off[LEVELS] = o; o = al(o + 8 * sizeof(Level));              // curriculum table
         off[BYTES] = o;  o = al(o + (size_t)G * P + 3 * (size_t)G * N + (size_t)G * M);
         off[NOFF] = o;

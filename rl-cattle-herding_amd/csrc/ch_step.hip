@@ -30,9 +30,19 @@
 namespace ch {
 
 // per-env integer scalars kept in LDS (index I * G + g)
-enum { I_N = 0, I_SC, I_SCA, I_HASPREV, I_LEVEL, I_TALLY, I_SPAWN, I_ACTIVE, I_EPISODE, I_FLOCK, I_RESET, I_COUNT };
+enum { I_N = 0, I_SC, I_SCA, I_HASPREV, I_LEVEL, I_TALLY, I_SPAWN, I_ACTIVE, I_EPISODE, I_FLOCK, I_RESET, I_NEWN,
+       I_COUNT };
 static_assert(I_COUNT == kV2EnvInts, "LDS env-int rows");
-enum { F_D = 0, F_T, F_H, F_A, F_E, F_Z };   // hand-off counters
+enum { F_D = 0, F_T, F_H, F_A, F_E, F_R, F_X0, F_X1, F_X2 };   // hand-off counters
+// after the per-env rows: flocking-env list [G], reset-env list [G], their counts, then the counters
+#define FL_LIST (I_COUNT * G)
+#define RS_LIST (I_COUNT * G + G)
+#define NF_AT (I_COUNT * G + 2 * G)
+#define NR_AT (I_COUNT * G + 2 * G + 1)
+
+// full unroll when the trip count is a compile-time constant (the geometry-specialised kernels): every
+// LDS load of a small per-env loop is then issued up front instead of one round trip per iteration
+#define CH_UNROLL _Pragma("unroll")
 
 // index of unordered pair (i, j), i < j, in row-major upper-triangle order
 __device__ __forceinline__ int tri(int i, int j, int M) { return i * M - ((i * (i + 1)) >> 1) + (j - i - 1); }
@@ -71,15 +81,25 @@ __device__ __forceinline__ void lds_wait(int* f, int target) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// barrier among the cow waves only (the drone wave keeps running); `global` also publishes their
+// global stores (needed before other cow lanes rewrite the same state)
+__device__ __forceinline__ void cow_sync(int* f, int waves, bool global) {
+    if (global) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    lds_signal(f);
+    lds_wait(f, waves);
+    if (global) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 // diagnostics: per-workgroup timestamps (slots: 0/1 wall clock at start/end, 2 shader clock at start,
 // 3 after the first barrier, 4 drone chain done, 5 reward terms done, 6 herded flags received,
 // 7 bookkeeping done, 8 cow waves: alpha rows done, 9 drone positions received, 10 velocity update
 // done, 11 obs copy done, 12 CU id, 13 second barrier, 14 end)
-#define TS(slot, val) do { if (p.tstamp) p.tstamp[(long long)blockIdx.x * 16 + (slot)] = (val); } while (0)
+#define TS(slot, val) do { if (p.tstamp) p.tstamp[(long long)blockIdx.x * 32 + (slot)] = (val); } while (0)
 
 template <class R>
 struct V2Smem {
     R *cx, *cy, *cvx, *cvy, *aux, *auy;              // [G*M] positions after integration, pre-flock velocities, alpha
+    R *spx, *spy;                                    // [G*M] spawn positions of the next episode (prefetched)
     R *dx, *dy, *dz;                                 // [G*N] drone position after physics
     R *pa, *pb, *sa, *sb, *ca, *cb, *scat, *psp;     // [G*N] per-drone reward terms
     R* mrew;                                         // [G*N] MARL per-agent reward scratch
@@ -87,7 +107,6 @@ struct V2Smem {
     R *prev, *clock;                                 // [G]
     R *tgx, *tgy, *tcx, *tcy;                        // [G*P] alpha pair table
     double* met;                                     // [kMetricRows*G]
-    float* img;                                      // [G][rows][86] observation image (output layout)
     int* ei;                                         // [I_COUNT*G] + list [G] + 2 + flags
     int* flags;
     Level* LT;                                       // curriculum table (curriculum_learning.py:10-194)
@@ -96,6 +115,7 @@ struct V2Smem {
     __device__ V2Smem(unsigned char* base, const V2Layout& L) {
         const int GM = L.G * L.M, GN = L.G * L.N, GP = L.G * L.P;
         cx = (R*)(base + L.off[V2Layout::CX]); cy = cx + GM; cvx = cy + GM; cvy = cvx + GM; aux = cvy + GM; auy = aux + GM;
+        spx = auy + GM; spy = spx + GM;
         dx = (R*)(base + L.off[V2Layout::DRONE]); dy = dx + GN; dz = dy + GN;
         pa = dz + GN; pb = pa + GN; sa = pb + GN; sb = sa + GN; ca = sb + GN; cb = ca + GN; scat = cb + GN;
         psp = scat + GN; mrew = psp + GN;
@@ -103,105 +123,83 @@ struct V2Smem {
         prev = (R*)(base + L.off[V2Layout::ENVR]); clock = prev + L.G;
         tgx = (R*)(base + L.off[V2Layout::PAIRS]); tgy = tgx + GP; tcx = tgy + GP; tcy = tcx + GP;
         met = (double*)(base + L.off[V2Layout::MET]);
-        img = (float*)(base + L.off[V2Layout::IMG]);
         ei = (int*)(base + L.off[V2Layout::EI]);
-        flags = ei + I_COUNT * L.G + L.G + 2;
+        flags = ei + I_COUNT * L.G + 2 * L.G + 2;
         LT = (Level*)(base + L.off[V2Layout::LEVELS]);
         pflag = base + L.off[V2Layout::BYTES]; dflags = pflag + GP; herded = dflags + GN; md1 = herded + GM;
         md2 = md1 + GN;
     }
 };
 
-// Copy the observation image of envs [0, Gv) (same layout as the output region) to HBM.
-__device__ __forceinline__ void copy_obs(float* out, const float* img, int Gv, int RW, int t0, int stride, bool vec4) {
-    const int total = Gv * RW;
-    if (vec4) {
-        const float4* s = reinterpret_cast<const float4*>(img);
-        float4* d = reinterpret_cast<float4*>(out);
-        for (int q = t0; q < (total >> 2); q += stride) d[q] = s[q];
-    } else {
-        const float2* s = reinterpret_cast<const float2*>(img);
-        float2* d = reinterpret_cast<float2*>(out);
-        for (int q = t0; q < (total >> 1); q += stride) d[q] = s[q];
-    }
+// Observation blocks are written straight to HBM by the lanes that produce each entry (BaseRLAviary.py:
+// 272-342 / BaseMARLAviary.py:253-303): own state (drone wave, after the chain), two nearest drones
+// (drone wave, after the reward terms), cattle offsets (cow waves, after the distance table), and the
+// always-zero bytes (cow waves, during the alpha phase).  `eb` is the env's block (row 0, col 0); 86 is
+// even, so every float2 below is 8-byte aligned.
+__device__ __forceinline__ void st2(float* eb, int off, float a, float b) {
+    reinterpret_cast<float2*>(eb + off)[0] = make_float2(a, b);
 }
 
-// Copy (or clear, with out == nullptr) the images of the envs listed in rl[0..nr) between LDS and the
-// output; one env's block is RW floats at offset g*RW in both.  16-byte units when RW % 4 == 0 (then
-// every env block is 16-byte aligned), 8-byte units otherwise (86 is even).
-__device__ __forceinline__ void env_list_obs(float* out, float* img, const int* rl, int nr, int RW, int t0, int stride) {
-    if ((RW & 3) == 0) {
-        const int RW4 = RW >> 2;
-        const float rR = 1.0f / (float)RW4;
-        for (int q = t0; q < nr * RW4; q += stride) {
-            const int k = qdiv(q, RW4, rR), g = rl[k], o = g * RW4 + (q - k * RW4);
-            if (out) reinterpret_cast<float4*>(out)[o] = reinterpret_cast<const float4*>(img)[o];
-            else reinterpret_cast<float4*>(img)[o] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        }
-    } else {
-        const int RW2 = RW >> 1;
-        const float rR = 1.0f / (float)RW2;
-        for (int q = t0; q < nr * RW2; q += stride) {
-            const int k = qdiv(q, RW2, rR), g = rl[k], o = g * RW2 + (q - k * RW2);
-            if (out) reinterpret_cast<float2*>(out)[o] = reinterpret_cast<const float2*>(img)[o];
-            else reinterpret_cast<float2*>(img)[o] = make_float2(0.0f, 0.0f);
-        }
-    }
-}
-
-// own-state observation entries of drone row `row` of env g (BaseRLAviary.py:289-295)
+// own-state entries of row `row` (BaseRLAviary.py:289-295)
 template <class R>
-__device__ __forceinline__ void img_own(float* img, int g, int rows, int row, R z, const R rpy[3], const R v[3],
-                                        const R w[3]) {
-    float* t = img + (g * rows + row) * 86;
-    reinterpret_cast<float2*>(t)[0] = make_float2((float)z, (float)rpy[0]);
-    reinterpret_cast<float2*>(t)[1] = make_float2((float)rpy[1], (float)rpy[2]);
-    reinterpret_cast<float2*>(t)[2] = make_float2((float)v[0], (float)v[1]);
-    reinterpret_cast<float2*>(t)[3] = make_float2((float)v[2], (float)w[0]);
-    reinterpret_cast<float2*>(t)[4] = make_float2((float)w[1], (float)w[2]);
+__device__ __forceinline__ void obs_own(float* eb, int row, R z, const R rpy[3], const R v[3], const R w[3]) {
+    const int o = row * 86;
+    st2(eb, o + 0, (float)z, (float)rpy[0]);
+    st2(eb, o + 2, (float)rpy[1], (float)rpy[2]);
+    st2(eb, o + 4, (float)v[0], (float)v[1]);
+    st2(eb, o + 6, (float)v[2], (float)w[0]);
+    st2(eb, o + 8, (float)w[1], (float)w[2]);
 }
 
-// nearest-neighbour observation entries (columns 10..13) from the two nearest drones i1, i2
+// nearest-neighbour entries (columns 10..13) of drone i from its two nearest drones i1, i2
 template <class R>
-__device__ __forceinline__ void img_nbr(float* img, const R* dx, const R* dy, int g, int N, int rows, int i, int i1,
-                                        int i2) {
-    const int b0 = g * N;
+__device__ __forceinline__ void obs_nbr(float* eb, const R* dx, const R* dy, int b0, int i, int i1, int i2) {
     const R xi = dx[b0 + i], yi = dy[b0 + i];
-    float2* t = reinterpret_cast<float2*>(img + (g * rows + i) * 86 + 10);
-    t[0] = i1 >= 0 ? make_float2((float)(dx[b0 + i1] - xi), (float)(dy[b0 + i1] - yi)) : make_float2(0.0f, 0.0f);
-    t[1] = i2 >= 0 ? make_float2((float)(dx[b0 + i2] - xi), (float)(dy[b0 + i2] - yi)) : make_float2(0.0f, 0.0f);
+    const int o = i * 86 + 10;
+    if (i1 >= 0) st2(eb, o, (float)(dx[b0 + i1] - xi), (float)(dy[b0 + i1] - yi)); else st2(eb, o, 0.0f, 0.0f);
+    if (i2 >= 0) st2(eb, o + 2, (float)(dx[b0 + i2] - xi), (float)(dy[b0 + i2] - yi)); else st2(eb, o + 2, 0.0f, 0.0f);
 }
 
-// two nearest drones of drone i in the reference's stable order (BaseRLAviary.py:303-317)
+// cattle-relative entries of cow j for every live drone row (BaseRLAviary.py:319-331)
 template <class R>
-__device__ __forceinline__ void nearest_two(const R* dx, const R* dy, int b0, int i, int n, int& i1, int& i2) {
+__device__ __forceinline__ void obs_cattle(float* eb, const R* dx, const R* dy, int b0, int j, int n, int cat_off, R qx,
+                                           R qy) {
+    for (int r = 0; r < n; ++r) st2(eb, r * 86 + cat_off + 2 * j, (float)(qx - dx[b0 + r]), (float)(qy - dy[b0 + r]));
+}
+
+// The bytes of an env block no producer writes this step: rows n..rows-1 in full, and in the live rows
+// columns 14..cat_off-1 and cat_off+2*m_obs..85 (the always-zero action-buffer block and padding).
+// Lane t of the team covers float2 t, t + stride, ... of the block (consecutive lanes, consecutive
+// addresses); float2 u sits at row u / 43, column 2 * (u % 43).
+__device__ __forceinline__ void obs_zero_env(float* eb, int n, int rows, int cat_off, int m_obs, int t0, int stride) {
+    for (int u = t0; u < rows * 43; u += stride) {
+        const int r = u / 43, c = 2 * (u - 43 * r);
+        if (r >= n || (c >= 14 && c < cat_off) || c >= cat_off + 2 * m_obs) st2(eb, 2 * u, 0.0f, 0.0f);
+    }
+}
+
+// two nearest drones of drone i in the reference's stable order (BaseRLAviary.py:303-317), packed as
+// (i1 + 1) | (i2 + 1) << 8 (0 = none); returned by value so nothing lands in scratch
+template <class R>
+__device__ __forceinline__ int nearest_two(const R* dx, const R* dy, int b0, int i, int n) {
     const R xi = dx[b0 + i], yi = dy[b0 + i];
     R b1 = 0, b2 = 0;
-    i1 = -1; i2 = -1;
+    int i1 = -1, i2 = -1;
     for (int j = 0; j < n; ++j) {
         if (j == i) continue;
         const R d = norm2(dx[b0 + j] - xi, dy[b0 + j] - yi);
         if (i1 < 0 || d < b1) { i2 = i1; b2 = b1; i1 = j; b1 = d; }
         else if (i2 < 0 || d < b2) { i2 = j; b2 = d; }
     }
-}
-
-// cattle-relative observation entries of cow j for every live drone row (BaseRLAviary.py:319-331)
-template <class R>
-__device__ __forceinline__ void img_cattle(float* img, const R* dx, const R* dy, int g, int N, int rows, int j, int n,
-                                           int cat_off, R qx, R qy) {
-    const int b0 = g * N;
-    for (int r = 0; r < n; ++r)
-        reinterpret_cast<float2*>(img + (g * rows + r) * 86 + cat_off + 2 * j)[0] =
-            make_float2((float)(qx - dx[b0 + r]), (float)(qy - dy[b0 + r]));
+    return (i1 + 1) | ((i2 + 1) << 8);
 }
 
 // flock alpha term, pair form, for every flocking env (flockUtils.py:237-258, 327-337; MathUtils 11-58).
 // l = lane rank among the A lanes that share the table.
 template <class R>
 __device__ __forceinline__ void alpha_pairs(const StepParams<R>& p, V2Smem<R>& S, int G, int M, int P, int l, int A) {
-    const int nf = S.ei[I_COUNT * G + G];
-    const int* flist = S.ei + I_COUNT * G;
+    const int nf = S.ei[NF_AT];
+    const int* flist = S.ei + FL_LIST;
     const R ra = sigma_norm_n(R(1.2)), da = ra;
     const int tot = nf * P;
     const float rP = 1.0f / (float)P;
@@ -231,7 +229,7 @@ __device__ __forceinline__ void alpha_row(V2Smem<R>& S, int M, int P, int u, int
     R gx = 0, gy = 0, cxx = 0, cyy = 0, ux = 0, uy = 0;
     int nb = 0;
     const int pb = g * P;
-    for (int k = 0; k < M; ++k) {
+    CH_UNROLL for (int k = 0; k < M; ++k) {
         if (k == j) continue;
         const bool fwd = j < k;
         const int idx = pb + (fwd ? tri(j, k, M) : tri(k, j, M));
@@ -368,8 +366,8 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
         }
         // compact list of flocking envs (BaseAviary.py:454: every second step_counter_A)
         const unsigned long long bal = __ballot(flk);
-        if (flk) ei[I_COUNT * G + __popcll(bal & ((1ull << tid) - 1ull))] = g;
-        if (tid == 0) { ei[I_COUNT * G + G] = __popcll(bal); ei[I_COUNT * G + G + 1] = 0; }
+        if (flk) ei[FL_LIST + __popcll(bal & ((1ull << tid) - 1ull))] = g;
+        if (tid == 0) { ei[NF_AT] = __popcll(bal); ei[NR_AT] = 0; }
         lds_signal(fl + F_E);
     } else {
         for (int u = ct; u < Gv * M; u += CW) {
@@ -381,17 +379,17 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
             p.cattle[0 * CS + ci] = x; p.cattle[1 * CS + ci] = y;
             S.cx[u] = x; S.cy[u] = y; S.cvx[u] = vx; S.cvy[u] = vy;
         }
-        float4* z4 = reinterpret_cast<float4*>(S.img);
-        const int n4 = (G * RW + 3) >> 2;
-        for (int k = ct; k < n4; k += CW) z4[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        lds_signal(fl + F_Z);
+        if (ct == 0) TS(16, (long long)clock64());
         lds_wait(fl + F_E, 1);   // env scalars and the flocking list from the drone wave
+        if (ct == 0) TS(17, (long long)clock64());
     }
     if (tid == 0) TS(3, (long long)clock64());
 
     const bool wobs = !(p.phase_mask & 8);
     float* obs_wg = p.obs + (long long)e0 * RW;
-    const bool vec4 = (((long long)e0 * RW) & 3) == 0 && ((Gv * RW) & 3) == 0;
+    // final per-env scalars, held by the drone wave's env lanes until the write-back
+    int f_n = 0, f_sc = 0, f_scA = 0, f_hp = 0, f_level = 0, f_tally = 0, f_spawn = 0, f_active = 0, f_episode = 0;
+    R f_prev = 0, f_clock = 0;
 
     if (tid < 64) {
         // ============ drone wave: the critical path ============================================
@@ -432,8 +430,7 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
             quat_to_euler(q, rpy_out);
             S.dx[tid] = pos[0]; S.dy[tid] = pos[1]; S.dz[tid] = pos[2];
         }
-        lds_wait(fl + F_Z, W1);   // the cow waves have integrated the herd and zeroed the image
-        if (live) img_own(S.img, dg, rows, dk, pos[2], rpy_out, v, w);
+        if (live && wobs) obs_own(obs_wg + dg * RW, dk, pos[2], rpy_out, v, w);
         wave_sync();
         lds_signal(fl + F_D);
         if (tid == 0) TS(4, (long long)clock64());
@@ -446,7 +443,8 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
             int i1 = -1, i2 = -1;
             uint8_t f = 0;
             bool iso = true;
-            for (int j = 0; j < n; ++j) {
+            CH_UNROLL for (int j = 0; j < N; ++j) {
+                if (j >= n) break;
                 if (j == i) continue;
                 const R d = norm2(S.dx[b0 + j] - xi, S.dy[b0 + j] - yi);
                 if (d != d) f |= 8;
@@ -466,7 +464,7 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
             if (p.compat || m2 < R(INFINITY)) ps += (cb + sb) / R(2.0);
             S.pa[tid] = m1; S.pb[tid] = m2; S.dflags[tid] = f;
             S.sa[tid] = sa; S.sb[tid] = sb; S.ca[tid] = ca; S.cb[tid] = cb; S.psp[tid] = ps;
-            img_nbr(S.img, S.dx, S.dy, dg, N, rows, i, i1, i2);
+            if (wobs) obs_nbr(obs_wg + dg * RW, S.dx, S.dy, b0, i, i1, i2);
         }
         lds_signal(fl + F_T);
         if (tid == 0) TS(5, (long long)clock64());
@@ -476,77 +474,69 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
             // closest cow (CattleAviary.py:248-252) from the cow waves' distance table -> cattle term
             const R* dc = S.dcow + tid * M;
             R best = R(INFINITY);
-            for (int j = 0; j < M; ++j) {
+            CH_UNROLL for (int j = 0; j < M; ++j) {
                 const R d = dc[j];
                 if (d < best) best = d;
             }
             S.scat[tid] = cattle_spacing(best, R(p.cs_cc));
         }
         wave_sync();
+        if (tid == 0) TS(15, (long long)clock64());
 
-        // per-env bookkeeping, one env per lane, in the reference's call order
+        // per-env bookkeeping, one env per lane, in the reference's call order; the final scalars stay in
+        // this lane's registers and go to HBM after the last barrier
         const int g = tid;
-        if (g < Gv && task) {
-            const int e = e0 + g, n = ei[I_N * G + g], b0 = g * N, c0 = g * M;
-            int sc = ei[I_SC * G + g], has_prev = ei[I_HASPREV * G + g], level = ei[I_LEVEL * G + g];
-            int tally = ei[I_TALLY * G + g], active = ei[I_ACTIVE * G + g];
-            R prev = S.prev[g], clock = S.clock[g];
-            R scx = 0, scy = 0, sdx = 0, sdy = 0;
+        const bool envl = g < Gv;
+        const int e = e0 + g, b0 = g * N, c0 = g * M;
+        if (envl) {
+            f_n = ei[I_N * G + g]; f_sc = ei[I_SC * G + g]; f_scA = ei[I_SCA * G + g]; f_hp = ei[I_HASPREV * G + g];
+            f_level = ei[I_LEVEL * G + g]; f_tally = ei[I_TALLY * G + g]; f_spawn = ei[I_SPAWN * G + g];
+            f_active = ei[I_ACTIVE * G + g]; f_episode = ei[I_EPISODE * G + g];
+            f_prev = S.prev[g]; f_clock = S.clock[g];
+        }
+        int done = 0, rs = 0, n_term = 0, n_trunc = 0, n_nan = 0, level_r = f_level;
+        double ret = 0;
+        bool te2 = false, tr = false;
+        R cent = 0, eff = 0, ms = R(INFINITY), scx = 0, scy = 0;
+        const R max_step = R(0.3 * kMaxSpeedKmh * (1000.0 / 3600.0)) / R(p.ctrl_freq);
+        if (envl && task) {
+            const int n = f_n;
+            R sdx = 0, sdy = 0;
             int herded = 0;
-            for (int j = 0; j < M; ++j) { scx += S.cx[c0 + j]; scy += S.cy[c0 + j]; herded += S.herded[c0 + j]; }
-            for (int i = 0; i < n; ++i) { sdx += S.dx[b0 + i]; sdy += S.dy[b0 + i]; }
+            CH_UNROLL for (int j = 0; j < M; ++j) { scx += S.cx[c0 + j]; scy += S.cy[c0 + j]; herded += S.herded[c0 + j]; }
+            CH_UNROLL for (int i = 0; i < N; ++i) if (i < n) { sdx += S.dx[b0 + i]; sdy += S.dy[b0 + i]; }
             scx /= R(M); scy /= R(M); sdx /= R(n); sdy /= R(n);
             R ex = sdx - scx, ey = sdy - scy;
-            const R cent = sqrt(ex * ex + ey * ey + R(0) * R(0));   // HerdCentroid/DroneCentroid, z = 0.95 both
-            const R eff = R((double)herded / M * 100);
-            R ms = R(INFINITY);
+            cent = sqrt(ex * ex + ey * ey + R(0) * R(0));   // HerdCentroid/DroneCentroid, z = 0.95 both
+            eff = R((double)herded / M * 100);
             bool anynan = false;
             uint8_t any = 0;
-            for (int i = 0; i < n; ++i) {
+            CH_UNROLL for (int i = 0; i < N; ++i) if (i < n) {
                 if (S.pa[b0 + i] < ms) ms = S.pa[b0 + i];
                 anynan |= (S.dflags[b0 + i] & 8) != 0;
                 any |= S.dflags[b0 + i];
             }
             if (anynan) ms = R(NAN);
-            const R max_step = R(0.3 * kMaxSpeedKmh * (1000.0 / 3600.0)) / R(p.ctrl_freq);
-            const bool time_up = (double)sc / p.ctrl_freq > p.episode_len;
-            int done = 0;
-            double ret = 0;
-            int n_term = 0, n_trunc = 0, n_nan = 0;
+            const bool time_up = (double)f_sc / p.ctrl_freq > p.episode_len;
             if constexpr (!marl) {
-                // CattleAviary._computeReward (CattleAviary.py:213-332) then terminated / truncated twice
-                const Level& Lv = LT[level];
-                R sp_simple = 0, sp_complex = 0, msp = 0, mcat = 0, cat = 0;
-                for (int i = 0; i < n; ++i) {
-                    if (p.compat || S.pa[b0 + i] < R(INFINITY)) { sp_complex += S.ca[b0 + i]; sp_simple += S.sa[b0 + i]; }
-                    if (p.compat || S.pb[b0 + i] < R(INFINITY)) { sp_complex += S.cb[b0 + i]; sp_simple += S.sb[b0 + i]; }
-                }
-                sp_complex /= R(n * 2.0); sp_simple /= R(n * 2.0);
-                R approach = 0;
-                if (has_prev) approach = clip(((prev - cent) / (max_step + R(1e-6))) * R(5), R(-1.0), R(1.0));
-                prev = cent; has_prev = 1;
-                for (int i = 0; i < n; ++i) cat += S.scat[b0 + i];
-                cat /= R(n);
-                R rg = sp_simple * R(Lv.w_simple) + sp_complex * R(Lv.w_complex) + R(0.1) * R(Lv.w_survival) +
-                       approach * R(Lv.w_approach) + (eff / R(100)) * R(Lv.w_eff) + cat * R(Lv.w_cattle);
-                for (int i = 0; i < n; ++i) { msp += S.psp[b0 + i]; mcat += S.scat[b0 + i]; }
-                msp /= R(n); mcat /= R(n);
-                R tot = 0;
-                for (int i = 0; i < n; ++i) tot += rg + R(0.5) * ((S.psp[b0 + i] - msp) + (S.scat[b0 + i] - mcat));
-                R rew = tot / R(n);
+                // CattleAviary: _computeReward (CattleAviary.py:213-332), then _computeTerminated twice and
+                // _computeTruncated.  The terminated calls read nothing the reward writes (the reward uses the
+                // level it started with), so they run first and the reset decision is published early.
                 const R inc = R(1.0 / 240);
-                bool te = term_call(LT, level, clock, inc, ms, cent, eff);
-                if (te) curriculum_success(LT, level, tally);
-                bool te2 = term_call(LT, level, clock, inc, ms, cent, eff);
-                bool tr = (any & 7) || cent > R(kMissionBoundary) || time_up;
-                p.reward[e] = (float)rew;
-                p.term[e] = te2; p.trunc[e] = tr;
+                bool te = term_call(LT, f_level, f_clock, inc, ms, cent, eff);
+                if (te) curriculum_success(LT, f_level, f_tally);
+                te2 = term_call(LT, f_level, f_clock, inc, ms, cent, eff);
+                tr = (any & 7) || cent > R(kMissionBoundary) || time_up;
                 done = te2 || tr;
-                ret = (double)rew;
-                n_term = te2; n_trunc = tr; n_nan = rew != rew;
             } else {
                 // MARLCattleAviary reward / terminated / truncated in the order env.step
                 // (rllib_envs/BaseAviary.py:425-431) and the wrapper (marl_wrapper.py:104-113) call them
+                int& level = f_level;
+                int& tally = f_tally;
+                int& has_prev = f_hp;
+                int& active = f_active;
+                R& prev = f_prev;
+                R& clock = f_clock;
                 const R inc = R(1.0) / R(p.ctrl_freq);
                 const int lvl0 = level;
                 auto trunc_i = [&](int i) -> bool {
@@ -620,7 +610,45 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
                     }
                 }
             }
-            sc += marl ? 1 : p.substeps;
+            rs = done && (p.flags & CH_STEP_AUTORESET);
+        }
+        // publish the reset list: the cow waves rebuild those envs while this wave finishes the reward.
+        // This wave's drone-state stores are complete first (the cow waves overwrite reset drones).
+        if (envl) ei[I_RESET * G + g] = rs;
+        const unsigned long long rbal = __ballot(rs != 0);
+        if (rs) ei[RS_LIST + __popcll(rbal & ((1ull << g) - 1ull))] = g;
+        if (tid == 0) ei[NR_AT] = __popcll(rbal);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        lds_signal(fl + F_R);
+        if (tid == 0) TS(15, (long long)clock64());
+        if (envl && task) {
+            const int n = f_n;
+            if constexpr (!marl) {
+                const Level& Lv = LT[level_r];
+                R sp_simple = 0, sp_complex = 0, msp = 0, mcat = 0, cat = 0;
+                CH_UNROLL for (int i = 0; i < N; ++i) if (i < n) {
+                    if (p.compat || S.pa[b0 + i] < R(INFINITY)) { sp_complex += S.ca[b0 + i]; sp_simple += S.sa[b0 + i]; }
+                    if (p.compat || S.pb[b0 + i] < R(INFINITY)) { sp_complex += S.cb[b0 + i]; sp_simple += S.sb[b0 + i]; }
+                }
+                sp_complex /= R(n * 2.0); sp_simple /= R(n * 2.0);
+                R approach = 0;
+                if (f_hp) approach = clip(((f_prev - cent) / (max_step + R(1e-6))) * R(5), R(-1.0), R(1.0));
+                f_prev = cent; f_hp = 1;
+                CH_UNROLL for (int i = 0; i < N; ++i) if (i < n) cat += S.scat[b0 + i];
+                cat /= R(n);
+                R rg = sp_simple * R(Lv.w_simple) + sp_complex * R(Lv.w_complex) + R(0.1) * R(Lv.w_survival) +
+                       approach * R(Lv.w_approach) + (eff / R(100)) * R(Lv.w_eff) + cat * R(Lv.w_cattle);
+                CH_UNROLL for (int i = 0; i < N; ++i) if (i < n) { msp += S.psp[b0 + i]; mcat += S.scat[b0 + i]; }
+                msp /= R(n); mcat /= R(n);
+                R tot = 0;
+                CH_UNROLL for (int i = 0; i < N; ++i) if (i < n) tot += rg + R(0.5) * ((S.psp[b0 + i] - msp) + (S.scat[b0 + i] - mcat));
+                R rew = tot / R(n);
+                p.reward[e] = (float)rew;
+                p.term[e] = te2; p.trunc[e] = tr;
+                ret = (double)rew;
+                n_term = te2; n_trunc = tr; n_nan = rew != rew;
+            }
+            f_sc += marl ? 1 : p.substeps;
             // metric accumulators (rank-local; bench.py all-reduces them)
             const double* mt = S.met;
             double o[kMetricRows];
@@ -642,31 +670,43 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
             }
 #pragma unroll
             for (int r = 0; r < kMetricRows; ++r) p.metrics[r * E + e] = o[r];
-            const int rs = done && (p.flags & CH_STEP_AUTORESET);
-            ei[I_SC * G + g] = sc; ei[I_HASPREV * G + g] = has_prev; ei[I_LEVEL * G + g] = level;
-            ei[I_TALLY * G + g] = tally; ei[I_ACTIVE * G + g] = active; ei[I_RESET * G + g] = rs;
-            S.prev[g] = prev; S.clock[g] = clock;
             if (p.reset_happened) p.reset_happened[e] = rs;
-            if (p.agent_active && !rs)
-                for (int i = 0; i < N; ++i) p.agent_active[(long long)e * N + i] = (active >> i) & 1;
-        } else if (g < Gv && p.reset_happened) {
-            p.reset_happened[e0 + g] = 0;
+            // SB3 auto-reset: the new episode's scalars (the cow waves rebuild its bodies and observation)
+            if (rs) reset_scalars(p, e, f_n, f_sc, f_scA, f_spawn, f_episode, f_active, f_hp, f_prev, f_clock);
+            if (p.agent_active)
+                for (int i = 0; i < N; ++i) p.agent_active[(long long)e * N + i] = (f_active >> i) & 1;
+        } else if (envl && p.reset_happened) {
+            p.reset_happened[e] = 0;
         }
-        // compact list of the envs that auto-reset in this launch (the reset phase walks only these)
-        const bool rs_lane = g < Gv && ei[I_RESET * G + g];
-        const unsigned long long rbal = __ballot(rs_lane);
-        if (rs_lane) ei[I_COUNT * G + __popcll(rbal & ((1ull << g) - 1ull))] = g;
-        if (tid == 0) ei[I_COUNT * G + G + 1] = __popcll(rbal);
         if (tid == 0) TS(7, (long long)clock64());
     } else {
         // ============ cow waves ================================================================
         alpha_pairs(p, S, G, M, P, ct, CW);
+        if (ct == 0) TS(18, (long long)clock64());
+        // the constant-zero bytes of the observation blocks, when the host cannot vouch that this buffer
+        // already holds them (first step into a buffer, after ch_set_state, ...; ch_api.cpp obs_zero_ptr)
+        if (wobs && p.obs_full)
+            for (int g = 0; g < Gv; ++g) obs_zero_env(obs_wg + g * RW, ei[I_N * G + g], rows, cat_off, m_obs, ct, CW);
+        if (ct == 0) TS(19, (long long)clock64());
         lds_signal(fl + F_A);
         lds_wait(fl + F_A, W1);
+        if (ct == 0) TS(20, (long long)clock64());
         const float rM = 1.0f / (float)M;
+        const int nf = ei[NF_AT];
+        const int* flist = ei + FL_LIST;
+        for (int u = ct; u < nf * M; u += CW) {   // cows of flocking envs only
+            const int f = qdiv(u, M, rM), g = flist[f], j = u - f * M;
+            alpha_row(S, M, P, g * M + j, g, j);
+        }
+        if (ct == 0) TS(21, (long long)clock64());
+        // spawn positions of the episode an auto-reset would start: scenario index + 1 (BaseAviary.py:600-606),
+        // looked up while the drone wave is still integrating, so a reset needs no global load
         for (int u = ct; u < Gv * M; u += CW) {
-            const int g = qdiv(u, M, rM);
-            if (ei[I_FLOCK * G + g]) alpha_row(S, M, P, u, g, u - g * M);
+            const int g = qdiv(u, M, rM), j = u - g * M;
+            int sp = ei[I_SPAWN * G + g] + 1;
+            if (sp >= p.n_scen) sp = 0;
+            const double* tab = p.spawn + ((long long)sp * p.n_cows + j) * 2;
+            S.spx[u] = R(tab[0]); S.spy[u] = R(tab[1]);
         }
         if (ct == 0) TS(8, (long long)clock64());
         lds_wait(fl + F_D, 1);
@@ -675,14 +715,16 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
             const int g = qdiv(u, M, rM), j = u - g * M;
             const int n = ei[I_N * G + g], b0 = g * N;
             const R qix = S.cx[u], qiy = S.cy[u];
-            for (int k = 0; k < n; ++k) {   // |y_k - q_j| for the shepherd term and the closest-cow search
+            CH_UNROLL for (int k = 0; k < N; ++k) {
+                if (k >= n) break;   // |y_k - q_j| for the shepherd term and the closest-cow search
                 const R ex = S.dx[b0 + k] - qix, ey = S.dy[b0 + k] - qiy;
                 S.dcow[(b0 + k) * M + j] = sqrt(ex * ex + ey * ey);
             }
             if (task) {
                 // evaluate_herding_effectiveness winding number (evaluation.py:100-138)
                 int wn = 0;
-                for (int i = 0; i < n; ++i) {
+                CH_UNROLL for (int i = 0; i < N; ++i) {
+                    if (i >= n) break;
                     int i2 = (i + 1 == n) ? 0 : i + 1;
                     R x1 = S.dx[b0 + i], y1 = S.dy[b0 + i], x2 = S.dx[b0 + i2], y2 = S.dy[b0 + i2];
                     R il = (x2 - x1) * (qiy - y1) - (qix - x1) * (y2 - y1);
@@ -691,88 +733,84 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
                 }
                 S.herded[u] = wn != 0;
             }
-            if (j < m_obs) img_cattle(S.img, S.dx, S.dy, g, N, rows, j, n, cat_off, qix, qiy);
+            if (j < m_obs && wobs) obs_cattle(obs_wg + g * RW, S.dx, S.dy, b0, j, n, cat_off, qix, qiy);
         }
         lds_signal(fl + F_H);
-        for (int u = ct; u < Gv * M; u += CW) {
-            const int g = qdiv(u, M, rM);
-            if (ei[I_FLOCK * G + g]) cow_flock(p, S, N, M, e0, u, g, u - g * M, ei[I_N * G + g]);
+        for (int u = ct; u < nf * M; u += CW) {   // cows of flocking envs only
+            const int f = qdiv(u, M, rM), g = flist[f], j = u - f * M;
+            cow_flock(p, S, N, M, e0, g * M + j, g, j, ei[I_N * G + g]);
         }
         if (ct == 0) TS(10, (long long)clock64());
-        lds_wait(fl + F_T, 1);    // neighbour entries of the drone wave
-        lds_wait(fl + F_H, W1);   // cattle entries of every cow wave
-        if (wobs) copy_obs(obs_wg, S.img, Gv, RW, ct, CW, vec4);
-        if (ct == 0) TS(11, (long long)clock64());
+        lds_wait(fl + F_R, 1);    // the reset list
+        const int nr = ei[NR_AT];
+        if (nr) {   // uniform across the cow waves
+            // ---- SB3 auto-reset of the listed envs (BaseAviary.reset, BaseAviary.py:280-331), rebuilt from
+            // the pre-step scalars (NUM_DRONES draw, spawn index + 1, episode) while the drone wave still
+            // computes rewards: R1 bodies + own-state rows, R2 neighbour and cattle entries, R3 copy.
+            const int* rl = ei + RS_LIST;
+            if (p.terminal_obs) {   // info["terminal_observation"]: the pre-reset observation, from HBM
+                cow_sync(fl + F_X0, W1, true);   // every cow wave's observation stores of this step are visible
+                for (int q = ct; q < nr * (RW >> 1); q += CW) {
+                    const int k = q / (RW >> 1), o = rl[k] * (RW >> 1) + (q - k * (RW >> 1));
+                    reinterpret_cast<float2*>(p.terminal_obs + (long long)e0 * RW)[o] = reinterpret_cast<const float2*>(obs_wg)[o];
+                }
+            }
+            cow_sync(fl + F_X1, W1, true);   // terminal observation read; flock stores to the cattle state done
+            const float rN = 1.0f / (float)N;
+            for (int u = ct; u < nr * N; u += CW) {
+                const int k0 = qdiv(u, N, rN), g = rl[k0], k = u - k0 * N, ud = g * N + k;
+                const int n = reset_draw_n(p, ei[I_EPISODE * G + g], p.env_off + e0 + g);
+                if (k == 0) ei[I_NEWN * G + g] = n;
+                R x, y, z;
+                reset_drone(p, (long long)e0 * N + ud, k, n, x, y, z);
+                S.dx[ud] = x; S.dy[ud] = y; S.dz[ud] = z;
+                if (!wobs) continue;
+                float* eb = obs_wg + g * RW;
+                if (k < n) {
+                    // identity quaternion: getEulerFromQuaternion gives atan2(+0, 1), asin(-2 * (+0)), atan2(+0, 1)
+                    // = (+0, -0, +0) (quat_to_euler); zero velocities
+                    const R zero3[3] = {0, 0, 0}, rpy0[3] = {R(0), -R(0), R(0)};
+                    obs_own(eb, k, z, rpy0, zero3, zero3);
+                } else if (k < ei[I_N * G + g]) {
+                    // a row the old episode used and the new one does not (rows >= the old NUM_DRONES are zero)
+                    for (int c = 0; c < 86; c += 2) st2(eb, k * 86 + c, 0.0f, 0.0f);
+                }
+            }
+            for (int u = ct; u < nr * M; u += CW) {
+                const int k0 = qdiv(u, M, rM), g = rl[k0], j = u - k0 * M, uc = g * M + j;
+                R x, y, vx, vy;
+                reset_cow_at(p, (long long)e0 * M + uc, p.env_off + e0 + g, j, S.spx[uc], S.spy[uc],
+                             (uint32_t)ei[I_EPISODE * G + g], x, y, vx, vy);
+                S.cx[uc] = x; S.cy[uc] = y;
+            }
+            cow_sync(fl + F_X2, W1, false);
+            if (wobs) {
+                for (int u = ct; u < nr * N; u += CW) {
+                    const int k0 = qdiv(u, N, rN), g = rl[k0], i = u - k0 * N;
+                    const int n = ei[I_NEWN * G + g];
+                    if (i >= n) continue;
+                    const int nb = nearest_two(S.dx, S.dy, g * N, i, n);
+                    obs_nbr(obs_wg + g * RW, S.dx, S.dy, g * N, i, (nb & 0xff) - 1, (nb >> 8) - 1);
+                }
+                for (int u = ct; u < nr * M; u += CW) {
+                    const int k0 = qdiv(u, M, rM), g = rl[k0], j = u - k0 * M, uc = g * M + j;
+                    if (j < m_obs)
+                        obs_cattle(obs_wg + g * RW, S.dx, S.dy, g * N, j, ei[I_NEWN * G + g], cat_off, S.cx[uc], S.cy[uc]);
+                }
+            }
+        }
     }
     lds_barrier();
     if (tid == 0) TS(13, (long long)clock64());
 
-    // ---- auto-reset of finished envs (SB3 VecEnv semantics) --------------------------------------
-    const int nr = ei[I_COUNT * G + G + 1];
-    if (nr) {   // uniform: read after the barrier
-        const int* rl = ei + I_COUNT * G;
-        if (p.terminal_obs)   // info["terminal_observation"]: the pre-reset observation
-            env_list_obs(p.terminal_obs + (long long)e0 * RW, S.img, rl, nr, RW, tid, BS);
-        if (tid < nr) {
-            const int g = rl[tid], e = e0 + g;
-            int n = ei[I_N * G + g], sc = ei[I_SC * G + g], scA = ei[I_SCA * G + g], spawn = ei[I_SPAWN * G + g];
-            int episode = ei[I_EPISODE * G + g], active = ei[I_ACTIVE * G + g], has_prev = ei[I_HASPREV * G + g];
-            R prev = S.prev[g], clock = S.clock[g];
-            reset_scalars(p, e, n, sc, scA, spawn, episode, active, has_prev, prev, clock);
-            ei[I_N * G + g] = n; ei[I_SC * G + g] = sc; ei[I_SCA * G + g] = scA; ei[I_SPAWN * G + g] = spawn;
-            ei[I_EPISODE * G + g] = episode; ei[I_ACTIVE * G + g] = active; ei[I_HASPREV * G + g] = has_prev;
-            S.prev[g] = prev; S.clock[g] = clock;
-            if (p.agent_active)
-                for (int i = 0; i < N; ++i) p.agent_active[(long long)e * N + i] = (active >> i) & 1;
-        }
-        lds_barrier();
-        env_list_obs(nullptr, S.img, rl, nr, RW, tid, BS);   // clear the images of the envs being reset
-        const float rN = 1.0f / (float)N, rM = 1.0f / (float)M;
-        for (int u = tid; u < nr * N; u += BS) {
-            const int k0 = qdiv(u, N, rN), g = rl[k0], k = u - k0 * N, ud = g * N + k;
-            const int n = ei[I_N * G + g];
-            R x, y, z;
-            reset_drone(p, (long long)e0 * N + ud, k, n, x, y, z);
-            S.dx[ud] = x; S.dy[ud] = y; S.dz[ud] = z;
-        }
-        for (int u = tid; u < nr * M; u += BS) {
-            const int k0 = qdiv(u, M, rM), g = rl[k0], j = u - k0 * M, uc = g * M + j;
-            R x, y, vx, vy;
-            reset_cow(p, (long long)e0 * M + uc, p.env_off + e0 + g, j, ei[I_SPAWN * G + g],
-                      (uint32_t)(ei[I_EPISODE * G + g] - 1), x, y, vx, vy);
-            S.cx[uc] = x; S.cy[uc] = y;
-        }
-        lds_barrier();
-        for (int u = tid; u < nr * N; u += BS) {
-            const int k0 = qdiv(u, N, rN), g = rl[k0], i = u - k0 * N, ud = g * N + i;
-            const int n = ei[I_N * G + g];
-            if (i >= n) continue;
-            // identity quaternion (getEulerFromQuaternion -> 0), zero velocities
-            const R qid[4] = {0, 0, 0, 1}, zero3[3] = {0, 0, 0};
-            R rpy0[3];
-            quat_to_euler(qid, rpy0);
-            img_own(S.img, g, rows, i, S.dz[ud], rpy0, zero3, zero3);
-            int i1, i2;
-            nearest_two(S.dx, S.dy, g * N, i, n, i1, i2);
-            img_nbr(S.img, S.dx, S.dy, g, N, rows, i, i1, i2);
-        }
-        for (int u = tid; u < nr * M; u += BS) {
-            const int k0 = qdiv(u, M, rM), g = rl[k0], j = u - k0 * M, uc = g * M + j;
-            if (j < m_obs) img_cattle(S.img, S.dx, S.dy, g, N, rows, j, ei[I_N * G + g], cat_off, S.cx[uc], S.cy[uc]);
-        }
-        lds_barrier();
-        if (wobs) env_list_obs(obs_wg, S.img, rl, nr, RW, tid, BS);
-    }
-
-    // ---- env scalars back to HBM -----------------------------------------------------------------
+    // ---- env scalars back to HBM (the drone wave's env lanes hold them) -----------------------------
     if (tid < Gv && wobs) {
-        const int g = tid, e = e0 + g;
-        p.envi[0 * E + e] = ei[I_N * G + g]; p.envi[1 * E + e] = ei[I_SC * G + g]; p.envi[2 * E + e] = ei[I_SCA * G + g];
-        p.envi[3 * E + e] = ei[I_HASPREV * G + g]; p.envi[4 * E + e] = ei[I_LEVEL * G + g];
-        p.envi[5 * E + e] = ei[I_TALLY * G + g]; p.envi[6 * E + e] = ei[I_SPAWN * G + g];
-        p.envi[7 * E + e] = ei[I_ACTIVE * G + g]; p.envi[8 * E + e] = ei[I_EPISODE * G + g];
+        const int e = e0 + tid;
+        p.envi[0 * E + e] = f_n; p.envi[1 * E + e] = f_sc; p.envi[2 * E + e] = f_scA; p.envi[3 * E + e] = f_hp;
+        p.envi[4 * E + e] = f_level; p.envi[5 * E + e] = f_tally; p.envi[6 * E + e] = f_spawn;
+        p.envi[7 * E + e] = f_active; p.envi[8 * E + e] = f_episode;
         p.envi[9 * E + e] += 1;   // ch_step calls on this env
-        p.envr[0 * E + e] = S.prev[g]; p.envr[1 * E + e] = S.clock[g];
+        p.envr[0 * E + e] = f_prev; p.envr[1 * E + e] = f_clock;
     }
     if (tid == 0) { TS(14, (long long)clock64()); TS(1, (long long)wall_clock64()); }
 }

@@ -265,3 +265,43 @@ def test_step_kernels_v1_v2_bit_identical(mode, n, m, E, geom):
     assert np.array_equal(hs[0].metrics(), hs[1].metrics(), equal_nan=True)
     for h in hs:
         h.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,n,m", [(0, 4, 16), (1, 4, 16), (0, 6, 8)])
+def test_obs_constant_bytes_sparse_writes(mode, n, m):
+    """The v2 step stores only the observation entries that change; the constant-zero bytes of each
+    block (rows >= NUM_DRONES, the action-buffer block) stay from the last full write (ch_api.cpp
+    obs_zero_ptr).  With NUM_DRONES drawn per episode the dead rows move at every reset; a caller that
+    scribbles over obs and calls invalidate_obs(), and a set_state(), must both get full blocks again.
+    Compared bit for bit with the v1 kernel, which writes every block in full each step."""
+    import ctypes
+    import torch
+    from cattleherd import _lib
+    E = 777
+    hs = [_batch(mode, n, m, E, None, min_drones=2, max_drones=n) for _ in range(2)]
+    assert _lib.lib().ch__set_kernel(hs[0].handle, ctypes.c_int32(1)) == 0
+    assert _lib.lib().ch__set_kernel(hs[1].handle, ctypes.c_int32(2)) == 0
+    for h in hs:
+        h.reset()
+    resets = 0
+    for t in range(200):
+        if t == 60:
+            hs[1].obs.fill_(3.0)
+            hs[1].invalidate_obs()
+        if t == 120:
+            d, i = hs[1].get_state_raw()
+            hs[1].obs.fill_(-1.0)
+            hs[1].set_state_raw(d, i)
+        outs = []
+        for h in hs:
+            h.step(random_actions=True, autoreset=True, terminal_obs=True)
+            outs.append([x.clone() for x in (h.obs, h.reward, h.terminated, h.truncated, h.terminal_obs,
+                                             h.reset_happened)])
+        torch.cuda.synchronize()
+        resets += int(outs[0][5].sum())
+        for a, b in zip(*outs):
+            assert torch.equal(torch.nan_to_num(a.float(), nan=7.0), torch.nan_to_num(b.float(), nan=7.0)), t
+    assert resets > 0
+    for h in hs:
+        h.close()

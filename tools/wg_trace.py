@@ -23,7 +23,7 @@ def trace(mode, E, n, m, prec, G=None, B=None, steps=4):
     g, blk, lds, kv = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int32()
     L.ch__geometry(b.handle, ctypes.byref(g), ctypes.byref(blk), ctypes.byref(lds), ctypes.byref(kv))
     grid = (E + g.value - 1) // g.value
-    ts = torch.zeros((grid, 16), dtype=torch.int64, device=b.device)
+    ts = torch.zeros((grid, 32), dtype=torch.int64, device=b.device)
     b.reset()
     for _ in range(250):   # steady state: resets have desynchronised the flocking parity
         b.step(random_actions=True, autoreset=True, terminal_obs=False)
@@ -47,9 +47,22 @@ def trace(mode, E, n, m, prec, G=None, B=None, steps=4):
               f"{np.percentile(start, 90):.1f}/{start.max():.1f}us | WG dur mean/max {dur.mean():.1f}/{dur.max():.1f}us"
               f" | ~{clk:.2f} GHz | CUs {cus}")
         print(f"   drone wave (cycles from start): B0 {rel(3):.0f} chain {rel(4):.0f} terms {rel(5):.0f} "
-              f"H {rel(6):.0f} book {rel(7):.0f} | cow waves: alpha {rel(8):.0f} D {rel(9):.0f} flock {rel(10):.0f} "
+              f"H {rel(6):.0f} resets-published {rel(15):.0f} book {rel(7):.0f} | cow waves: alpha {rel(8):.0f} D {rel(9):.0f} flock {rel(10):.0f} "
               f"copy {rel(11):.0f} | B1 {rel(13):.0f} end {rel(14):.0f}")
-    L.ch__set_tstamp(b.handle, None)
+        print(f"   cow waves: integrate {rel(16):.0f} E {rel(17):.0f} pairs {rel(18):.0f} zero {rel(19):.0f} "
+              f"A {rel(20):.0f} rows {rel(21):.0f} spawn {rel(8):.0f}")
+        tail = (t[:, 14] - t[:, 13]).astype(np.float64)
+        chain = (t[:, 4] - t[:, 3]).astype(np.float64)
+        res = tail > 3000
+        print(f"   spread: WG cycles q50/q90/max {np.percentile(cyc, 50):.0f}/{np.percentile(cyc, 90):.0f}/{cyc.max():.0f}"
+              f" | resetting WGs {int(res.sum())}: cycles mean {cyc[res].mean() if res.any() else 0:.0f} vs "
+              f"{cyc[~res].mean():.0f} | chain q50/q90/max {np.percentile(chain, 50):.0f}/{np.percentile(chain, 90):.0f}/"
+              f"{chain.max():.0f}")
+        slow = np.argsort(cyc)[-5:]
+        for k in slow:
+            print(f"     slow WG {k}: cyc {cyc[k]:.0f} chain {chain[k]:.0f} tail {tail[k]:.0f} B0 {t[k, 3] - t[k, 2]} "
+                  f"terms {t[k, 5] - t[k, 4]} H {t[k, 6] - t[k, 5]} book {t[k, 7] - t[k, 6]} B1 {t[k, 13] - t[k, 7]} "
+                  f"cu {t[k, 12]}")
     b.close()
 
 
@@ -90,7 +103,7 @@ def back_to_back(mode="ctde", E=4096, n=4, m=16, prec="f64", k=12):
     g, blk, lds, kv = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int32()
     L.ch__geometry(b.handle, ctypes.byref(g), ctypes.byref(blk), ctypes.byref(lds), ctypes.byref(kv))
     grid = (E + g.value - 1) // g.value
-    ts = torch.zeros((k, grid, 16), dtype=torch.int64, device=b.device)
+    ts = torch.zeros((k, grid, 32), dtype=torch.int64, device=b.device)
     b.reset()
     for _ in range(250):
         b.step(random_actions=True, autoreset=True, terminal_obs=False)
