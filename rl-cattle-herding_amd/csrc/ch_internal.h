@@ -61,10 +61,10 @@ struct Level {
 };
 
 // LDS carve of one v2 step workgroup (ch_step.hip); identical on host (size) and device (offsets).
-constexpr int kV2EnvInts = 12;
-constexpr int kV2Flags = 9;          // LDS hand-off counters between the drone wave and the cow waves
+constexpr int kV2EnvInts = 13;
+constexpr int kV2Flags = 16;         // LDS hand-off counters between the drone wave and the cow waves + work counters
 struct V2Layout {
-    enum { CX = 0, DRONE, DCOW, ENVR, PAIRS, MET, IMG, EI, LEVELS, BYTES, NOFF };
+    enum { CX = 0, DRONE, DCOW, ENVR, PAIRS, MET, IMG, EI, LEVELS, PAIRL, BYTES, NOFF };
     int G, N, M, P, rows;
     size_t off[NOFF + 1];
     static __host__ __device__ size_t al(size_t x) { return (x + 15) & ~size_t(15); }
@@ -74,13 +74,14 @@ struct V2Layout {
         off[CX] = o;     o = al(o + 8 * (size_t)G * M * rb);         // cx cy cvx cvy aux auy spx spy
         off[DRONE] = o;  o = al(o + 12 * (size_t)G * N * rb);        // dx dy dz pa pb sa sb ca cb scat psp mrew
         off[DCOW] = o;   o = al(o + (size_t)G * N * M * rb);         // cow-drone distances
-        off[ENVR] = o;   o = al(o + 2 * (size_t)G * rb);             // prev clock
-        off[PAIRS] = o;  o = al(o + 4 * (size_t)G * P * rb);         // alpha pair table
+        off[ENVR] = o;   o = al(o + 4 * (size_t)G * rb);             // prev clock, herd centroid x y
+        off[PAIRS] = o;  o = al(o + (4 * (size_t)G * P > 6 * (size_t)G * M * N ? 4 * (size_t)G * P : 6 * (size_t)G * M * N) * rb);   // alpha pair table, then shepherd terms
         off[MET] = o;    o = al(o + (size_t)kMetricRows * G * 8);
         off[IMG] = o;                                                // (observations go straight to HBM)
         off[EI] = o;     o = al(o + ((size_t)kV2EnvInts * G + 2 * G + 2 + kV2Flags) * 4);   // + flock/reset lists
         off[LEVELS] = o; o = al(o + 8 * sizeof(Level));              // curriculum table
-        off[BYTES] = o;  o = al(o + (size_t)G * P + 3 * (size_t)G * N + (size_t)G * M);
+        off[PAIRL] = o;  o = al(o + 2 * (size_t)P);                  // unordered cow pairs (i | j << 8)
+        off[BYTES] = o;  o = al(o + (size_t)G * P + 3 * (size_t)G * N + (size_t)G * M + (size_t)G * M * N);
         off[NOFF] = o;
     }
     __host__ __device__ size_t bytes() const { return off[NOFF]; }

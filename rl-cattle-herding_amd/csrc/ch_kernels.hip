@@ -253,7 +253,7 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
                     pair_terms(qix, qiy, pix, piy, qkx, qky, pkx, pky, ra_b, da_b, gx, gy, cxx, cyy);
                 }
                 if (dn <= R(1.1)) {
-                    R d3 = m_pow(dn, R(3.0));
+                    R d3 = cube(dn);
                     sx += R(-650000.0) * ex / d3;
                     sy += R(-650000.0) * ey / d3;
                 }

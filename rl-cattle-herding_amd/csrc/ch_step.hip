@@ -31,9 +31,10 @@ namespace ch {
 
 // per-env integer scalars kept in LDS (index I * G + g)
 enum { I_N = 0, I_SC, I_SCA, I_HASPREV, I_LEVEL, I_TALLY, I_SPAWN, I_ACTIVE, I_EPISODE, I_FLOCK, I_RESET, I_NEWN,
-       I_COUNT };
+       I_HERD, I_COUNT };
 static_assert(I_COUNT == kV2EnvInts, "LDS env-int rows");
-enum { F_D = 0, F_T, F_H, F_A, F_E, F_R, F_X0, F_X1, F_X2 };   // hand-off counters
+enum { F_D = 0, F_T, F_H, F_A, F_E, F_R, F_X0, F_X1, F_X2,     // hand-off counters
+       C_PAIRS, C_ROWS, C_COWS, C_FLOCK, C_DELTA, F_W, F_Q };    // work counters (grab), cow-wave syncs
 // after the per-env rows: flocking-env list [G], reset-env list [G], their counts, then the counters
 #define FL_LIST (I_COUNT * G)
 #define RS_LIST (I_COUNT * G + G)
@@ -83,6 +84,16 @@ __device__ __forceinline__ void lds_wait(int* f, int target) {
 
 // barrier among the cow waves only (the drone wave keeps running); `global` also publishes their
 // global stores (needed before other cow lanes rewrite the same state)
+// Dynamic share-out of a cow-wave loop: each call hands the calling wave the next n items of the
+// counter.  The cow waves do not run at equal speed (one of them shares its SIMD with the other
+// resident workgroup's prioritised drone wave), so a static lane -> item split leaves the slowest
+// wave with as many items as the fastest.
+__device__ __forceinline__ int grab(int* ctr, int n) {
+    int b = 0;
+    if ((threadIdx.x & 63) == 0) b = atomicAdd(ctr, n);
+    return __builtin_amdgcn_readfirstlane(b);
+}
+
 __device__ __forceinline__ void cow_sync(int* f, int waves, bool global) {
     if (global) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     lds_signal(f);
@@ -104,13 +115,16 @@ struct V2Smem {
     R *pa, *pb, *sa, *sb, *ca, *cb, *scat, *psp;     // [G*N] per-drone reward terms
     R* mrew;                                         // [G*N] MARL per-agent reward scratch
     R* dcow;                                         // [G*N*M] cow-drone distances, (g*N + k)*M + j
-    R *prev, *clock;                                 // [G]
+    R *prev, *clock, *hcx, *hcy;                     // [G] env reals; herd centroid (cow waves)
     R *tgx, *tgy, *tcx, *tcy;                        // [G*P] alpha pair table
+    R* td;                                           // [6][G*M*N] shepherd/predator terms (reuses the pair table)
     double* met;                                     // [kMetricRows*G]
     int* ei;                                         // [I_COUNT*G] + list [G] + 2 + flags
     int* flags;
     Level* LT;                                       // curriculum table (curriculum_learning.py:10-194)
+    const uint16_t* pl;                              // [P] unordered cow pairs, copied from p.pairs
     uint8_t *pflag, *dflags, *herded, *md1, *md2;    // [G*P], [G*N], [G*M], [G*N], [G*N]
+    uint8_t* tdf;                                    // [G*M*N] shepherd term in range | predator in range << 1
 
     __device__ V2Smem(unsigned char* base, const V2Layout& L) {
         const int GM = L.G * L.M, GN = L.G * L.N, GP = L.G * L.P;
@@ -120,14 +134,16 @@ struct V2Smem {
         pa = dz + GN; pb = pa + GN; sa = pb + GN; sb = sa + GN; ca = sb + GN; cb = ca + GN; scat = cb + GN;
         psp = scat + GN; mrew = psp + GN;
         dcow = (R*)(base + L.off[V2Layout::DCOW]);
-        prev = (R*)(base + L.off[V2Layout::ENVR]); clock = prev + L.G;
+        prev = (R*)(base + L.off[V2Layout::ENVR]); clock = prev + L.G; hcx = clock + L.G; hcy = hcx + L.G;
+        pl = (const uint16_t*)(base + L.off[V2Layout::PAIRL]);
         tgx = (R*)(base + L.off[V2Layout::PAIRS]); tgy = tgx + GP; tcx = tgy + GP; tcy = tcx + GP;
+        td = tgx;
         met = (double*)(base + L.off[V2Layout::MET]);
         ei = (int*)(base + L.off[V2Layout::EI]);
         flags = ei + I_COUNT * L.G + 2 * L.G + 2;
         LT = (Level*)(base + L.off[V2Layout::LEVELS]);
         pflag = base + L.off[V2Layout::BYTES]; dflags = pflag + GP; herded = dflags + GN; md1 = herded + GM;
-        md2 = md1 + GN;
+        md2 = md1 + GN; tdf = md2 + GN;
     }
 };
 
@@ -136,8 +152,15 @@ struct V2Smem {
 // (drone wave, after the reward terms), cattle offsets (cow waves, after the distance table), and the
 // always-zero bytes (cow waves, during the alpha phase).  `eb` is the env's block (row 0, col 0); 86 is
 // even, so every float2 below is 8-byte aligned.
+#ifdef CH_NT_STORES
+#define CH_ST(ptr, val) __builtin_nontemporal_store((val), (ptr))
+#else
+#define CH_ST(ptr, val) (*(ptr) = (val))
+#endif
+typedef float f2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void st2(float* eb, int off, float a, float b) {
-    reinterpret_cast<float2*>(eb + off)[0] = make_float2(a, b);
+    f2v v = {a, b};
+    CH_ST(reinterpret_cast<f2v*>(eb + off), v);
 }
 
 // own-state entries of row `row` (BaseRLAviary.py:289-295)
@@ -197,7 +220,7 @@ __device__ __forceinline__ int nearest_two(const R* dx, const R* dy, int b0, int
 // flock alpha term, pair form, for every flocking env (flockUtils.py:237-258, 327-337; MathUtils 11-58).
 // l = lane rank among the A lanes that share the table.
 template <class R>
-__device__ __forceinline__ void alpha_pairs(const StepParams<R>& p, V2Smem<R>& S, int G, int M, int P, int l, int A) {
+__device__ __forceinline__ void alpha_pairs(const StepParams<R>& p, V2Smem<R>& S, int G, int M, int P) {
     const int nf = S.ei[NF_AT];
     const int* flist = S.ei + FL_LIST;
     const R ra = sigma_norm_n(R(1.2)), da = ra;
@@ -205,7 +228,7 @@ __device__ __forceinline__ void alpha_pairs(const StepParams<R>& p, V2Smem<R>& S
     const float rP = 1.0f / (float)P;
     auto one = [&](int q) {
         const int f = qdiv(q, P, rP), r = q - f * P, g = flist[f];
-        const uint32_t pr = p.pairs[r];
+        const uint32_t pr = S.pl[r];
         const int bi = g * M + (pr & 0xff), bj = g * M + (pr >> 8);
         const R zx = S.cx[bj] - S.cx[bi], zy = S.cy[bj] - S.cy[bi];
         const R nrm = sqrt(zx * zx + zy * zy);
@@ -216,9 +239,12 @@ __device__ __forceinline__ void alpha_pairs(const StepParams<R>& p, V2Smem<R>& S
         if (in) pair_terms_n(nrm, zx, zy, S.cvx[bi], S.cvy[bi], S.cvx[bj], S.cvy[bj], ra, da, gx, gy, cx, cy);
         S.tgx[idx] = gx; S.tgy[idx] = gy; S.tcx[idx] = cx; S.tcy[idx] = cy;
     };
-    for (int q = l; q < tot; q += 2 * A) {   // two independent pairs per iteration (instruction-level parallelism)
-        one(q);
-        if (q + A < tot) one(q + A);
+    const int lane = threadIdx.x & 63;
+    for (;;) {   // 128 pairs per grab, two independent pairs per lane (instruction-level parallelism)
+        const int b = grab(S.flags + C_PAIRS, 128);
+        if (b >= tot) break;
+        if (b + lane < tot) one(b + lane);
+        if (b + 64 + lane < tot) one(b + 64 + lane);
     }
 }
 
@@ -243,53 +269,55 @@ __device__ __forceinline__ void alpha_row(V2Smem<R>& S, int M, int P, int u, int
     S.aux[u] = ux; S.auy[u] = uy;
 }
 
-// shepherd (delta, flockUtils.py:271-317), predator (343-348) and gamma (150-160, 340-341) terms and the
-// velocity update with the speed clip (BaseAviary.py:1384-1400) of cow u; |y_k - q_i| from the
-// distance table.  Four drones per batch, evaluated independently and accumulated in drone order.
+// shepherd (delta, flockUtils.py:271-317) and predator (343-348) terms of drone k on cow u = g*M + j,
+// one (cow, drone) item per lane; stored in the term table for flock_combine.
 template <class R>
-__device__ __forceinline__ void cow_flock(const StepParams<R>& p, V2Smem<R>& S, int N, int M, int e0, int u, int g,
-                                          int j, int n) {
+__device__ __forceinline__ void delta_term(V2Smem<R>& S, int N, int M, int u, int g, int k, int T) {
+    const R ra_b = sigma_norm_n(R(1.0)), da_b = ra_b;
+    const R qix = S.cx[u], qiy = S.cy[u], pix = S.cvx[u], piy = S.cvy[u];
+    const R yx = S.dx[g * N + k], yy = S.dy[g * N + k];
+    const R ex = yx - qix, ey = yy - qiy;
+    const R dn = sqrt(ex * ex + ey * ey);   // = the distance table entry
+    const bool in = dn <= R(999 + 2), pr = dn <= R(1.1);
+    R t[6] = {0, 0, 0, 0, 0, 0};
+    if (in) {
+        R difx = qix - yx, dify = qiy - yy;
+        R d = dn + R(1e-6);
+        R mu = d / R(1.0) < R(1.0) ? d / R(1.0) : R(1.0);
+        R akx = difx / d, aky = dify / d;
+        R P00 = R(1) - akx * akx, P01 = R(0) - akx * aky, P10 = R(0) - aky * akx, P11 = R(1) - aky * aky;
+        R qkx = mu * qix + (R(1) - mu) * yx, qky = mu * qiy + (R(1) - mu) * yy;
+        R pkx = mu * (P00 * pix + P01 * piy), pky = mu * (P10 * pix + P11 * piy);
+        pair_terms(qix, qiy, pix, piy, qkx, qky, pkx, pky, ra_b, da_b, t[0], t[1], t[2], t[3]);
+    }
+    if (pr) {
+        R d3 = cube(dn);
+        t[4] = R(-650000.0) * ex / d3;
+        t[5] = R(-650000.0) * ey / d3;
+    }
+    const int i = u * N + k;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) S.td[c * T + i] = t[c];
+    S.tdf[i] = (uint8_t)(in | (pr << 1));
+}
+
+// gamma term (flockUtils.py:150-160, 340-341), the drone terms summed in drone order, and the velocity
+// update with the speed clip (BaseAviary.py:1384-1400) of cow u.  A term out of range is +0 in the
+// table, and adding +0 to a sum that starts at +0 leaves it unchanged, so only the count needs the flag.
+template <class R>
+__device__ __forceinline__ void flock_combine(const StepParams<R>& p, V2Smem<R>& S, int N, int M, int e0, int u, int n,
+                                              int T) {
     const long long CS = (long long)p.E * M;
     const R C2B = R(2 * 4.47213595499958), C1G = R(5), C2G = R(0.2 * 2.23606797749979);
-    const R ra_b = sigma_norm_n(R(1.0)), da_b = ra_b;
-    const int b0 = g * N;
     const R qix = S.cx[u], qiy = S.cy[u], pix = S.cvx[u], piy = S.cvy[u];
     R ddx = 0, ddy = 0, sx = 0, sy = 0, gx = 0, gy = 0, cxx = 0, cyy = 0;
     int nb = 0;
-    for (int k0 = 0; k0 < n; k0 += 4) {
-        R t[4][6];
-        bool in[4], pr[4];
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-            const int k = min(k0 + v, n - 1);
-            const R yx = S.dx[b0 + k], yy = S.dy[b0 + k];
-            const R ex = yx - qix, ey = yy - qiy;
-            const R dn = S.dcow[(b0 + k) * M + j];   // = sqrt(ex * ex + ey * ey)
-            in[v] = dn <= R(999 + 2);
-            pr[v] = dn <= R(1.1);
-            t[v][0] = t[v][1] = t[v][2] = t[v][3] = t[v][4] = t[v][5] = 0;
-            if (in[v]) {
-                R difx = qix - yx, dify = qiy - yy;
-                R d = dn + R(1e-6);
-                R mu = d / R(1.0) < R(1.0) ? d / R(1.0) : R(1.0);
-                R akx = difx / d, aky = dify / d;
-                R P00 = R(1) - akx * akx, P01 = R(0) - akx * aky, P10 = R(0) - aky * akx, P11 = R(1) - aky * aky;
-                R qkx = mu * qix + (R(1) - mu) * yx, qky = mu * qiy + (R(1) - mu) * yy;
-                R pkx = mu * (P00 * pix + P01 * piy), pky = mu * (P10 * pix + P11 * piy);
-                pair_terms(qix, qiy, pix, piy, qkx, qky, pkx, pky, ra_b, da_b, t[v][0], t[v][1], t[v][2], t[v][3]);
-            }
-            if (pr[v]) {
-                R d3 = m_pow(dn, R(3.0));
-                t[v][4] = R(-650000.0) * ex / d3;
-                t[v][5] = R(-650000.0) * ey / d3;
-            }
-        }
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-            if (k0 + v >= n) break;
-            if (in[v]) { ++nb; gx += t[v][0]; gy += t[v][1]; cxx += t[v][2]; cyy += t[v][3]; }
-            if (pr[v]) { sx += t[v][4]; sy += t[v][5]; }
-        }
+    CH_UNROLL for (int k = 0; k < N; ++k) {
+        if (k >= n) break;
+        const int i = u * N + k;
+        const int f = S.tdf[i];
+        if (f & 1) { ++nb; gx += S.td[i]; gy += S.td[T + i]; cxx += S.td[2 * T + i]; cyy += S.td[3 * T + i]; }
+        if (f & 2) { sx += S.td[4 * T + i]; sy += S.td[5 * T + i]; }
     }
     if (nb > 0) { ddx = C2B * gx + C2B * cxx; ddy = C2B * gy + C2B * cyy; }
     ddx += sx; ddy += sy;
@@ -300,7 +328,7 @@ __device__ __forceinline__ void cow_flock(const StepParams<R>& p, V2Smem<R>& S, 
     R sp = norm2(vx, vy);
     if (sp > R(kMaxVelCattle)) { R f = R(kMaxVelCattle) / sp; vx *= f; vy *= f; }
     const long long ci = (long long)e0 * M + u;
-    p.cattle[2 * CS + ci] = vx; p.cattle[3 * CS + ci] = vy;
+    CH_ST(&p.cattle[2 * CS + ci], vx); CH_ST(&p.cattle[3 * CS + ci], vy);
 }
 
 // GT/NT/MT > 0 specialise the kernel for one geometry (envs per workgroup, drones, cattle): the LDS
@@ -325,6 +353,7 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
     int* fl = S.flags;
     const Level* LT = S.LT;
     if (tid == 0) { TS(0, (long long)wall_clock64()); TS(2, (long long)clock64()); TS(12, (long long)__smid()); }
+    if ((tid & 63) == 0 && tid < 256) TS(22 + (tid >> 6), (long long)__builtin_amdgcn_s_getreg((31 << 11) | 4));   // HW_ID
     if (tid < kV2Flags) fl[tid] = 0;
     lds_barrier();   // hand-off counters cleared before anyone signals
 
@@ -349,6 +378,7 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
         }
         for (int k = tid; k < (int)(sizeof(kLevels) / 4); k += 64)
             reinterpret_cast<uint32_t*>(S.LT)[k] = reinterpret_cast<const uint32_t*>(kLevels)[k];
+        for (int k = tid; k < P; k += 64) const_cast<uint16_t*>(S.pl)[k] = p.pairs[k];
         const int g = tid;
         bool flk = false;
         if (g < Gv) {
@@ -359,7 +389,7 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
             ei[I_HASPREV * G + g] = p.envi[3 * E + e]; ei[I_LEVEL * G + g] = p.envi[4 * E + e];
             ei[I_TALLY * G + g] = p.envi[5 * E + e]; ei[I_SPAWN * G + g] = p.envi[6 * E + e];
             ei[I_ACTIVE * G + g] = p.envi[7 * E + e]; ei[I_EPISODE * G + g] = p.envi[8 * E + e];
-            ei[I_FLOCK * G + g] = flk; ei[I_RESET * G + g] = 0;
+            ei[I_FLOCK * G + g] = flk; ei[I_RESET * G + g] = 0; ei[I_HERD * G + g] = 0;
             S.prev[g] = p.envr[e]; S.clock[g] = p.envr[E + e];
 #pragma unroll
             for (int r = 0; r < kMetricRows; ++r) S.met[r * G + g] = p.metrics[r * E + e];
@@ -370,18 +400,23 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
         if (tid == 0) { ei[NF_AT] = __popcll(bal); ei[NR_AT] = 0; }
         lds_signal(fl + F_E);
     } else {
+        const float rM0 = 1.0f / (float)M;
         for (int u = ct; u < Gv * M; u += CW) {
             const long long ci = (long long)e0 * M + u;   // the workgroup's cows are contiguous per component
             R x = p.cattle[0 * CS + ci], y = p.cattle[1 * CS + ci];
             const R vx = p.cattle[2 * CS + ci], vy = p.cattle[3 * CS + ci];
+            const int g = qdiv(u, M, rM0), j = u - g * M;
+            int sp = p.envi[6 * E + e0 + g] + 1;   // spawn index of the episode an auto-reset would start
             const R dt = R(p.dt);
             for (int s = 0; s < p.substeps; ++s) { x += vx * dt; y += vy * dt; }   // frictionless cube (trace-pinned)
-            p.cattle[0 * CS + ci] = x; p.cattle[1 * CS + ci] = y;
+            CH_ST(&p.cattle[0 * CS + ci], x); CH_ST(&p.cattle[1 * CS + ci], y);
             S.cx[u] = x; S.cy[u] = y; S.cvx[u] = vx; S.cvy[u] = vy;
+            // its cow positions (BaseAviary.py:600-606), fetched now so that a reset needs no global load
+            if (sp >= p.n_scen) sp = 0;
+            const double* tab = p.spawn + ((long long)sp * p.n_cows + j) * 2;
+            S.spx[u] = R(tab[0]); S.spy[u] = R(tab[1]);
         }
-        if (ct == 0) TS(16, (long long)clock64());
         lds_wait(fl + F_E, 1);   // env scalars and the flocking list from the drone wave
-        if (ct == 0) TS(17, (long long)clock64());
     }
     if (tid == 0) TS(3, (long long)clock64());
 
@@ -421,12 +456,14 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
                     drone_substep(pos, q, v, w, rpm, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0);
             }
             R* D = p.drone;
-            D[0 * DS + di] = pos[0]; D[1 * DS + di] = pos[1]; D[2 * DS + di] = pos[2];
-            D[3 * DS + di] = q[0]; D[4 * DS + di] = q[1]; D[5 * DS + di] = q[2]; D[6 * DS + di] = q[3];
-            D[7 * DS + di] = v[0]; D[8 * DS + di] = v[1]; D[9 * DS + di] = v[2];
-            D[10 * DS + di] = w[0]; D[11 * DS + di] = w[1]; D[12 * DS + di] = w[2];
 #pragma unroll
-            for (int c = 0; c < 9; ++c) D[(13 + c) * DS + di] = pid[c];
+            for (int c = 0; c < 3; ++c) CH_ST(&D[c * DS + di], pos[c]);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) CH_ST(&D[(3 + c) * DS + di], q[c]);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) { CH_ST(&D[(7 + c) * DS + di], v[c]); CH_ST(&D[(10 + c) * DS + di], w[c]); }
+#pragma unroll
+            for (int c = 0; c < 9; ++c) CH_ST(&D[(13 + c) * DS + di], pid[c]);
             quat_to_euler(q, rpy_out);
             S.dx[tid] = pos[0]; S.dy[tid] = pos[1]; S.dz[tid] = pos[2];
         }
@@ -481,13 +518,13 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
             S.scat[tid] = cattle_spacing(best, R(p.cs_cc));
         }
         wave_sync();
-        if (tid == 0) TS(15, (long long)clock64());
+        if (tid == 0) TS(26, (long long)clock64());
 
         // per-env bookkeeping, one env per lane, in the reference's call order; the final scalars stay in
         // this lane's registers and go to HBM after the last barrier
         const int g = tid;
         const bool envl = g < Gv;
-        const int e = e0 + g, b0 = g * N, c0 = g * M;
+        const int e = e0 + g, b0 = g * N;
         if (envl) {
             f_n = ei[I_N * G + g]; f_sc = ei[I_SC * G + g]; f_scA = ei[I_SCA * G + g]; f_hp = ei[I_HASPREV * G + g];
             f_level = ei[I_LEVEL * G + g]; f_tally = ei[I_TALLY * G + g]; f_spawn = ei[I_SPAWN * G + g];
@@ -502,10 +539,10 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
         if (envl && task) {
             const int n = f_n;
             R sdx = 0, sdy = 0;
-            int herded = 0;
-            CH_UNROLL for (int j = 0; j < M; ++j) { scx += S.cx[c0 + j]; scy += S.cy[c0 + j]; herded += S.herded[c0 + j]; }
+            const int herded = ei[I_HERD * G + g];   // counted by the cow waves (winding number)
+            scx = S.hcx[g]; scy = S.hcy[g];          // herd centroid, summed by the cow waves
             CH_UNROLL for (int i = 0; i < N; ++i) if (i < n) { sdx += S.dx[b0 + i]; sdy += S.dy[b0 + i]; }
-            scx /= R(M); scy /= R(M); sdx /= R(n); sdy /= R(n);
+            sdx /= R(n); sdy /= R(n);
             R ex = sdx - scx, ey = sdy - scy;
             cent = sqrt(ex * ex + ey * ey + R(0) * R(0));   // HerdCentroid/DroneCentroid, z = 0.95 both
             eff = R((double)herded / M * 100);
@@ -618,6 +655,7 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
         const unsigned long long rbal = __ballot(rs != 0);
         if (rs) ei[RS_LIST + __popcll(rbal & ((1ull << g) - 1ull))] = g;
         if (tid == 0) ei[NR_AT] = __popcll(rbal);
+        if (tid == 0) TS(27, (long long)clock64());
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         lds_signal(fl + F_R);
         if (tid == 0) TS(15, (long long)clock64());
@@ -669,7 +707,8 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
                 o[kMetricCurLen] = 0;
             }
 #pragma unroll
-            for (int r = 0; r < kMetricRows; ++r) p.metrics[r * E + e] = o[r];
+            for (int r = 0; r < kMetricRows; ++r) CH_ST(&p.metrics[r * E + e], o[r]);
+            if (g == 0) TS(28, (long long)clock64());
             if (p.reset_happened) p.reset_happened[e] = rs;
             // SB3 auto-reset: the new episode's scalars (the cow waves rebuild its bodies and observation)
             if (rs) reset_scalars(p, e, f_n, f_sc, f_scA, f_spawn, f_episode, f_active, f_hp, f_prev, f_clock);
@@ -681,7 +720,7 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
         if (tid == 0) TS(7, (long long)clock64());
     } else {
         // ============ cow waves ================================================================
-        alpha_pairs(p, S, G, M, P, ct, CW);
+        alpha_pairs(p, S, G, M, P);
         if (ct == 0) TS(18, (long long)clock64());
         // the constant-zero bytes of the observation blocks, when the host cannot vouch that this buffer
         // already holds them (first step into a buffer, after ch_set_state, ...; ch_api.cpp obs_zero_ptr)
@@ -694,24 +733,32 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
         const float rM = 1.0f / (float)M;
         const int nf = ei[NF_AT];
         const int* flist = ei + FL_LIST;
-        for (int u = ct; u < nf * M; u += CW) {   // cows of flocking envs only
-            const int f = qdiv(u, M, rM), g = flist[f], j = u - f * M;
-            alpha_row(S, M, P, g * M + j, g, j);
+        const int lane = tid & 63;
+        for (;;) {   // alpha rows of the cows of flocking envs
+            const int b = grab(fl + C_ROWS, 64), u = b + lane;
+            if (b >= nf * M) break;
+            if (u < nf * M) {
+                const int f = qdiv(u, M, rM), g = flist[f], j = u - f * M;
+                alpha_row(S, M, P, g * M + j, g, j);
+            }
         }
+        cow_sync(fl + F_W, W1, false);   // every alpha row read the pair table: its space now takes the drone terms
         if (ct == 0) TS(21, (long long)clock64());
-        // spawn positions of the episode an auto-reset would start: scenario index + 1 (BaseAviary.py:600-606),
-        // looked up while the drone wave is still integrating, so a reset needs no global load
-        for (int u = ct; u < Gv * M; u += CW) {
-            const int g = qdiv(u, M, rM), j = u - g * M;
-            int sp = ei[I_SPAWN * G + g] + 1;
-            if (sp >= p.n_scen) sp = 0;
-            const double* tab = p.spawn + ((long long)sp * p.n_cows + j) * 2;
-            S.spx[u] = R(tab[0]); S.spy[u] = R(tab[1]);
-        }
         if (ct == 0) TS(8, (long long)clock64());
         lds_wait(fl + F_D, 1);
         if (ct == 0) TS(9, (long long)clock64());
-        for (int u = ct; u < Gv * M; u += CW) {
+        for (;;) {   // per cow: distances, winding number, observation entries; then per env: herd centroid
+            const int b = grab(fl + C_COWS, 64), u = b + lane;
+            if (b >= Gv * M + Gv) break;
+            if (u >= Gv * M) {
+                const int g = u - Gv * M;   // herd centroid (CattleAviary.py: HerdCentroid, np.mean over the cattle)
+                if (g < Gv) {
+                    R sx = 0, sy = 0;
+                    CH_UNROLL for (int j = 0; j < M; ++j) { sx += S.cx[g * M + j]; sy += S.cy[g * M + j]; }
+                    S.hcx[g] = sx / R(M); S.hcy[g] = sy / R(M);
+                }
+                continue;
+            }
             const int g = qdiv(u, M, rM), j = u - g * M;
             const int n = ei[I_N * G + g], b0 = g * N;
             const R qix = S.cx[u], qiy = S.cy[u];
@@ -731,16 +778,35 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
                     if (y1 <= qiy) { if (y2 > qiy && il > R(0)) wn += 1; }
                     else { if (y2 <= qiy && il < R(0)) wn -= 1; }
                 }
-                S.herded[u] = wn != 0;
+                if (wn != 0) atomicAdd(&ei[I_HERD * G + g], 1);
             }
             if (j < m_obs && wobs) obs_cattle(obs_wg + g * RW, S.dx, S.dy, b0, j, n, cat_off, qix, qiy);
         }
         lds_signal(fl + F_H);
-        for (int u = ct; u < nf * M; u += CW) {   // cows of flocking envs only
-            const int f = qdiv(u, M, rM), g = flist[f], j = u - f * M;
-            cow_flock(p, S, N, M, e0, g * M + j, g, j, ei[I_N * G + g]);
+        const int T = G * M * N, MN = M * N;
+        const float rMN = 1.0f / (float)MN, rN = 1.0f / (float)N;
+        for (;;) {   // (cow, drone) items of flocking envs: shepherd and predator terms
+            const int b = grab(fl + C_DELTA, 64), q = b + lane;
+            if (b >= nf * MN) break;
+            if (q < nf * MN) {
+                const int f = qdiv(q, MN, rMN), rem = q - f * MN, j = qdiv(rem, N, rN), k = rem - j * N;
+                const int g = flist[f];
+                if (k < ei[I_N * G + g]) delta_term(S, N, M, g * M + j, g, k, T);
+            }
         }
-        if (ct == 0) TS(10, (long long)clock64());
+        if (ct == 0) TS(16, (long long)clock64());
+        cow_sync(fl + F_Q, W1, false);   // every drone term of every cow
+        if (ct == 0) TS(17, (long long)clock64());
+        for (;;) {   // cows of flocking envs only
+            const int b = grab(fl + C_FLOCK, 64), u = b + lane;
+            if (b >= nf * M) break;
+            if (u < nf * M) {
+                const int f = qdiv(u, M, rM), g = flist[f], j = u - f * M;
+                flock_combine(p, S, N, M, e0, g * M + j, ei[I_N * G + g], T);
+            }
+        }
+        if (lane == 0) TS(ct == 0 ? 10 : 28 + (ct >> 6), (long long)clock64());
+        if (ct == 0) TS(31, (long long)nf);
         lds_wait(fl + F_R, 1);    // the reset list
         const int nr = ei[NR_AT];
         if (nr) {   // uniform across the cow waves
@@ -756,7 +822,6 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
                 }
             }
             cow_sync(fl + F_X1, W1, true);   // terminal observation read; flock stores to the cattle state done
-            const float rN = 1.0f / (float)N;
             for (int u = ct; u < nr * N; u += CW) {
                 const int k0 = qdiv(u, N, rN), g = rl[k0], k = u - k0 * N, ud = g * N + k;
                 const int n = reset_draw_n(p, ei[I_EPISODE * G + g], p.env_off + e0 + g);

@@ -49,8 +49,38 @@ def trace(mode, E, n, m, prec, G=None, B=None, steps=4):
         print(f"   drone wave (cycles from start): B0 {rel(3):.0f} chain {rel(4):.0f} terms {rel(5):.0f} "
               f"H {rel(6):.0f} resets-published {rel(15):.0f} book {rel(7):.0f} | cow waves: alpha {rel(8):.0f} D {rel(9):.0f} flock {rel(10):.0f} "
               f"copy {rel(11):.0f} | B1 {rel(13):.0f} end {rel(14):.0f}")
-        print(f"   cow waves: integrate {rel(16):.0f} E {rel(17):.0f} pairs {rel(18):.0f} zero {rel(19):.0f} "
-              f"A {rel(20):.0f} rows {rel(21):.0f} spawn {rel(8):.0f}")
+        nfv = t[:, 31]
+        for sel, name in ((nfv >= 0, "all"), (nfv <= 2, "nf<=2"), (nfv >= 7, "nf>=7")):
+            if not sel.any():
+                continue
+            r2 = lambda k: (t[sel, k] - t[sel, 2]).mean()  # noqa: E731
+            print(f"   cow waves [{name}, {int(sel.sum())} WGs]: pairs {r2(18):.0f} A {r2(20):.0f} rows+sync {r2(21):.0f} "
+                  f"D {r2(9):.0f} H(drone) {r2(6):.0f} delta {r2(16):.0f} Q {r2(17):.0f} flock {r2(10):.0f} "
+                  f"| drone book {r2(7):.0f} B1 {r2(13):.0f} end {r2(14):.0f}")
+        print(f"   drone wave after H: dtaskB {rel(26):.0f} pre-fence {rel(27):.0f} published {rel(15):.0f} "
+              f"metrics stored {rel(28):.0f} book {rel(7):.0f}")
+        simd = (t[:, 22:26] >> 4) & 3
+        same = 0
+        pairs = 0
+        for cu in np.unique(t[:, 12]):
+            ks = np.nonzero(t[:, 12] == cu)[0]
+            for a in range(len(ks)):
+                for c in range(a + 1, len(ks)):
+                    pairs += 1
+                    same += int(simd[ks[a], 0] == simd[ks[c], 0])
+        from collections import Counter
+        pat = Counter()
+        for cu in np.unique(t[:, 12]):
+            ks = np.nonzero(t[:, 12] == cu)[0]
+            if len(ks) == 2:
+                a, b2 = ks
+                pat[(tuple(simd[a].tolist()), tuple(simd[b2].tolist()))] += 1
+        print("   co-resident wave->SIMD patterns (first WG, second WG):", pat.most_common(6))
+        split = sum(1 for cu in np.unique(t[:, 12]) for ks in [np.nonzero(t[:, 12] == cu)[0]]
+                    if len(ks) == 2 and ks[0] < len(t) // 2 <= ks[1])
+        print(f"   CUs whose first WG is in the lower half of the grid and second in the upper: {split}")
+        print(f"   SIMD of wave 0: counts {np.bincount(simd[:, 0], minlength=4).tolist()} | wave order sample "
+              f"{simd[:3].tolist()} | co-resident WG pairs {pairs}, drone waves on the same SIMD {same}")
         tail = (t[:, 14] - t[:, 13]).astype(np.float64)
         chain = (t[:, 4] - t[:, 3]).astype(np.float64)
         res = tail > 3000
@@ -59,6 +89,11 @@ def trace(mode, E, n, m, prec, G=None, B=None, steps=4):
               f"{cyc[~res].mean():.0f} | chain q50/q90/max {np.percentile(chain, 50):.0f}/{np.percentile(chain, 90):.0f}/"
               f"{chain.max():.0f}")
         slow = np.argsort(cyc)[-5:]
+        nfv = t[:, 31]
+        print(f"   flocking envs per WG: mean {nfv.mean():.2f} | slow WGs' nf {nfv[slow].tolist()} | cycles by nf: " +
+              " ".join(f"{v}:{cyc[nfv == v].mean():.0f}" for v in np.unique(nfv)))
+        for k in slow:
+            print(f"     slow WG {k}: flock end per cow wave {t[k, 10] - t[k, 2]} {t[k, 29] - t[k, 2]} {t[k, 30] - t[k, 2]}")
         for k in slow:
             print(f"     slow WG {k}: cyc {cyc[k]:.0f} chain {chain[k]:.0f} tail {tail[k]:.0f} B0 {t[k, 3] - t[k, 2]} "
                   f"terms {t[k, 5] - t[k, 4]} H {t[k, 6] - t[k, 5]} book {t[k, 7] - t[k, 6]} B1 {t[k, 13] - t[k, 7]} "
