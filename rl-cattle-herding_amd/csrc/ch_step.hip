@@ -363,10 +363,14 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
     const int dg = dlane ? tid / N : 0, dk = tid - dg * N;
     const long long di = (long long)e0 * N + tid;
     R pos[3], q[4], v[3], w[3], pid[9];
-    int stepi = 0;
+    int stepi = 0, n0 = 0, act0 = 0;
     if (tid < 64) {
+        // the drone wave loads only what its chain reads, so the chain starts after one round trip; the
+        // cow waves stage the env scalars, the curriculum table and the pair list meanwhile
         __builtin_amdgcn_s_setprio(3);   // the drone wave is the critical path: it wins issue on a shared SIMD
         if (dlane) {
+            n0 = p.envi[0 * E + e0 + dg];
+            if (marl) act0 = p.envi[7 * E + e0 + dg];
             pos[0] = p.drone[0 * DS + di]; pos[1] = p.drone[1 * DS + di]; pos[2] = p.drone[2 * DS + di];
 #pragma unroll
             for (int c = 0; c < 4; ++c) q[c] = p.drone[(3 + c) * DS + di];
@@ -376,29 +380,6 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
             for (int c = 0; c < 9; ++c) pid[c] = p.drone[(13 + c) * DS + di];
             stepi = p.envi[9 * E + e0 + dg];   // ch_step calls on this env so far: the Philox action counter
         }
-        for (int k = tid; k < (int)(sizeof(kLevels) / 4); k += 64)
-            reinterpret_cast<uint32_t*>(S.LT)[k] = reinterpret_cast<const uint32_t*>(kLevels)[k];
-        for (int k = tid; k < P; k += 64) const_cast<uint16_t*>(S.pl)[k] = p.pairs[k];
-        const int g = tid;
-        bool flk = false;
-        if (g < Gv) {
-            const int e = e0 + g;
-            const int scA = p.envi[2 * E + e] + 1;
-            flk = (scA % 2) == 0 && !(p.phase_mask & 2);
-            ei[I_N * G + g] = p.envi[0 * E + e]; ei[I_SC * G + g] = p.envi[1 * E + e]; ei[I_SCA * G + g] = scA;
-            ei[I_HASPREV * G + g] = p.envi[3 * E + e]; ei[I_LEVEL * G + g] = p.envi[4 * E + e];
-            ei[I_TALLY * G + g] = p.envi[5 * E + e]; ei[I_SPAWN * G + g] = p.envi[6 * E + e];
-            ei[I_ACTIVE * G + g] = p.envi[7 * E + e]; ei[I_EPISODE * G + g] = p.envi[8 * E + e];
-            ei[I_FLOCK * G + g] = flk; ei[I_RESET * G + g] = 0; ei[I_HERD * G + g] = 0;
-            S.prev[g] = p.envr[e]; S.clock[g] = p.envr[E + e];
-#pragma unroll
-            for (int r = 0; r < kMetricRows; ++r) S.met[r * G + g] = p.metrics[r * E + e];
-        }
-        // compact list of flocking envs (BaseAviary.py:454: every second step_counter_A)
-        const unsigned long long bal = __ballot(flk);
-        if (flk) ei[FL_LIST + __popcll(bal & ((1ull << tid) - 1ull))] = g;
-        if (tid == 0) { ei[NF_AT] = __popcll(bal); ei[NR_AT] = 0; }
-        lds_signal(fl + F_E);
     } else {
         const float rM0 = 1.0f / (float)M;
         for (int u = ct; u < Gv * M; u += CW) {
@@ -416,7 +397,31 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
             const double* tab = p.spawn + ((long long)sp * p.n_cows + j) * 2;
             S.spx[u] = R(tab[0]); S.spy[u] = R(tab[1]);
         }
-        lds_wait(fl + F_E, 1);   // env scalars and the flocking list from the drone wave
+        for (int k = ct; k < (int)(sizeof(kLevels) / 4); k += CW)
+            reinterpret_cast<uint32_t*>(S.LT)[k] = reinterpret_cast<const uint32_t*>(kLevels)[k];
+        for (int k = ct; k < P; k += CW) const_cast<uint16_t*>(S.pl)[k] = p.pairs[k];
+        if (ct < 64) {   // the first cow wave: env scalars, one env per lane
+        const int g = ct;
+        bool flk = false;
+        if (g < Gv) {
+            const int e = e0 + g;
+            const int scA = p.envi[2 * E + e] + 1;
+            flk = (scA % 2) == 0 && !(p.phase_mask & 2);
+            ei[I_N * G + g] = p.envi[0 * E + e]; ei[I_SC * G + g] = p.envi[1 * E + e]; ei[I_SCA * G + g] = scA;
+            ei[I_HASPREV * G + g] = p.envi[3 * E + e]; ei[I_LEVEL * G + g] = p.envi[4 * E + e];
+            ei[I_TALLY * G + g] = p.envi[5 * E + e]; ei[I_SPAWN * G + g] = p.envi[6 * E + e];
+            ei[I_ACTIVE * G + g] = p.envi[7 * E + e]; ei[I_EPISODE * G + g] = p.envi[8 * E + e];
+            ei[I_FLOCK * G + g] = flk; ei[I_RESET * G + g] = 0; ei[I_HERD * G + g] = 0;
+            S.prev[g] = p.envr[e]; S.clock[g] = p.envr[E + e];
+#pragma unroll
+            for (int r = 0; r < kMetricRows; ++r) S.met[r * G + g] = p.metrics[r * E + e];
+        }
+        // compact list of flocking envs (BaseAviary.py:454: every second step_counter_A)
+        const unsigned long long bal = __ballot(flk);
+        if (flk) ei[FL_LIST + __popcll(bal & ((1ull << ct) - 1ull))] = g;
+        if (ct == 0) { ei[NF_AT] = __popcll(bal); ei[NR_AT] = 0; }
+        }
+        cow_sync(fl + F_E, W1, false);   // env scalars, flocking list, tables: seen by every cow wave
     }
     if (tid == 0) TS(3, (long long)clock64());
 
@@ -428,8 +433,7 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
 
     if (tid < 64) {
         // ============ drone wave: the critical path ============================================
-        wave_sync();   // this wave's env scalars
-        const int n = dlane ? ei[I_N * G + dg] : 0;
+        const int n = dlane ? n0 : 0;
         const bool live = dlane && dk < n;
         R rpy_out[3] = {0, 0, 0};
         if (live) {
@@ -445,7 +449,7 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
                 float4 a4 = reinterpret_cast<const float4*>(p.actions)[di];
                 a[0] = a4.x; a[1] = a4.y; a[2] = a4.z; a[3] = a4.w;
             }
-            if (marl && !((ei[I_ACTIVE * G + dg] >> dk) & 1)) { a[0] = a[1] = a[2] = a[3] = 0.0f; }  // marl_wrapper.py:80-84
+            if (marl && !((act0 >> dk) & 1)) { a[0] = a[1] = a[2] = a[3] = 0.0f; }  // marl_wrapper.py:80-84
             R Rm[9], rpy[3];
             quat_to_mat(q, Rm);
             quat_to_euler(q, rpy);
@@ -471,6 +475,7 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
         wave_sync();
         lds_signal(fl + F_D);
         if (tid == 0) TS(4, (long long)clock64());
+        lds_wait(fl + F_E, W1);   // env scalars and the curriculum table (staged by the cow waves)
 
         // per-drone reward terms (CattleAviary.py:230-246, 572-679) and neighbour obs (BaseRLAviary.py:303-317)
         if (live && task) {
