@@ -490,6 +490,7 @@ int ch__set_tstamp(ch_handle* h, long long* dev) {
 /* Internal diagnostics: override the v2 geometry (envs per workgroup, block size) for sweeps. */
 int ch__set_geometry(ch_handle* h, int32_t G, int32_t block) {
     if (!h || G < 1 || G > 64 || G * h->NC > 64 || block < 128 || block > 256 || block % 64) return CH_ERR_INVALID;
+    if (G * h->M > 3 * (block - 64)) return CH_ERR_UNSUPPORTED;   // the cow waves prefetch <= 3 spawn slots per lane
     const size_t lds = V2Layout(G, h->NC, h->M, h->P, h->cfg.mode, (int)h->rsize).bytes();
     if (lds > 150 * 1024) return CH_ERR_UNSUPPORTED;
     h->G = G; h->block = block; h->lds = lds;

@@ -49,6 +49,11 @@ template <class R> CH_MATH_ATTR R m_exp(R x) { return exp(x); }
 template <class R> CH_MATH_ATTR R m_cos(R x) { return cos(x); }
 template <class R> CH_MATH_ATTR R m_sin(R x) { return sin(x); }
 template <class R> CH_MATH_ATTR R m_pow(R x, R y) { return pow(x, y); }
+// sin and cos of one argument share the range reduction
+template <class R> CH_MATH_ATTR void m_sincos(R x, R* s, R* c) {
+    if constexpr (sizeof(R) == 8) sincos(x, s, c);
+    else sincosf(x, s, c);
+}
 
 // d ** 3 of the predator term (flockUtils.py:343-348, np.power -> libm pow): the cube in double-word
 // arithmetic rounded once, i.e. correctly rounded like pow (<= 0.52 ulp) up to double-rounding ties,
@@ -125,7 +130,9 @@ __device__ __forceinline__ void pid_vel(const R pos[3], const R q[4], const R ve
     R thrust = (sqrt(scalar / (R(4) * R(kKF))) - R(kPwmConst)) / R(kPwmScale);
     R tn = sqrt(T[0] * T[0] + T[1] * T[1] + T[2] * T[2]);
     R z[3] = {T[0] / tn, T[1] / tn, T[2] / tn};
-    R xc[3] = {m_cos(yaw), m_sin(yaw), R(0)};
+    R sy, cy;
+    m_sincos(yaw, &sy, &cy);
+    R xc[3] = {cy, sy, R(0)};
     R yt[3] = {z[1] * xc[2] - z[2] * xc[1], z[2] * xc[0] - z[0] * xc[2], z[0] * xc[1] - z[1] * xc[0]};
     R yn = sqrt(yt[0] * yt[0] + yt[1] * yt[1] + yt[2] * yt[2]);
     R y[3] = {yt[0] / yn, yt[1] / yn, yt[2] / yn};
@@ -230,10 +237,13 @@ __device__ __forceinline__ void drone_substep(R p[3], R q[4], R v[3], R w[3], co
     // btMultiBody::stepPositionsMultiDof exponential-map quaternion update (base body)
     R fang = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
     if (fang * dt > R(0.5 * (0.5 * kPi))) fang = R(0.5 * (0.5 * kPi)) / dt;
+    // sin(0.5 fang dt) and cos(fang dt 0.5): the same double (a factor 0.5 commutes with rounding)
+    R sh, ch;
+    m_sincos(R(0.5) * fang * dt, &sh, &ch);
     R s;
     if (fang < R(0.001)) s = R(0.5) * dt - (dt * dt * dt) * R(0.020833333333) * fang * fang;
-    else s = m_sin(R(0.5) * fang * dt) / fang;
-    R a[4] = {w[0] * s, w[1] * s, w[2] * s, m_cos(fang * dt * R(0.5))};
+    else s = sh / fang;
+    R a[4] = {w[0] * s, w[1] * s, w[2] * s, ch};
     R o[4] = {a[3] * q[0] + a[0] * q[3] + a[1] * q[2] - a[2] * q[1],
               a[3] * q[1] + a[1] * q[3] + a[2] * q[0] - a[0] * q[2],
               a[3] * q[2] + a[2] * q[3] + a[0] * q[1] - a[1] * q[0],

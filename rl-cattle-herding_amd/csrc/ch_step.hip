@@ -75,6 +75,9 @@ __device__ __forceinline__ void lds_signal(int* f) {
     if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(f, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 // spin until *f >= target (bounded: a broken hand-off ends the kernel with wrong data, never a hang)
+__device__ __forceinline__ int lds_peek(int* f) {
+    return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 __device__ __forceinline__ void lds_wait(int* f, int target) {
     int spins = 0;
     while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target && ++spins < (1 << 22))
@@ -82,8 +85,6 @@ __device__ __forceinline__ void lds_wait(int* f, int target) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// barrier among the cow waves only (the drone wave keeps running); `global` also publishes their
-// global stores (needed before other cow lanes rewrite the same state)
 // Dynamic share-out of a cow-wave loop: each call hands the calling wave the next n items of the
 // counter.  The cow waves do not run at equal speed (one of them shares its SIMD with the other
 // resident workgroup's prioritised drone wave), so a static lane -> item split leaves the slowest
@@ -94,6 +95,8 @@ __device__ __forceinline__ int grab(int* ctr, int n) {
     return __builtin_amdgcn_readfirstlane(b);
 }
 
+// barrier among the cow waves only (the drone wave keeps running); `global` also publishes their
+// global stores (needed before other cow lanes rewrite the same state)
 __device__ __forceinline__ void cow_sync(int* f, int waves, bool global) {
     if (global) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     lds_signal(f);
@@ -105,7 +108,10 @@ __device__ __forceinline__ void cow_sync(int* f, int waves, bool global) {
 // 3 after the first barrier, 4 drone chain done, 5 reward terms done, 6 herded flags received,
 // 7 bookkeeping done, 8 cow waves: alpha rows done, 9 drone positions received, 10 velocity update
 // done, 11 obs copy done, 12 CU id, 13 second barrier, 14 end)
-#define TS(slot, val) do { if (p.tstamp) p.tstamp[(long long)blockIdx.x * 32 + (slot)] = (val); } while (0)
+#define TS(slot, val) do { if (p.tstamp) p.tstamp[(long long)blockIdx.x * 64 + (slot)] = (val); } while (0)
+// diagnostics: per cow wave, chunks taken and cycles spent in each dynamic loop (slots 32 + 10 (w - 1) + 2 loop)
+#define CHUNK_T0 const long long ck0_ = p.tstamp ? (long long)clock64() : 0
+#define CHUNK_T1(loop) do { if (p.tstamp && (threadIdx.x & 63) == 0) { long long* q_ = p.tstamp + (long long)blockIdx.x * 64 + 32 + 10 * ((threadIdx.x >> 6) - 1) + 2 * (loop); q_[0] += 1; q_[1] += (long long)clock64() - ck0_; } } while (0)
 
 template <class R>
 struct V2Smem {
@@ -243,8 +249,10 @@ __device__ __forceinline__ void alpha_pairs(const StepParams<R>& p, V2Smem<R>& S
     for (;;) {   // 128 pairs per grab, two independent pairs per lane (instruction-level parallelism)
         const int b = grab(S.flags + C_PAIRS, 128);
         if (b >= tot) break;
+        CHUNK_T0;
         if (b + lane < tot) one(b + lane);
         if (b + 64 + lane < tot) one(b + 64 + lane);
+        CHUNK_T1(0);
     }
 }
 
@@ -259,8 +267,9 @@ __device__ __forceinline__ void alpha_row(V2Smem<R>& S, int M, int P, int u, int
         if (k == j) continue;
         const bool fwd = j < k;
         const int idx = pb + (fwd ? tri(j, k, M) : tri(k, j, M));
-        if (!S.pflag[idx]) continue;
-        ++nb;
+        // out-of-range pairs hold +0 terms and adding (+/-)0 to a sum that starts at +0 changes
+        // nothing, so every entry is summed without waiting on its flag (no load -> branch chain)
+        nb += S.pflag[idx];
         const R tgx = S.tgx[idx], tgy = S.tgy[idx], tcx = S.tcx[idx], tcy = S.tcy[idx];
         gx += fwd ? tgx : -tgx; gy += fwd ? tgy : -tgy;
         cxx += fwd ? tcx : -tcx; cyy += fwd ? tcy : -tcy;
@@ -364,6 +373,7 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
     const long long di = (long long)e0 * N + tid;
     R pos[3], q[4], v[3], w[3], pid[9];
     int stepi = 0, n0 = 0, act0 = 0;
+    R spx_r[3] = {0, 0, 0}, spy_r[3] = {0, 0, 0};   // cow waves: prefetched spawn positions
     if (tid < 64) {
         // the drone wave loads only what its chain reads, so the chain starts after one round trip; the
         // cow waves stage the env scalars, the curriculum table and the pair list meanwhile
@@ -386,16 +396,10 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
             const long long ci = (long long)e0 * M + u;   // the workgroup's cows are contiguous per component
             R x = p.cattle[0 * CS + ci], y = p.cattle[1 * CS + ci];
             const R vx = p.cattle[2 * CS + ci], vy = p.cattle[3 * CS + ci];
-            const int g = qdiv(u, M, rM0), j = u - g * M;
-            int sp = p.envi[6 * E + e0 + g] + 1;   // spawn index of the episode an auto-reset would start
             const R dt = R(p.dt);
             for (int s = 0; s < p.substeps; ++s) { x += vx * dt; y += vy * dt; }   // frictionless cube (trace-pinned)
             CH_ST(&p.cattle[0 * CS + ci], x); CH_ST(&p.cattle[1 * CS + ci], y);
             S.cx[u] = x; S.cy[u] = y; S.cvx[u] = vx; S.cvy[u] = vy;
-            // its cow positions (BaseAviary.py:600-606), fetched now so that a reset needs no global load
-            if (sp >= p.n_scen) sp = 0;
-            const double* tab = p.spawn + ((long long)sp * p.n_cows + j) * 2;
-            S.spx[u] = R(tab[0]); S.spy[u] = R(tab[1]);
         }
         for (int k = ct; k < (int)(sizeof(kLevels) / 4); k += CW)
             reinterpret_cast<uint32_t*>(S.LT)[k] = reinterpret_cast<const uint32_t*>(kLevels)[k];
@@ -422,6 +426,21 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
         if (ct == 0) { ei[NF_AT] = __popcll(bal); ei[NR_AT] = 0; }
         }
         cow_sync(fl + F_E, W1, false);   // env scalars, flocking list, tables: seen by every cow wave
+        if (ct == 0) TS(11, (long long)clock64());
+        // spawn positions of the episode an auto-reset would start: scenario index + 1 (BaseAviary.py:600-606).
+        // Loaded into registers here and parked in LDS after the pair loop, so the load latency hides
+        // behind it and a reset needs no global load.  (Host geometry: G*M <= 3 * cow lanes.)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int u = ct + k * CW;
+            if (u < Gv * M) {
+                const int g = qdiv(u, M, rM0), j = u - g * M;
+                int sp = ei[I_SPAWN * G + g] + 1;
+                if (sp >= p.n_scen) sp = 0;
+                const double* tab = p.spawn + ((long long)sp * p.n_cows + j) * 2;
+                spx_r[k] = R(tab[0]); spy_r[k] = R(tab[1]);
+            }
+        }
     }
     if (tid == 0) TS(3, (long long)clock64());
 
@@ -727,34 +746,43 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
         // ============ cow waves ================================================================
         alpha_pairs(p, S, G, M, P);
         if (ct == 0) TS(18, (long long)clock64());
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int u = ct + k * CW;
+            if (u < Gv * M) { S.spx[u] = spx_r[k]; S.spy[u] = spy_r[k]; }
+        }
         // the constant-zero bytes of the observation blocks, when the host cannot vouch that this buffer
         // already holds them (first step into a buffer, after ch_set_state, ...; ch_api.cpp obs_zero_ptr)
         if (wobs && p.obs_full)
             for (int g = 0; g < Gv; ++g) obs_zero_env(obs_wg + g * RW, ei[I_N * G + g], rows, cat_off, m_obs, ct, CW);
         if (ct == 0) TS(19, (long long)clock64());
         lds_signal(fl + F_A);
-        lds_wait(fl + F_A, W1);
-        if (ct == 0) TS(20, (long long)clock64());
         const float rM = 1.0f / (float)M;
         const int nf = ei[NF_AT];
         const int* flist = ei + FL_LIST;
         const int lane = tid & 63;
-        for (;;) {   // alpha rows of the cows of flocking envs
+        // alpha rows while the drone wave still integrates: once every pair is in the table, row chunks
+        // are taken until the drone positions arrive; the rest follows the drone hand-off below
+        for (int spins = 0; spins < (1 << 22); ++spins) {
+            if (lds_peek(fl + F_D) >= 1) break;
+            if (lds_peek(fl + F_A) < W1) { __builtin_amdgcn_s_sleep(1); continue; }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");   // the pair table
             const int b = grab(fl + C_ROWS, 64), u = b + lane;
             if (b >= nf * M) break;
+            CHUNK_T0;
             if (u < nf * M) {
                 const int f = qdiv(u, M, rM), g = flist[f], j = u - f * M;
                 alpha_row(S, M, P, g * M + j, g, j);
             }
+            CHUNK_T1(2);
         }
-        cow_sync(fl + F_W, W1, false);   // every alpha row read the pair table: its space now takes the drone terms
-        if (ct == 0) TS(21, (long long)clock64());
         if (ct == 0) TS(8, (long long)clock64());
         lds_wait(fl + F_D, 1);
         if (ct == 0) TS(9, (long long)clock64());
         for (;;) {   // per cow: distances, winding number, observation entries; then per env: herd centroid
             const int b = grab(fl + C_COWS, 64), u = b + lane;
             if (b >= Gv * M + Gv) break;
+            CHUNK_T0;
             if (u >= Gv * M) {
                 const int g = u - Gv * M;   // herd centroid (CattleAviary.py: HerdCentroid, np.mean over the cattle)
                 if (g < Gv) {
@@ -762,8 +790,7 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
                     CH_UNROLL for (int j = 0; j < M; ++j) { sx += S.cx[g * M + j]; sy += S.cy[g * M + j]; }
                     S.hcx[g] = sx / R(M); S.hcy[g] = sy / R(M);
                 }
-                continue;
-            }
+            } else {
             const int g = qdiv(u, M, rM), j = u - g * M;
             const int n = ei[I_N * G + g], b0 = g * N;
             const R qix = S.cx[u], qiy = S.cy[u];
@@ -786,18 +813,37 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
                 if (wn != 0) atomicAdd(&ei[I_HERD * G + g], 1);
             }
             if (j < m_obs && wobs) obs_cattle(obs_wg + g * RW, S.dx, S.dy, b0, j, n, cat_off, qix, qiy);
+            }
+            CHUNK_T1(1);
         }
         lds_signal(fl + F_H);
+        // the alpha rows only feed the velocity update: they wait until the drone wave has its hand-off
+        lds_wait(fl + F_A, W1);   // every pair of the table
+        if (ct == 0) TS(20, (long long)clock64());
+        for (;;) {   // alpha rows of the cows of flocking envs
+            const int b = grab(fl + C_ROWS, 64), u = b + lane;
+            if (b >= nf * M) break;
+            CHUNK_T0;
+            if (u < nf * M) {
+                const int f = qdiv(u, M, rM), g = flist[f], j = u - f * M;
+                alpha_row(S, M, P, g * M + j, g, j);
+            }
+            CHUNK_T1(2);
+        }
+        cow_sync(fl + F_W, W1, false);   // every alpha row read the pair table: its space now takes the drone terms
+        if (ct == 0) TS(21, (long long)clock64());
         const int T = G * M * N, MN = M * N;
         const float rMN = 1.0f / (float)MN, rN = 1.0f / (float)N;
         for (;;) {   // (cow, drone) items of flocking envs: shepherd and predator terms
             const int b = grab(fl + C_DELTA, 64), q = b + lane;
             if (b >= nf * MN) break;
+            CHUNK_T0;
             if (q < nf * MN) {
                 const int f = qdiv(q, MN, rMN), rem = q - f * MN, j = qdiv(rem, N, rN), k = rem - j * N;
                 const int g = flist[f];
                 if (k < ei[I_N * G + g]) delta_term(S, N, M, g * M + j, g, k, T);
             }
+            CHUNK_T1(3);
         }
         if (ct == 0) TS(16, (long long)clock64());
         cow_sync(fl + F_Q, W1, false);   // every drone term of every cow
@@ -805,10 +851,12 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
         for (;;) {   // cows of flocking envs only
             const int b = grab(fl + C_FLOCK, 64), u = b + lane;
             if (b >= nf * M) break;
+            CHUNK_T0;
             if (u < nf * M) {
                 const int f = qdiv(u, M, rM), g = flist[f], j = u - f * M;
                 flock_combine(p, S, N, M, e0, g * M + j, ei[I_N * G + g], T);
             }
+            CHUNK_T1(4);
         }
         if (lane == 0) TS(ct == 0 ? 10 : 28 + (ct >> 6), (long long)clock64());
         if (ct == 0) TS(31, (long long)nf);

@@ -23,7 +23,7 @@ def trace(mode, E, n, m, prec, G=None, B=None, steps=4):
     g, blk, lds, kv = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int32()
     L.ch__geometry(b.handle, ctypes.byref(g), ctypes.byref(blk), ctypes.byref(lds), ctypes.byref(kv))
     grid = (E + g.value - 1) // g.value
-    ts = torch.zeros((grid, 32), dtype=torch.int64, device=b.device)
+    ts = torch.zeros((grid, 64), dtype=torch.int64, device=b.device)
     b.reset()
     for _ in range(250):   # steady state: resets have desynchronised the flocking parity
         b.step(random_actions=True, autoreset=True, terminal_obs=False)
@@ -54,7 +54,7 @@ def trace(mode, E, n, m, prec, G=None, B=None, steps=4):
             if not sel.any():
                 continue
             r2 = lambda k: (t[sel, k] - t[sel, 2]).mean()  # noqa: E731
-            print(f"   cow waves [{name}, {int(sel.sum())} WGs]: pairs {r2(18):.0f} A {r2(20):.0f} rows+sync {r2(21):.0f} "
+            print(f"   cow waves [{name}, {int(sel.sum())} WGs]: E {r2(11):.0f} pairs {r2(18):.0f} A {r2(20):.0f} rows+sync {r2(21):.0f} "
                   f"D {r2(9):.0f} H(drone) {r2(6):.0f} delta {r2(16):.0f} Q {r2(17):.0f} flock {r2(10):.0f} "
                   f"| drone book {r2(7):.0f} B1 {r2(13):.0f} end {r2(14):.0f}")
         print(f"   drone wave after H: dtaskB {rel(26):.0f} pre-fence {rel(27):.0f} published {rel(15):.0f} "
@@ -75,6 +75,22 @@ def trace(mode, E, n, m, prec, G=None, B=None, steps=4):
             if len(ks) == 2:
                 a, b2 = ks
                 pat[(tuple(simd[a].tolist()), tuple(simd[b2].tolist()))] += 1
+        # per cow wave: chunks and cycles per loop; the wave that shares its SIMD with the co-resident
+        # workgroup's drone wave: wave 1 in the grid's first half, wave 3 in the second
+        names = ("pairs", "cows", "rows", "delta", "flock")
+        half = len(t) // 2
+        for w in (1, 2, 3):
+            sh = np.array([(w == 1) if k < half else (w == 3) for k in range(len(t))])
+            for lab, sel in (("shared", sh), ("free", ~sh)):
+                if not sel.any():
+                    continue
+                base = 32 + 10 * (w - 1)
+                parts = []
+                for li, nm in enumerate(names):
+                    c = t[sel, base + 2 * li].astype(np.float64)
+                    cy = t[sel, base + 2 * li + 1].astype(np.float64)
+                    parts.append(f"{nm} {c.mean():.2f}x{(cy.sum() / max(c.sum(), 1)):.0f}")
+                print(f"   cow wave {w} [{lab}, {int(sel.sum())}]: " + " | ".join(parts))
         print("   co-resident wave->SIMD patterns (first WG, second WG):", pat.most_common(6))
         split = sum(1 for cu in np.unique(t[:, 12]) for ks in [np.nonzero(t[:, 12] == cu)[0]]
                     if len(ks) == 2 and ks[0] < len(t) // 2 <= ks[1])
@@ -138,7 +154,7 @@ def back_to_back(mode="ctde", E=4096, n=4, m=16, prec="f64", k=12):
     g, blk, lds, kv = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int32()
     L.ch__geometry(b.handle, ctypes.byref(g), ctypes.byref(blk), ctypes.byref(lds), ctypes.byref(kv))
     grid = (E + g.value - 1) // g.value
-    ts = torch.zeros((k, grid, 32), dtype=torch.int64, device=b.device)
+    ts = torch.zeros((k, grid, 64), dtype=torch.int64, device=b.device)
     b.reset()
     for _ in range(250):
         b.step(random_actions=True, autoreset=True, terminal_obs=False)
