@@ -38,7 +38,10 @@ def algorithmic_bytes(mode, n, m, rows, real_bytes):
     cattle = (4 * real_bytes + 2 * real_bytes + real_bytes) * m   # read pos+vel, write pos, vel every 2nd step
     env = 2 * (9 * 4 + 2 * real_bytes)                # env scalars read + write
     metrics = 2 * 7 * 8                               # per-env metric accumulators read + write
-    obs = rows * 86 * 4
+    # observation: the entries a step changes in each live row -- own state (10), two nearest drones
+    # (4), min(m, 16) cattle offsets (2 each); the constant-zero bytes of the [rows][86] block persist
+    # in the caller's buffer and are not rewritten (ch_api.cpp obs_zero_ptr, DESIGN.md "Observations")
+    obs = n * (10 + 4 + 2 * min(m, 16)) * 4
     k = 1 if mode == "ctde" else n
     flags = 4 * k + 2 * k + n + 1                     # reward, terminated, truncated, agent_active, reset flag
     return drone + actions + cattle + env + metrics + obs + flags
@@ -144,15 +147,17 @@ def main():
     dt = time.perf_counter() - t0
     _, dt = D.reduce_rollout([0.0], dt, device=b.device)   # max over ranks
 
-    # live per-launch kernel timing with HIP events on the launch stream (roofline)
+    # live per-launch kernel timing with HIP events on the launch stream (roofline): one event pair
+    # around nk back-to-back launches (an event between every two launches would break the queue's
+    # back-to-back dispatch and add its own packet time to every sample)
     nk = min(200, args.steps)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nk)]
-    for s_ev, e_ev in evs:
-        s_ev.record(stream)
+    s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s_ev.record(stream)
+    for _ in range(nk):
         b.step(random_actions=True, autoreset=True, terminal_obs=False)
-        e_ev.record(stream)
+    e_ev.record(stream)
     torch.cuda.synchronize()
-    kern_us = sum(s.elapsed_time(e) for s, e in evs) / nk * 1000.0
+    kern_us = s_ev.elapsed_time(e_ev) / nk * 1000.0
     rb = 8 if args.precision == "f64" else 4
     bytes_step = algorithmic_bytes(mode, n, m, b.obs_rows, rb)
     achieved = bytes_step * E / (kern_us * 1e-6) / 1e9

@@ -158,8 +158,8 @@ struct V2Smem {
 // (drone wave, after the reward terms), cattle offsets (cow waves, after the distance table), and the
 // always-zero bytes (cow waves, during the alpha phase).  `eb` is the env's block (row 0, col 0); 86 is
 // even, so every float2 below is 8-byte aligned.
-#ifdef CH_NT_STORES
-#define CH_ST(ptr, val) __builtin_nontemporal_store((val), (ptr))
+#ifndef CH_NO_NT_STORES
+#define CH_ST(ptr, val) __builtin_nontemporal_store((val), (ptr))   // streaming: fewer dirty L2 lines at the kernel-end release
 #else
 #define CH_ST(ptr, val) (*(ptr) = (val))
 #endif
