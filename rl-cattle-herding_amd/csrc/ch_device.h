@@ -55,6 +55,23 @@ template <class R> CH_MATH_ATTR void m_sincos(R x, R* s, R* c) {
     else sincosf(x, s, c);
 }
 
+// x / c, correctly rounded, for a divisor whose reciprocal folds to a constant (or is loop-invariant):
+// q = RN(x * RN(1/c)), the residual x - q c exactly by fma, and one fma correction give RN(x / c)
+// (Markstein's correction step; 2.9e8 random operands over this file's divisors and random
+// divisors reproduce IEEE division bit for bit, tools/div_check.c).  A zero or NaN residual means
+// q is already exact (keeps -0) or x was infinite/NaN, and q is returned.  6 instructions instead
+// of the 11-12 of the IEEE division sequence.
+template <class R> __device__ __forceinline__ R divc(R x, R c) {
+    const R rc = R(1) / c;
+    const R q = x * rc;
+    const R r = fma(-q, c, x);
+    const R q2 = fma(r, rc, q);
+    bool keep;
+    if constexpr (sizeof(R) == 8) keep = __builtin_amdgcn_class(r, 1 | 2 | 32 | 64);   // NaN or +-0
+    else keep = __builtin_amdgcn_classf(r, 1 | 2 | 32 | 64);
+    return keep ? q : q2;
+}
+
 // d ** 3 of the predator term (flockUtils.py:343-348, np.power -> libm pow): the cube in double-word
 // arithmetic rounded once, i.e. correctly rounded like pow (<= 0.52 ulp) up to double-rounding ties,
 // in 8 instructions instead of pow's log/exp pair
@@ -127,15 +144,15 @@ __device__ __forceinline__ void pid_vel(const R pos[3], const R q[4], const R ve
     T[2] += R(kG * kMass);
     R scalar = T[0] * Rm[2] + T[1] * Rm[5] + T[2] * Rm[8];
     if (!(scalar > R(0))) scalar = 0;
-    R thrust = (sqrt(scalar / (R(4) * R(kKF))) - R(kPwmConst)) / R(kPwmScale);
+    R thrust = divc(sqrt(divc(scalar, R(4) * R(kKF))) - R(kPwmConst), R(kPwmScale));
     R tn = sqrt(T[0] * T[0] + T[1] * T[1] + T[2] * T[2]);
-    R z[3] = {T[0] / tn, T[1] / tn, T[2] / tn};
+    R z[3] = {divc(T[0], tn), divc(T[1], tn), divc(T[2], tn)};
     R sy, cy;
     m_sincos(yaw, &sy, &cy);
     R xc[3] = {cy, sy, R(0)};
     R yt[3] = {z[1] * xc[2] - z[2] * xc[1], z[2] * xc[0] - z[0] * xc[2], z[0] * xc[1] - z[1] * xc[0]};
     R yn = sqrt(yt[0] * yt[0] + yt[1] * yt[1] + yt[2] * yt[2]);
-    R y[3] = {yt[0] / yn, yt[1] / yn, yt[2] / yn};
+    R y[3] = {divc(yt[0], yn), divc(yt[1], yn), divc(yt[2], yn)};
     R x[3] = {y[1] * z[2] - y[2] * z[1], y[2] * z[0] - y[0] * z[2], y[0] * z[1] - y[1] * z[0]};
     // target rotation columns x, y, z; rot_e from (Rt^T R - R^T Rt)
     const R Rt[9] = {x[0], y[0], z[0], x[1], y[1], z[1], x[2], y[2], z[2]};
@@ -151,7 +168,7 @@ __device__ __forceinline__ void pid_vel(const R pos[3], const R q[4], const R ve
     R rates_e[3], tt[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-        rates_e[i] = R(0.0) - (rpy[i] - pid[i]) / dt;
+        rates_e[i] = R(0.0) - divc(rpy[i] - pid[i], dt);
         pid[i] = rpy[i];
         pid[6 + i] = clip(pid[6 + i] - rot_e[i] * dt, R(-1500.), R(1500.));
     }
@@ -225,11 +242,11 @@ __device__ __forceinline__ void drone_substep(R p[3], R q[4], R v[3], R w[3], co
 #pragma unroll
         for (int i = 0; i < 3; ++i) tb[i] -= g[i];
     }
-    R ab[3] = {tb[0] / J[0], tb[1] / J[1], tb[2] / J[2]};
+    R ab[3] = {divc(tb[0], J[0]), divc(tb[1], J[1]), divc(tb[2], J[2])};
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         R aw = M[i * 3 + 0] * ab[0] + M[i * 3 + 1] * ab[1] + M[i * 3 + 2] * ab[2];
-        v[i] = v[i] + (F[i] / R(kMass)) * dt;
+        v[i] = v[i] + divc(F[i], R(kMass)) * dt;
         w[i] = w[i] + aw * dt;
     }
 #pragma unroll
@@ -250,16 +267,16 @@ __device__ __forceinline__ void drone_substep(R p[3], R q[4], R v[3], R w[3], co
               a[3] * q[3] - a[0] * q[0] - a[1] * q[1] - a[2] * q[2]};
     R n = sqrt(o[0] * o[0] + o[1] * o[1] + o[2] * o[2] + o[3] * o[3]);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) q[i] = o[i] / n;
+    for (int i = 0; i < 4; ++i) q[i] = divc(o[i], n);   // one reciprocal, four corrected quotients
 }
 
 // ---- flocking: MathematicalFlock (flockUtils.py:11-382) ----------------------------------------
 constexpr double kEps = 0.1, kH = 0.2;
-template <class R> __device__ __forceinline__ R sigma_norm_n(R n) { return (sqrt(R(1) + R(kEps) * (n * n)) - R(1)) / R(kEps); }
+template <class R> __device__ __forceinline__ R sigma_norm_n(R n) { return divc(sqrt(R(1) + R(kEps) * (n * n)) - R(1), R(kEps)); }
 template <class R> __device__ __forceinline__ R bump(R z) {
     if (z < R(0)) return R(0);
     if (z < R(kH)) return R(1);
-    if (z <= R(1)) return (R(1) + m_cos(R(kPi) * (z - R(kH)) / (R(1) - R(kH)))) / R(2);
+    if (z <= R(1)) return (R(1) + m_cos(divc(R(kPi) * (z - R(kH)), R(1) - R(kH)))) / R(2);
     return R(0);
 }
 template <class R> __device__ __forceinline__ R sigma_1(R z) { return z / sqrt(R(1) + z * z); }
@@ -272,8 +289,8 @@ __device__ __forceinline__ void pair_terms(R qix, R qiy, R pix, R piy, R qjx, R 
     R zx = qjx - qix, zy = qjy - qiy;
     R n = sqrt(zx * zx + zy * zy);
     R den = sqrt(R(1) + R(kEps) * (n * n));
-    R sn = (den - R(1)) / R(kEps);
-    R b = bump(sn / ra);
+    R sn = divc(den - R(1), R(kEps));
+    R b = bump(divc(sn, ra));
     R zz = sn - da;
     R ph = b * ((R(5.0 + 5.0) * sigma_1(zz + R(0.0)) + R(5.0 - 5.0)) / R(2));
     gx += ph * (zx / den);
@@ -287,8 +304,8 @@ template <class R>
 __device__ __forceinline__ void pair_terms_n(R n, R zx, R zy, R pix, R piy, R pjx, R pjy, R ra, R da, R& gx, R& gy,
                                              R& cx, R& cy) {
     R den = sqrt(R(1) + R(kEps) * (n * n));
-    R sn = (den - R(1)) / R(kEps);
-    R b = bump(sn / ra);
+    R sn = divc(den - R(1), R(kEps));
+    R b = bump(divc(sn, ra));
     R zz = sn - da;
     R ph = b * ((R(5.0 + 5.0) * sigma_1(zz + R(0.0)) + R(5.0 - 5.0)) / R(2));
     gx += ph * (zx / den);
