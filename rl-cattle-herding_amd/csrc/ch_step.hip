@@ -565,17 +565,26 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
             R sdx = 0, sdy = 0;
             const int herded = ei[I_HERD * G + g];   // counted by the cow waves (winding number)
             scx = S.hcx[g]; scy = S.hcy[g];          // herd centroid, summed by the cow waves
-            CH_UNROLL for (int i = 0; i < N; ++i) if (i < n) { sdx += S.dx[b0 + i]; sdy += S.dy[b0 + i]; }
-            sdx /= R(n); sdy /= R(n);
+            // per-drone sums without per-lane branches: a drone beyond NUM_DRONES adds +0, which leaves a sum
+            // that starts at +0 unchanged (x + +0 = x unless x = -0, and such a sum is never -0)
+            CH_UNROLL for (int i = 0; i < N; ++i) {
+                const bool li = i < n;
+                const R xi = S.dx[b0 + i], yi = S.dy[b0 + i];
+                sdx += li ? xi : R(0); sdy += li ? yi : R(0);
+            }
+            sdx = divc(sdx, R(n)); sdy = divc(sdy, R(n));
             R ex = sdx - scx, ey = sdy - scy;
             cent = sqrt(ex * ex + ey * ey + R(0) * R(0));   // HerdCentroid/DroneCentroid, z = 0.95 both
             eff = R((double)herded / M * 100);
             bool anynan = false;
             uint8_t any = 0;
-            CH_UNROLL for (int i = 0; i < N; ++i) if (i < n) {
-                if (S.pa[b0 + i] < ms) ms = S.pa[b0 + i];
-                anynan |= (S.dflags[b0 + i] & 8) != 0;
-                any |= S.dflags[b0 + i];
+            CH_UNROLL for (int i = 0; i < N; ++i) {
+                const bool li = i < n;
+                const R pa = S.pa[b0 + i];
+                const uint8_t df = li ? S.dflags[b0 + i] : 0;
+                if (li && pa < ms) ms = pa;
+                anynan |= (df & 8) != 0;
+                any |= df;
             }
             if (anynan) ms = R(NAN);
             const bool time_up = (double)f_sc / p.ctrl_freq > p.episode_len;
@@ -687,29 +696,37 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
             const int n = f_n;
             if constexpr (!marl) {
                 const Level& Lv = LT[level_r];
+                // branch-free per-drone sums (a skipped term adds +0, see the centroid above)
                 R sp_simple = 0, sp_complex = 0, msp = 0, mcat = 0, cat = 0;
-                CH_UNROLL for (int i = 0; i < N; ++i) if (i < n) {
-                    if (p.compat || S.pa[b0 + i] < R(INFINITY)) { sp_complex += S.ca[b0 + i]; sp_simple += S.sa[b0 + i]; }
-                    if (p.compat || S.pb[b0 + i] < R(INFINITY)) { sp_complex += S.cb[b0 + i]; sp_simple += S.sb[b0 + i]; }
+                R psp_i[NT ? NT : 12], scat_i[NT ? NT : 12];
+                CH_UNROLL for (int i = 0; i < N; ++i) {
+                    const bool li = i < n;
+                    const R pa = S.pa[b0 + i], pb = S.pb[b0 + i];
+                    const bool ua = li && (p.compat || pa < R(INFINITY)), ub = li && (p.compat || pb < R(INFINITY));
+                    sp_complex += ua ? S.ca[b0 + i] : R(0); sp_simple += ua ? S.sa[b0 + i] : R(0);
+                    sp_complex += ub ? S.cb[b0 + i] : R(0); sp_simple += ub ? S.sb[b0 + i] : R(0);
+                    psp_i[i] = S.psp[b0 + i]; scat_i[i] = S.scat[b0 + i];
                 }
-                sp_complex /= R(n * 2.0); sp_simple /= R(n * 2.0);
+                const R n2 = R(n * 2.0), nn = R(n);
+                sp_complex = divc(sp_complex, n2); sp_simple = divc(sp_simple, n2);
                 R approach = 0;
-                if (f_hp) approach = clip(((f_prev - cent) / (max_step + R(1e-6))) * R(5), R(-1.0), R(1.0));
+                if (f_hp) approach = clip(divc(f_prev - cent, max_step + R(1e-6)) * R(5), R(-1.0), R(1.0));
                 f_prev = cent; f_hp = 1;
-                CH_UNROLL for (int i = 0; i < N; ++i) if (i < n) cat += S.scat[b0 + i];
-                cat /= R(n);
+                CH_UNROLL for (int i = 0; i < N; ++i) cat += i < n ? scat_i[i] : R(0);
+                cat = divc(cat, nn);
                 R rg = sp_simple * R(Lv.w_simple) + sp_complex * R(Lv.w_complex) + R(0.1) * R(Lv.w_survival) +
-                       approach * R(Lv.w_approach) + (eff / R(100)) * R(Lv.w_eff) + cat * R(Lv.w_cattle);
-                CH_UNROLL for (int i = 0; i < N; ++i) if (i < n) { msp += S.psp[b0 + i]; mcat += S.scat[b0 + i]; }
-                msp /= R(n); mcat /= R(n);
+                       approach * R(Lv.w_approach) + divc(eff, R(100)) * R(Lv.w_eff) + cat * R(Lv.w_cattle);
+                CH_UNROLL for (int i = 0; i < N; ++i) { msp += i < n ? psp_i[i] : R(0); mcat += i < n ? scat_i[i] : R(0); }
+                msp = divc(msp, nn); mcat = divc(mcat, nn);
                 R tot = 0;
-                CH_UNROLL for (int i = 0; i < N; ++i) if (i < n) tot += rg + R(0.5) * ((S.psp[b0 + i] - msp) + (S.scat[b0 + i] - mcat));
-                R rew = tot / R(n);
+                CH_UNROLL for (int i = 0; i < N; ++i) tot += i < n ? rg + R(0.5) * ((psp_i[i] - msp) + (scat_i[i] - mcat)) : R(0);
+                R rew = divc(tot, nn);
                 p.reward[e] = (float)rew;
                 p.term[e] = te2; p.trunc[e] = tr;
                 ret = (double)rew;
                 n_term = te2; n_trunc = tr; n_nan = rew != rew;
             }
+            if (g == 0) TS(19, (long long)clock64());
             f_sc += marl ? 1 : p.substeps;
             // metric accumulators (rank-local; bench.py all-reduces them)
             const double* mt = S.met;
@@ -755,7 +772,6 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
         // already holds them (first step into a buffer, after ch_set_state, ...; ch_api.cpp obs_zero_ptr)
         if (wobs && p.obs_full)
             for (int g = 0; g < Gv; ++g) obs_zero_env(obs_wg + g * RW, ei[I_N * G + g], rows, cat_off, m_obs, ct, CW);
-        if (ct == 0) TS(19, (long long)clock64());
         lds_signal(fl + F_A);
         const float rM = 1.0f / (float)M;
         const int nf = ei[NF_AT];

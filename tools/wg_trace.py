@@ -58,7 +58,7 @@ def trace(mode, E, n, m, prec, G=None, B=None, steps=4):
                   f"D {r2(9):.0f} H(drone) {r2(6):.0f} delta {r2(16):.0f} Q {r2(17):.0f} flock {r2(10):.0f} "
                   f"| drone book {r2(7):.0f} B1 {r2(13):.0f} end {r2(14):.0f}")
         print(f"   drone wave after H: dtaskB {rel(26):.0f} pre-fence {rel(27):.0f} published {rel(15):.0f} "
-              f"metrics stored {rel(28):.0f} book {rel(7):.0f}")
+              f"reward {rel(19):.0f} metrics stored {rel(28):.0f} book {rel(7):.0f}")
         simd = (t[:, 22:26] >> 4) & 3
         same = 0
         pairs = 0
