@@ -56,6 +56,7 @@ def trace(mode, E, n, m, prec, G=None, B=None, steps=4):
             r2 = lambda k: (t[sel, k] - t[sel, 2]).mean()  # noqa: E731
             print(f"   cow waves [{name}, {int(sel.sum())} WGs]: E {r2(11):.0f} pairs {r2(18):.0f} A {r2(20):.0f} rows+sync {r2(21):.0f} "
                   f"D {r2(9):.0f} H(drone) {r2(6):.0f} delta {r2(16):.0f} Q {r2(17):.0f} flock {r2(10):.0f} "
+                  f"| last cow wave done {(t[sel][:, [10, 29, 30]].max(1) - t[sel, 2]).mean():.0f} "
                   f"| drone book {r2(7):.0f} B1 {r2(13):.0f} end {r2(14):.0f}")
         print(f"   drone wave after H: dtaskB {rel(26):.0f} pre-fence {rel(27):.0f} published {rel(15):.0f} "
               f"reward {rel(19):.0f} metrics stored {rel(28):.0f} book {rel(7):.0f}")
