@@ -28,6 +28,8 @@ WORKLOADS = {
     "c5": ("marl", 4096, 4, 32, "BASELINE configs[4]: 4096 envs x (4 drones, 32 cattle), MARL per-agent obs (4,86)"),
 }
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+MFMA_F32_PEAK_TFLOPS = 157.3   # f32-input MFMA: 64 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz (dense)
+POLICY_GOLDEN = os.path.join(ROOT, "tests", "golden", "policy_ctde_v16_6.npz")
 PROFILES = os.path.join(ROOT, "profiles")
 
 
@@ -70,6 +72,45 @@ def kernel_name(b):
     return "ch::k_env (team per env)"
 
 
+def policy_rollout(b, n, steps, warmup):
+    """Rollout with the reference's trained CTDE actor (model-v16-6, f32 MFMA forward) choosing every
+    action: env-steps/s of forward + step, and the forward alone against the f32 MFMA peak."""
+    import numpy as np
+    import torch
+    from cattleherd.policy import DevicePolicy
+    d = np.load(POLICY_GOLDEN)
+    actor = DevicePolicy.sb3_actor({k.replace("__", "."): torch.tensor(d[k]) for k in d.files if "__" in k})
+    E = b.n_envs
+    stream = torch.cuda.current_stream()
+    b.reset()
+    for _ in range(warmup):
+        b.step_policy(actor)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        b.step_policy(actor)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    nk = min(200, steps)
+    s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    y = torch.empty((E, actor.dims[-1]), dtype=torch.float32, device=b.device)
+    s_ev.record(stream)
+    for _ in range(nk):
+        actor.forward_batch(b, y)
+    e_ev.record(stream)
+    torch.cuda.synchronize()
+    fwd_us = s_ev.elapsed_time(e_ev) / nk * 1000.0
+    # multiplied work: the live input width n*86 of layer 1 (the zero tail is skipped), layers 2-3 in full
+    d0 = actor.dims
+    flops = 2.0 * E * (n * 86 * d0[1] + sum(d0[i] * d0[i + 1] for i in range(1, len(d0) - 1)))
+    tf = flops / (fwd_us * 1e-6) / 1e12
+    return {"env_steps_per_s": E * steps / dt, "ms_per_step": dt / steps * 1000.0,
+            "policy": "SB3 MlpPolicy actor 1032-128-128-48 tanh (model-v16-6), deterministic, f32",
+            "forward_us": fwd_us,
+            "roofline": {"bound": "mfma", "achieved": tf, "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": tf / MFMA_F32_PEAK_TFLOPS, "flops_per_forward": flops}}
+
+
 def cpu_baseline(mode, n, m, seconds=12.0):
     """The CPU oracle (scalar fp64 C port, OpenMP one env per thread) on a bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -98,6 +139,8 @@ def main():
     ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--policy", action="store_true",
+                    help="also time a rollout driven by the on-device SB3 policy (model-v16-6 weights, CTDE only)")
     ap.add_argument("--graph", type=int, default=0,
                     help="steps per captured HIP graph in the timed loop (0 = one host launch per step)")
     args = ap.parse_args()
@@ -183,6 +226,8 @@ def main():
             "rollout_metrics": {"episodes": mv[1], "mean_return": (mv[2] / mv[1]) if mv[1] else None,
                                 "nan_rewards": mv[6], "terminated": mv[4], "truncated": mv[5]},
         }
+        if args.policy and mode == "ctde":
+            out["policy_rollout"] = policy_rollout(b, n, args.steps, args.warmup)
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(mode, n, m, args.cpu_seconds)
         elif world == 1:

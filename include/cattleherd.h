@@ -152,6 +152,36 @@ int ch_builtin_spawn_table(double* out, int32_t* scenarios, int32_t* cows);
  * deterministically for cows > 16 (out: host double[100][max(cows,16)][2]; out may be NULL to query). */
 int ch_spawn_table(int32_t cows, double* out, int32_t* scenarios, int32_t* out_cows);
 
+/* ---- On-device policy ---------------------------------------------------------
+ * A dense MLP evaluated on the matrix cores in f32 (exact f32 products, f32 sums), weights in
+ * device memory in torch nn.Linear layout.  The SB3 actor of the reference's CTDE driver is
+ * dims {1032, 128, 128, 48}, tanh hidden, output clipped to [-1, 1]; its critic {1032, 128, 128, 1};
+ * the RLlib per-agent model {86, 256, 256, 8}. */
+#define CH_ACT_NONE 0
+#define CH_ACT_TANH 1
+#define CH_ACT_RELU 2
+typedef struct ch_mlp {
+    int32_t n_layers;          /* 1..4 */
+    int32_t dims[5];           /* dims[0] inputs; dims[i + 1] outputs of layer i (<= 256) */
+    const float* weight[4];    /* device [dims[i+1]][dims[i]] row-major (nn.Linear.weight) */
+    const float* bias[4];      /* device [dims[i+1]] or NULL */
+    int32_t hidden_act;        /* CH_ACT_* applied after every layer but the last */
+    int32_t clip;              /* non-zero: clip the output to [lo, hi] */
+    float lo, hi;
+} ch_mlp;
+
+/* Replaces: stable_baselines3 ActorCriticPolicy.predict(obs, deterministic=True) for a Box action
+ * space (mlp_extractor.policy_net -> action_net -> np.clip to the space, CTDECattleHerder.py:203,
+ * 106-127) and predict_values (value_net), and the RLlib model forward of DTDECattleHerder.py.
+ * y[rows][dims[L]] = MLP(x[rows][dims[0]]); x and y are device buffers. */
+int ch_mlp_forward(const ch_mlp* net, const float* x, int64_t rows, float* y, void* stream);
+
+/* ch_mlp_forward on a handle's observation buffer: one row per env for CTDE (x = obs [E][R][86]
+ * flattened, dims[0] = R*86) or per agent for MARL (x = obs [E][N][86], dims[0] = 86, E*N rows).
+ * Input features past an env's NUM_DRONES rows (CTDE) or of agents past NUM_DRONES (MARL) are zero
+ * in the observation and are not multiplied. */
+int ch_policy_forward(ch_handle* h, const ch_mlp* net, const float* obs, float* y, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

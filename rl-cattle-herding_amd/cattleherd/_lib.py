@@ -20,7 +20,8 @@ ABI_VERSION = 1
 # every symbol include/cattleherd.h declares
 EXPORTS = ("ch_default_config", "ch_create", "ch_destroy", "ch_last_error", "ch_shape", "ch_reset", "ch_step",
            "ch_state_size", "ch_get_state", "ch_set_state", "ch_metrics", "ch_builtin_spawn_table",
-           "ch_spawn_table")
+           "ch_spawn_table", "ch_mlp_forward", "ch_policy_forward")
+CH_ACT_NONE, CH_ACT_TANH, CH_ACT_RELU = 0, 1, 2
 
 
 class ChConfig(ctypes.Structure):
@@ -38,6 +39,12 @@ class ChStepIO(ctypes.Structure):
                 ("reward", ctypes.c_void_p), ("terminated", ctypes.c_void_p), ("truncated", ctypes.c_void_p),
                 ("terminal_obs", ctypes.c_void_p), ("agent_active", ctypes.c_void_p),
                 ("reset_happened", ctypes.c_void_p), ("flags", ctypes.c_uint32), ("_pad", ctypes.c_uint32)]
+
+
+class ChMlp(ctypes.Structure):
+    _fields_ = [("n_layers", ctypes.c_int32), ("dims", ctypes.c_int32 * 5), ("weight", ctypes.c_void_p * 4),
+                ("bias", ctypes.c_void_p * 4), ("hidden_act", ctypes.c_int32), ("clip", ctypes.c_int32),
+                ("lo", ctypes.c_float), ("hi", ctypes.c_float)]
 
 
 class ChError(RuntimeError):
@@ -74,6 +81,8 @@ def lib():
     L.ch_metrics.argtypes = [vp, vp, i32, vp]
     L.ch_builtin_spawn_table.argtypes = [vp, P(i32), P(i32)]
     L.ch_spawn_table.argtypes = [i32, vp, P(i32), P(i32)]
+    L.ch_mlp_forward.argtypes = [P(ChMlp), vp, i64, vp, vp]
+    L.ch_policy_forward.argtypes = [vp, P(ChMlp), vp, vp, vp]
     for name in EXPORTS:
         if name not in ("ch_last_error",):
             getattr(L, name).restype = ctypes.c_int

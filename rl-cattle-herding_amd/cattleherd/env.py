@@ -130,6 +130,12 @@ class HerdBatch:
             L.check(rc, self.handle)
         return self.obs, self.reward, self.terminated, self.truncated
 
+    def step_policy(self, policy, autoreset=True, terminal_obs=False):
+        """One step with the actions of an on-device policy (cattleherd.policy.DevicePolicy) for the
+        current observations: the SB3 ``model.predict(obs, deterministic=True)`` + ``env.step`` loop
+        of CTDECattleHerder.py:202-204 without leaving the GPU."""
+        return self.step(policy.act(self), autoreset=autoreset, terminal_obs=terminal_obs)
+
     def invalidate_obs(self):
         """The caller modified ``self.obs``: the next step writes every observation block in full."""
         L.check(L.lib().ch__obs_invalidate(self.handle), self.handle)

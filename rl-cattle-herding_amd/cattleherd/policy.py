@@ -1,0 +1,148 @@
+"""On-device policy forward: the reference's trained MLPs on the matrix cores.
+
+The CTDE driver trains ``PPO("MlpPolicy", net_arch=dict(pi=[128, 128], vf=[128, 128]))`` on the
+flattened (12, 86) observation (``simulator/CTDECattleHerder.py:106-127``) and rolls it out with
+``model.predict(obs, deterministic=True)`` (203): actor MLP -> ``action_net`` -> ``np.clip`` to the
+[-1, 1] action box.  ``DevicePolicy`` runs that forward for every env of a ``HerdBatch`` in one HIP
+launch (``csrc/ch_policy.hip``, f32 MFMA), so a rollout never leaves the GPU.
+
+Weights come from an SB3 model zip (``policy.pth`` read with ``torch.load(weights_only=True)``,
+nothing unpickled), from a state dict, or are random-initialised with the same architecture.
+"""
+import ctypes
+import io
+import zipfile
+
+from . import _lib as L
+
+_ACTS = {"none": L.CH_ACT_NONE, "tanh": L.CH_ACT_TANH, "relu": L.CH_ACT_RELU}
+
+
+def load_sb3_state_dict(path):
+    """``policy.pth`` of an SB3 model zip as a tensor dict (weights only; the zip's pickled
+    ``data`` entry is never deserialised)."""
+    import torch
+    with zipfile.ZipFile(path) as z:
+        return torch.load(io.BytesIO(z.read("policy.pth")), weights_only=True, map_location="cpu")
+
+
+class DevicePolicy:
+    """A dense MLP (1-4 layers, widths <= 256) evaluated by ``ch_mlp_forward``.
+
+    ``layers``: list of (weight [out, in], bias [out] or None) tensors in ``nn.Linear`` layout;
+    ``hidden_act`` after every layer but the last; ``clip`` = (lo, hi) or None on the output."""
+
+    def __init__(self, layers, hidden_act="tanh", clip=None, device=None):
+        import torch
+        if not torch.cuda.is_available():
+            raise RuntimeError("DevicePolicy needs a ROCm GPU; there is no CPU fallback")
+        if not 1 <= len(layers) <= 4:
+            raise ValueError("1..4 layers")
+        self.torch = torch
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.weights, self.biases = [], []
+        dims = [int(layers[0][0].shape[1])]
+        for w, b in layers:
+            w = torch.as_tensor(w, dtype=torch.float32).to(self.device).contiguous()
+            if w.shape[1] != dims[-1] or w.shape[0] > 256:
+                raise ValueError(f"layer shape {tuple(w.shape)} does not chain (widths <= 256)")
+            self.weights.append(w)
+            self.biases.append(None if b is None else torch.as_tensor(b, dtype=torch.float32).to(self.device).contiguous())
+            dims.append(int(w.shape[0]))
+        self.dims = dims
+        self.hidden_act = hidden_act
+        self.clip = clip
+        net = L.ChMlp()
+        net.n_layers = len(layers)
+        for i, d in enumerate(dims):
+            net.dims[i] = d
+        for i in range(len(layers)):
+            net.weight[i] = self.weights[i].data_ptr()
+            net.bias[i] = self.biases[i].data_ptr() if self.biases[i] is not None else None
+        net.hidden_act = _ACTS[hidden_act]
+        net.clip = 1 if clip is not None else 0
+        net.lo, net.hi = (clip if clip is not None else (0.0, 0.0))
+        self._net = net
+
+    # ---- constructors for the reference's models ------------------------------------------------
+    @classmethod
+    def sb3_actor(cls, state_dict, device=None):
+        """Deterministic SB3 ActorCriticPolicy action: policy_net (tanh) -> action_net, clipped to [-1, 1]."""
+        sd = state_dict
+        layers = [(sd["mlp_extractor.policy_net.0.weight"], sd["mlp_extractor.policy_net.0.bias"]),
+                  (sd["mlp_extractor.policy_net.2.weight"], sd["mlp_extractor.policy_net.2.bias"]),
+                  (sd["action_net.weight"], sd["action_net.bias"])]
+        return cls(layers, "tanh", (-1.0, 1.0), device)
+
+    @classmethod
+    def sb3_critic(cls, state_dict, device=None):
+        """SB3 ActorCriticPolicy.predict_values: value_net on the tanh value MLP."""
+        sd = state_dict
+        layers = [(sd["mlp_extractor.value_net.0.weight"], sd["mlp_extractor.value_net.0.bias"]),
+                  (sd["mlp_extractor.value_net.2.weight"], sd["mlp_extractor.value_net.2.bias"]),
+                  (sd["value_net.weight"], sd["value_net.bias"])]
+        return cls(layers, "tanh", None, device)
+
+    @staticmethod
+    def random_layers(dims, seed=0):
+        """nn.Linear default initialisation (uniform +-1/sqrt(fan_in)) for the given widths."""
+        import torch
+        g = torch.Generator().manual_seed(seed)
+        out = []
+        for i in range(len(dims) - 1):
+            bound = 1.0 / dims[i] ** 0.5
+            w = (torch.rand(dims[i + 1], dims[i], generator=g) * 2 - 1) * bound
+            b = (torch.rand(dims[i + 1], generator=g) * 2 - 1) * bound
+            out.append((w, b))
+        return out
+
+    # ---- forward ---------------------------------------------------------------------------------
+    def _stream(self):
+        return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+
+    def forward(self, x, out=None):
+        """y[rows, dims[-1]] = MLP(x[rows, dims[0]]) on the device (x float32, contiguous)."""
+        torch = self.torch
+        x = x.to(device=self.device, dtype=torch.float32).contiguous()
+        rows = x.numel() // self.dims[0]
+        if x.numel() != rows * self.dims[0]:
+            raise ValueError(f"input has {x.numel()} floats, not a multiple of {self.dims[0]}")
+        if out is None:
+            out = torch.empty((rows, self.dims[-1]), dtype=torch.float32, device=self.device)
+        L.check(L.lib().ch_mlp_forward(ctypes.byref(self._net), ctypes.c_void_p(x.data_ptr()), rows,
+                                       ctypes.c_void_p(out.data_ptr()), self._stream()))
+        return out
+
+    def forward_batch(self, batch, out=None):
+        """The forward on a HerdBatch's current observations (one row per env for CTDE, per agent for
+        MARL), skipping the input columns past each env's NUM_DRONES."""
+        torch = self.torch
+        rows = batch.n_envs if batch.mode == L.CH_MODE_CTDE else batch.n_envs * batch.num_drones
+        if out is None:
+            out = torch.empty((rows, self.dims[-1]), dtype=torch.float32, device=self.device)
+        L.check(L.lib().ch_policy_forward(batch.handle, ctypes.byref(self._net), ctypes.c_void_p(batch.obs.data_ptr()),
+                                          ctypes.c_void_p(out.data_ptr()), self._stream()), batch.handle)
+        return out
+
+    def act(self, batch, out=None):
+        """Deterministic actions [E, N, 4] for the batch's observations (SB3 predict semantics: the
+        first NUM_DRONES rows of the (12, 4) action; for MARL the first 4 of each agent's outputs)."""
+        y = self.forward_batch(batch, out)
+        n = batch.num_drones
+        if batch.mode == L.CH_MODE_CTDE:
+            return y.view(batch.n_envs, -1, 4)[:, :n, :]
+        return y.view(batch.n_envs, n, -1)[:, :, :4]
+
+    def reference(self, x):
+        """Plain torch float32 forward of the same network (test oracle for the MFMA kernel)."""
+        torch = self.torch
+        h = x.to(device=self.device, dtype=torch.float32).reshape(-1, self.dims[0])
+        for i, (w, b) in enumerate(zip(self.weights, self.biases)):
+            h = h @ w.t()
+            if b is not None:
+                h = h + b
+            if i < len(self.weights) - 1:
+                h = {"tanh": torch.tanh, "relu": torch.relu, "none": lambda t: t}[self.hidden_act](h)
+        if self.clip is not None:
+            h = h.clamp(self.clip[0], self.clip[1])
+        return h

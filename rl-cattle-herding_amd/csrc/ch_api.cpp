@@ -522,6 +522,56 @@ int ch__set_phase_mask(ch_handle* h, int32_t mask) {
     return CH_OK;
 }
 
+static int mlp_args(const ch_mlp* net, const float* x, int64_t rows, float* y, MlpArgs& a, std::string& err) {
+    if (!net || !x || !y) { err = "NULL argument"; return CH_ERR_INVALID; }
+    if (net->n_layers < 1 || net->n_layers > 4) { err = "n_layers must be 1..4"; return CH_ERR_INVALID; }
+    if (rows < 0) { err = "rows < 0"; return CH_ERR_INVALID; }
+    std::memset(&a, 0, sizeof(a));
+    a.layers = net->n_layers;
+    for (int i = 0; i <= net->n_layers; ++i) {
+        a.dims[i] = net->dims[i];
+        if (net->dims[i] < 1 || (i > 0 && net->dims[i] > 256)) { err = "layer widths must be 1..256"; return CH_ERR_UNSUPPORTED; }
+    }
+    for (int i = 0; i < net->n_layers; ++i) {
+        if (!net->weight[i]) { err = "NULL weight"; return CH_ERR_INVALID; }
+        a.w[i] = net->weight[i]; a.b[i] = net->bias[i];
+    }
+    if (net->hidden_act < CH_ACT_NONE || net->hidden_act > CH_ACT_RELU) { err = "unknown activation"; return CH_ERR_INVALID; }
+    a.hidden_act = net->hidden_act; a.clip = net->clip != 0; a.lo = net->lo; a.hi = net->hi;
+    a.x = x; a.rows = rows; a.y = y; a.rows_per_env = 1;
+    return CH_OK;
+}
+
+int ch_mlp_forward(const ch_mlp* net, const float* x, int64_t rows, float* y, void* stream) {
+    MlpArgs a;
+    std::string err;
+    const int rc = mlp_args(net, x, rows, y, a, err);
+    if (rc) return fail(nullptr, rc, "ch_mlp_forward: " + err);
+    const hipError_t e = launch_mlp(a, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(nullptr, CH_ERR_DEVICE, std::string("ch_mlp_forward launch: ") + hipGetErrorString(e));
+    return CH_OK;
+}
+
+int ch_policy_forward(ch_handle* h, const ch_mlp* net, const float* obs, float* y, void* stream) {
+    if (!h) return fail(nullptr, CH_ERR_INVALID, "ch_policy_forward: NULL handle");
+    const bool marl = h->cfg.mode == CH_MODE_MARL;
+    const int64_t rows = marl ? h->E * h->NC : h->E;
+    const int want = marl ? 86 : h->rows * 86;
+    if (net && net->dims[0] != want)
+        return fail(h, CH_ERR_INVALID, "ch_policy_forward: dims[0] must be " + std::to_string(want) + " for this handle");
+    MlpArgs a;
+    std::string err;
+    const int rc = mlp_args(net, obs, rows, y, a, err);
+    if (rc) return fail(h, rc, "ch_policy_forward: " + err);
+    a.env_n = h->envi;   // envi row 0: NUM_DRONES of the episode each env is in
+    a.rows_per_env = marl ? h->NC : 1;
+    a.k_unit = 86;
+    HIP_TRY(h, hipSetDevice(h->device));
+    const hipError_t e = launch_mlp(a, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(h, CH_ERR_DEVICE, std::string("ch_policy_forward launch: ") + hipGetErrorString(e));
+    return CH_OK;
+}
+
 int ch_metrics(ch_handle* h, double* out, int32_t reset_after, void* stream) {
     if (!h || !out) return fail(h, CH_ERR_INVALID, "ch_metrics: NULL argument");
     HIP_TRY(h, hipSetDevice(h->device));

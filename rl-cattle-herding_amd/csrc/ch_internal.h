@@ -87,6 +87,24 @@ struct V2Layout {
     __host__ __device__ size_t bytes() const { return off[NOFF]; }
 };
 
+// on-device policy (ch_policy.hip)
+struct MlpArgs {
+    int layers;
+    int dims[5];
+    const float* w[4];
+    const float* b[4];
+    int hidden_act, clip;
+    float lo, hi;
+    const float* x;
+    long long rows;
+    float* y;
+    const int* env_n;          // optional: NUM_DRONES per env (handle envi row 0) -> live input width
+    long long rows_per_env;    // 1: CTDE (live width n * k_unit); N: MARL (agent j live iff j < n)
+    int k_unit;
+};
+size_t mlp_lds_bytes();
+hipError_t launch_mlp(const MlpArgs& a, hipStream_t st);
+
 template <class R> hipError_t launch_step(const StepParams<R>& p, int team, hipStream_t st);
 template <class R> hipError_t launch_reset(const StepParams<R>& p, int team, hipStream_t st);
 template <class R> hipError_t launch_step_v2(const StepParams<R>& p, int block, size_t lds, hipStream_t st);

@@ -1,0 +1,122 @@
+"""On-device policy forward (csrc/ch_policy.hip) against torch.
+
+Tolerances: the kernel multiplies in f32 on the matrix cores (each output a k-ordered f32 fma
+chain); torch's CPU/GPU GEMMs sum in other orders.  Outputs are compared with an fp64 torch
+forward of the same weights at atol 2e-5 + rtol 2e-5 (f32 rounding over K <= 1032 terms of
+|w x| ~ 1e-2), and with the reference model's own fp32 outputs (golden file) at the same bar.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GOLD = "tests/golden/policy_ctde_v16_6.npz"
+
+
+def _sd(d):
+    import torch
+    return {k.replace("__", "."): torch.tensor(d[k]) for k in d.files if "__" in k}
+
+
+def _ref64(pol, x):
+    import torch
+    h = x.double().cpu().reshape(-1, pol.dims[0])
+    for i, (w, b) in enumerate(zip(pol.weights, pol.biases)):
+        h = h @ w.double().cpu().t()
+        if b is not None:
+            h = h + b.double().cpu()
+        if i < len(pol.weights) - 1:
+            h = torch.tanh(h) if pol.hidden_act == "tanh" else (torch.relu(h) if pol.hidden_act == "relu" else h)
+    if pol.clip is not None:
+        h = h.clamp(*pol.clip)
+    return h
+
+
+def _close(a, b, tol=2e-5):
+    a = a.double().cpu()
+    b = b.double().cpu()
+    err = ((a - b).abs() - tol * b.abs()).max().item()
+    return err <= tol, err
+
+
+def test_sb3_actor_and_critic_match_reference_model():
+    """model-v16-6 (the reference's trained CTDE PPO policy): deterministic actions and values."""
+    import os
+    import torch
+    from cattleherd.policy import DevicePolicy
+    d = np.load(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), GOLD))
+    sd = _sd(d)
+    actor, critic = DevicePolicy.sb3_actor(sd), DevicePolicy.sb3_critic(sd)
+    x = torch.tensor(d["obs"]).reshape(len(d["obs"]), -1)
+    a = actor.forward(x)
+    v = critic.forward(x)
+    torch.cuda.synchronize()
+    ok, err = _close(a, torch.tensor(d["actions"]))
+    assert ok, err
+    ok, err = _close(v[:, 0], torch.tensor(d["values"]))
+    assert ok, err
+    assert (a.abs() <= 1).all()
+
+
+@pytest.mark.parametrize("dims,act,rows", [((1032, 128, 128, 48), "tanh", 4096), ((86, 256, 256, 8), "tanh", 4095),
+                                           ((50, 16, 3), "relu", 17), ((1032, 128, 128, 1), "tanh", 1),
+                                           ((7, 200, 33, 250, 5), "none", 100)])
+def test_mlp_forward_vs_fp64(dims, act, rows):
+    import torch
+    from cattleherd.policy import DevicePolicy
+    pol = DevicePolicy(DevicePolicy.random_layers(dims, seed=len(dims) + rows), act,
+                       (-1.0, 1.0) if dims[-1] == 48 else None)
+    g = torch.Generator().manual_seed(rows)
+    x = torch.randn(rows, dims[0], generator=g)
+    y = pol.forward(x)
+    torch.cuda.synchronize()
+    assert y.shape == (rows, dims[-1])
+    ok, err = _close(y, _ref64(pol, x))
+    assert ok, err
+
+
+@pytest.mark.parametrize("mode,n,m", [("ctde", 4, 16), ("marl", 4, 16), ("ctde", 6, 8)])
+def test_policy_forward_on_batch_skips_dead_rows_exactly(mode, n, m):
+    """ch_policy_forward multiplies only the live part of each observation; the result equals the
+    full-width forward of the same buffer (the skipped products are 0 * w)."""
+    import torch
+    from cattleherd.env import HerdBatch
+    from cattleherd.policy import DevicePolicy
+    b = HerdBatch(1000, n, m, mode=mode, min_drones=2, max_drones=n)
+    dims = (12 * 86, 128, 128, 48) if mode == "ctde" else (86, 256, 256, 8)
+    pol = DevicePolicy(DevicePolicy.random_layers(dims, seed=3), "tanh", (-1.0, 1.0))
+    b.reset()
+    for t in range(30):
+        a = pol.act(b)
+        full = pol.forward(b.obs)
+        part = pol.forward_batch(b)
+        torch.cuda.synchronize()
+        assert torch.equal(part + 0.0, full + 0.0), t
+        assert a.shape == (1000, n, 4)
+        b.step(a, autoreset=True)
+    torch.cuda.synchronize()
+    ok, err = _close(pol.forward_batch(b), _ref64(pol, b.obs))
+    assert ok, err
+    b.close()
+
+
+def test_policy_rollout_matches_host_policy_loop():
+    """A device-policy rollout equals stepping the same batch with actions from the torch forward of
+    each step's observation (to the forward's tolerance; actions are compared, the env runs on)."""
+    import os
+    import torch
+    from cattleherd.env import HerdBatch
+    from cattleherd.policy import DevicePolicy
+    d = np.load(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), GOLD))
+    actor = DevicePolicy.sb3_actor(_sd(d))
+    b = HerdBatch(512, 4, 16)
+    b.reset()
+    worst = 0.0
+    for t in range(60):
+        a = actor.act(b).contiguous()
+        ref = actor.reference(b.obs).view(512, 12, 4)[:, :4]
+        torch.cuda.synchronize()
+        worst = max(worst, (a - ref).abs().max().item())
+        b.step(a, autoreset=True)
+    assert worst < 5e-5, worst
+    b.close()
