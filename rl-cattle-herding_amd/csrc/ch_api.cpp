@@ -27,6 +27,11 @@ struct ch_handle {
     double episode_len = 0;
     size_t rsize = 8;
     void* drone = nullptr;
+    // Euler angles of each drone's stored quaternion, written by the v2 step at the end of every
+    // step (it needs them for the observation anyway) and read by the next one instead of
+    // recomputing atan2/asin/atan2; any other writer of the state clears rpy_valid.
+    void* rpy = nullptr;
+    bool rpy_valid = false;
     void* cattle = nullptr;
     void* envr = nullptr;
     int* envi = nullptr;
@@ -137,7 +142,7 @@ static StepParams<R> params(ch_handle* h) {
     p.k0 = (uint32_t)c.seed; p.k1 = (uint32_t)(c.seed >> 32);
     p.env_off = c.env_id_offset;
     p.cs_cc = cattle_spacing_cc();
-    p.drone = (R*)h->drone; p.cattle = (R*)h->cattle; p.envr = (R*)h->envr; p.envi = h->envi;
+    p.drone = (R*)h->drone; p.rpy = (R*)h->rpy; p.rpy_valid = h->rpy_valid; p.cattle = (R*)h->cattle; p.envr = (R*)h->envr; p.envi = h->envi;
     p.metrics = h->metrics; p.spawn = h->spawn; p.n_scen = h->n_scen; p.n_cows = h->n_cows;
     p.debug = h->debug;
     p.phase_mask = h->phase_mask;
@@ -191,7 +196,7 @@ int ch_default_config(ch_config* c, int32_t mode, int32_t num_drones, int32_t nu
 const char* ch_last_error(const ch_handle* h) { return h ? h->err.c_str() : g_create_err.c_str(); }
 
 static void free_all(ch_handle* h) {
-    void* ptrs[] = {h->drone, h->cattle, h->envr, h->envi, h->metrics, h->spawn, h->pairs};
+    void* ptrs[] = {h->drone, h->rpy, h->cattle, h->envr, h->envi, h->metrics, h->spawn, h->pairs};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
 }
@@ -262,6 +267,7 @@ int ch_create(const ch_config* c, int64_t n_envs, int32_t device, ch_handle** ou
     CTRY(hipSetDevice(device));
     const int64_t E = h->E;
     CTRY(hipMalloc(&h->drone, h->rsize * kDroneComps * E * h->NC));
+    CTRY(hipMalloc(&h->rpy, h->rsize * 3 * E * h->NC));
     CTRY(hipMalloc(&h->cattle, h->rsize * kCattleComps * E * h->M));
     CTRY(hipMalloc(&h->envr, h->rsize * kEnvReal * E));
     CTRY(hipMalloc(&h->envi, sizeof(int) * kEnvInt * E));
@@ -370,6 +376,7 @@ int ch_reset(ch_handle* h, const uint8_t* mask_dev, float* obs_dev, void* stream
         e = launch_reset(p, h->team, st);
     }
     if (e != hipSuccess) return fail(h, CH_ERR_DEVICE, std::string("ch_reset launch: ") + hipGetErrorString(e));
+    h->rpy_valid = false;                                        // reset bodies: angles recomputed next step
     if (!mask_dev) h->obs_zero_ptr = obs_dev;                    // every block written in full
     else if (h->obs_zero_ptr != obs_dev) h->obs_zero_ptr = nullptr;   // some blocks of obs_dev unknown
     return CH_OK;
@@ -407,6 +414,7 @@ int ch_step(ch_handle* h, const ch_step_io* io, void* stream) {
     }
     if (e != hipSuccess) return fail(h, CH_ERR_DEVICE, std::string("ch_step launch: ") + hipGetErrorString(e));
     h->obs_zero_ptr = (h->phase_mask & 8) ? nullptr : io->obs;
+    h->rpy_valid = h->kernel == 2 && !(h->phase_mask & 1);   // v2 stored the angles of every live drone
     return CH_OK;
 }
 
@@ -447,6 +455,7 @@ int ch_set_state(ch_handle* h, const double* hd, const int32_t* hi, void* stream
     hipStream_t st = (hipStream_t)stream;
     HIP_TRY(h, hipStreamSynchronize(st));
     h->obs_zero_ptr = nullptr;   // NUM_DRONES may change: the next step writes every obs block in full
+    h->rpy_valid = false;
     const size_t nd = (size_t)kDroneComps * h->E * h->NC, nc = (size_t)kCattleComps * h->E * h->M,
                  nr = (size_t)kEnvReal * h->E;
     if (hd) {

@@ -26,6 +26,8 @@ struct StepParams {
     long long env_off;
     double cs_cc;   // CattleSpacingRewardFunction continuation constant (host-evaluated)
     R* drone;       // [22][E][NC]
+    R* rpy;         // v2: [3][E][NC] Euler angles of the stored quaternion (valid iff rpy_valid)
+    int rpy_valid;
     R* cattle;      // [4][E][M]
     R* envr;        // [2][E]
     int* envi;      // [10][E]

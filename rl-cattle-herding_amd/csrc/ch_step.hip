@@ -371,7 +371,7 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
     const bool dlane = tid < nd;
     const int dg = dlane ? tid / N : 0, dk = tid - dg * N;
     const long long di = (long long)e0 * N + tid;
-    R pos[3], q[4], v[3], w[3], pid[9];
+    R pos[3], q[4], v[3], w[3], pid[9], rpy_in[3] = {0, 0, 0};
     int stepi = 0, n0 = 0, act0 = 0;
     R spx_r[3] = {0, 0, 0}, spy_r[3] = {0, 0, 0};   // cow waves: prefetched spawn positions
     if (tid < 64) {
@@ -388,6 +388,10 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
             for (int c = 0; c < 3; ++c) { v[c] = p.drone[(7 + c) * DS + di]; w[c] = p.drone[(10 + c) * DS + di]; }
 #pragma unroll
             for (int c = 0; c < 9; ++c) pid[c] = p.drone[(13 + c) * DS + di];
+            if (p.rpy_valid) {   // Euler angles of this quaternion, stored by the previous step
+#pragma unroll
+                for (int c = 0; c < 3; ++c) rpy_in[c] = p.rpy[c * DS + di];
+            }
             stepi = p.envi[9 * E + e0 + dg];   // ch_step calls on this env so far: the Philox action counter
         }
     } else {
@@ -471,7 +475,8 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
             if (marl && !((act0 >> dk) & 1)) { a[0] = a[1] = a[2] = a[3] = 0.0f; }  // marl_wrapper.py:80-84
             R Rm[9], rpy[3];
             quat_to_mat(q, Rm);
-            quat_to_euler(q, rpy);
+            if (p.rpy_valid) { rpy[0] = rpy_in[0]; rpy[1] = rpy_in[1]; rpy[2] = rpy_in[2]; }
+            else quat_to_euler(q, rpy);
             if (!(p.phase_mask & 1)) {
                 R rpm[4];
                 pid_vel(pos, q, v, Rm, rpy, a, R(p.dt_ctrl), pid, rpm, p.debug ? p.debug + di * 16 : nullptr);
@@ -488,6 +493,8 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
 #pragma unroll
             for (int c = 0; c < 9; ++c) CH_ST(&D[(13 + c) * DS + di], pid[c]);
             quat_to_euler(q, rpy_out);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) CH_ST(&p.rpy[c * DS + di], rpy_out[c]);
             S.dx[tid] = pos[0]; S.dy[tid] = pos[1]; S.dz[tid] = pos[2];
         }
         if (live && wobs) obs_own(obs_wg + dg * RW, dk, pos[2], rpy_out, v, w);
@@ -897,6 +904,10 @@ __global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
                 if (k == 0) ei[I_NEWN * G + g] = n;
                 R x, y, z;
                 reset_drone(p, (long long)e0 * N + ud, k, n, x, y, z);
+                {   // identity attitude: Euler angles (+0, -0, +0) for the next step's cache
+                    const long long dd = (long long)e0 * N + ud;
+                    CH_ST(&p.rpy[dd], R(0)); CH_ST(&p.rpy[DS + dd], -R(0)); CH_ST(&p.rpy[2 * DS + dd], R(0));
+                }
                 S.dx[ud] = x; S.dy[ud] = y; S.dz[ud] = z;
                 if (!wobs) continue;
                 float* eb = obs_wg + g * RW;
