@@ -325,10 +325,10 @@ template <class R> __device__ __forceinline__ R simple_spacing(R r, const Level&
 }
 template <class R> __device__ __forceinline__ R complex_spacing(R r, const Level& L) {
     R ds = R(L.desired);
-    R t = (r - ds) / R(0.4 + 1e-9);
+    R t = divc(r - ds, R(0.4 + 1e-9));
     R gauss = m_exp(R(-0.5) * (t * t));
-    R coll = r < R(0.3) ? R(-1.0) * (R(1.0) - (r / R(0.3 + 1e-9))) : R(0.0);
-    R pull = r > R(1.5) ? R(-0.3) * (r - R(1.5)) / R(5.0 - 1.5) : R(0.0);
+    R coll = r < R(0.3) ? R(-1.0) * (R(1.0) - divc(r, R(0.3 + 1e-9))) : R(0.0);
+    R pull = r > R(1.5) ? divc(R(-0.3) * (r - R(1.5)), R(5.0 - 1.5)) : R(0.0);
     R rew = gauss + coll + pull;
     rew += R(0.1) * (R(1) - fabs(r - ds));
     return rew;
@@ -338,7 +338,7 @@ template <class R> __device__ __forceinline__ R complex_spacing(R r, const Level
 template <class R> __device__ __forceinline__ R cattle_spacing(R r, R cc) {
     const double A = 1.2, B = 2.1, C = 3.3, K = 0.2, D = -1, R0 = 1.3, LAM = 0.8;
     if (r <= R(R0))
-        return R(A) * m_exp(-((r - R(D)) * (r - R(D))) / R(2 * (C * C))) - R(B) * m_exp(-(r * r) / R(2 * (K * K)));
+        return R(A) * m_exp(divc(-((r - R(D)) * (r - R(D))), R(2 * (C * C)))) - R(B) * m_exp(divc(-(r * r), R(2 * (K * K))));
     return cc * m_exp(R(-LAM) * r);
 }
 

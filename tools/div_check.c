@@ -38,7 +38,7 @@ int main(int argc, char** argv) {
     const double kEps = 0.1, kH = 0.2;
     const double cs[] = {0.027 /* kMass */, 1.4e-5, 2.17e-5 /* J */, 4 * 3.16e-10 /* 4 kf */, 0.2685 /* pwm scale */,
                          kEps, 1 - kH, (sqrt(1 + kEps * (1.2 * 1.2)) - 1) / kEps /* ra */, 1.0 / 60 /* dt */,
-                         1.0 / 240, 0.4 + 1e-9, 0.3 + 1e-9, 3.5};
+                         1.0 / 240, 0.4 + 1e-9, 0.3 + 1e-9, 3.5, 2 * (3.3 * 3.3), 2 * (0.2 * 0.2), 100.0, 16.0};
     long bad_total = 0;
     for (size_t k = 0; k < sizeof(cs) / sizeof(cs[0]); ++k) {
         const double c = cs[k], rc = 1.0 / c;
