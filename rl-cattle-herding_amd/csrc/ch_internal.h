@@ -63,6 +63,9 @@ struct Level {
 };
 
 // LDS carve of one v2 step workgroup (ch_step.hip); identical on host (size) and device (offsets).
+#ifndef CH_V2_MAX_BLOCK
+#define CH_V2_MAX_BLOCK 512   // v2 workgroup size bound (__launch_bounds__)
+#endif
 constexpr int kV2EnvInts = 13;
 constexpr int kV2Flags = 16;         // LDS hand-off counters between the drone wave and the cow waves + work counters
 struct V2Layout {

@@ -343,7 +343,7 @@ __device__ __forceinline__ void flock_combine(const StepParams<R>& p, V2Smem<R>&
 // GT/NT/MT > 0 specialise the kernel for one geometry (envs per workgroup, drones, cattle): the LDS
 // carve and all index arithmetic then fold to immediates, which keeps the kernel within the SGPR file.
 template <class R, int MODE, int GT, int NT, int MT>
-__global__ __launch_bounds__(256) void k_step2(StepParams<R> p) {
+__global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
     extern __shared__ __align__(16) unsigned char smem[];
     constexpr bool marl = MODE == 1;
     const int G = GT ? GT : p.G, N = NT ? NT : p.NC, M = MT ? MT : p.M, P = MT ? MT * (MT - 1) / 2 : p.P;
@@ -983,6 +983,7 @@ hipError_t launch_step_v2(const StepParams<R>& p, int block, size_t lds, hipStre
         return launch_v2_kernel<R, 1, 0, 0, 0>(p, block, lds, st);
     }
     if (G == 8 && N == 4 && M == 16) return launch_v2_kernel<R, 0, 8, 4, 16>(p, block, lds, st);          // configs[3]
+    if (G == 16 && N == 4 && M == 16) return launch_v2_kernel<R, 0, 16, 4, 16>(p, block, lds, st);         // configs[3], 512 threads
     if (G == 16 && N == 2 && M == 8) return launch_v2_kernel<R, 0, 16, 2, 8>(p, block, lds, st);          // configs[2]
     if (G == 4 && N == 2 && M == 8) return launch_v2_kernel<R, 0, 4, 2, 8>(p, block, lds, st);            // configs[1]
     return launch_v2_kernel<R, 0, 0, 0, 0>(p, block, lds, st);

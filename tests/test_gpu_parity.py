@@ -235,7 +235,7 @@ def test_full_size_properties():
 @pytest.mark.parametrize("mode,n,m,E,geom", [(0, 4, 16, 4096, None), (0, 2, 8, 1024, None), (1, 4, 32, 600, None),
                                              (0, 12, 16, 300, None), (1, 3, 8, 257, None), (0, 8, 64, 40, None),
                                              (0, 4, 16, 1000, (4, 128)), (0, 4, 16, 999, (2, 128)),
-                                             (0, 4, 16, 1001, (8, 256)), (1, 5, 16, 333, (3, 128)),
+                                             (0, 4, 16, 1001, (8, 256)), (0, 4, 16, 1003, (16, 512)), (1, 5, 16, 333, (3, 128)),
                                              (0, 2, 8, 700, (1, 256))])
 def test_step_kernels_v1_v2_bit_identical(mode, n, m, E, geom):
     """The role-split v2 step kernel (ch_step.hip, the default) and the team-per-env v1 kernel
