@@ -108,10 +108,10 @@ __device__ __forceinline__ void cow_sync(int* f, int waves, bool global) {
 // 3 after the first barrier, 4 drone chain done, 5 reward terms done, 6 herded flags received,
 // 7 bookkeeping done, 8 cow waves: alpha rows done, 9 drone positions received, 10 velocity update
 // done, 11 obs copy done, 12 CU id, 13 second barrier, 14 end)
-#define TS(slot, val) do { if (p.tstamp) p.tstamp[(long long)blockIdx.x * 64 + (slot)] = (val); } while (0)
-// diagnostics: per cow wave, chunks taken and cycles spent in each dynamic loop (slots 32 + 10 (w - 1) + 2 loop)
+#define TS(slot, val) do { if (p.tstamp) p.tstamp[(long long)blockIdx.x * 128 + (slot)] = (val); } while (0)
+// diagnostics: per cow wave 1..6, chunks taken and cycles spent in each dynamic loop (slots 64 + 10 (w - 1) + 2 loop)
 #define CHUNK_T0 const long long ck0_ = p.tstamp ? (long long)clock64() : 0
-#define CHUNK_T1(loop) do { if (p.tstamp && (threadIdx.x & 63) == 0) { long long* q_ = p.tstamp + (long long)blockIdx.x * 64 + 32 + 10 * ((threadIdx.x >> 6) - 1) + 2 * (loop); q_[0] += 1; q_[1] += (long long)clock64() - ck0_; } } while (0)
+#define CHUNK_T1(loop) do { if (p.tstamp && (threadIdx.x & 63) == 0 && (threadIdx.x >> 6) <= 6) { long long* q_ = p.tstamp + (long long)blockIdx.x * 128 + 64 + 10 * ((threadIdx.x >> 6) - 1) + 2 * (loop); q_[0] += 1; q_[1] += (long long)clock64() - ck0_; } } while (0)
 
 template <class R>
 struct V2Smem {
@@ -857,31 +857,45 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
         if (ct == 0) TS(21, (long long)clock64());
         const int T = G * M * N, MN = M * N;
         const float rMN = 1.0f / (float)MN, rN = 1.0f / (float)N;
-        for (;;) {   // (cow, drone) items of flocking envs: shepherd and predator terms
+        // (cow, drone) items of flocking envs: shepherd and predator terms.  A chunk of 64 items holds
+        // whole cows when N divides 64 (the cow's N items are consecutive): the wave that computed a cow's
+        // terms then finishes that cow's velocity update itself (lane k = 0), with no workgroup sync.
+        const bool fuse = (64 % N) == 0;
+        for (;;) {
             const int b = grab(fl + C_DELTA, 64), q = b + lane;
             if (b >= nf * MN) break;
             CHUNK_T0;
-            if (q < nf * MN) {
-                const int f = qdiv(q, MN, rMN), rem = q - f * MN, j = qdiv(rem, N, rN), k = rem - j * N;
-                const int g = flist[f];
-                if (k < ei[I_N * G + g]) delta_term(S, N, M, g * M + j, g, k, T);
+            int f = 0, j = 0, k = 0, g = 0, n = 0;
+            const bool valid = q < nf * MN;
+            if (valid) {
+                f = qdiv(q, MN, rMN);
+                const int rem = q - f * MN;
+                j = qdiv(rem, N, rN); k = rem - j * N;
+                g = flist[f]; n = ei[I_N * G + g];
+                if (k < n) delta_term(S, N, M, g * M + j, g, k, T);
+            }
+            if (fuse) {
+                wave_sync();   // the cow's terms, written by other lanes of this wave
+                if (valid && k == 0) flock_combine(p, S, N, M, e0, g * M + j, n, T);
             }
             CHUNK_T1(3);
         }
         if (ct == 0) TS(16, (long long)clock64());
-        cow_sync(fl + F_Q, W1, false);   // every drone term of every cow
-        if (ct == 0) TS(17, (long long)clock64());
-        for (;;) {   // cows of flocking envs only
-            const int b = grab(fl + C_FLOCK, 64), u = b + lane;
-            if (b >= nf * M) break;
-            CHUNK_T0;
-            if (u < nf * M) {
-                const int f = qdiv(u, M, rM), g = flist[f], j = u - f * M;
-                flock_combine(p, S, N, M, e0, g * M + j, ei[I_N * G + g], T);
+        if (!fuse) {
+            cow_sync(fl + F_Q, W1, false);   // every drone term of every cow
+            if (ct == 0) TS(17, (long long)clock64());
+            for (;;) {   // cows of flocking envs only
+                const int b = grab(fl + C_FLOCK, 64), u = b + lane;
+                if (b >= nf * M) break;
+                CHUNK_T0;
+                if (u < nf * M) {
+                    const int f = qdiv(u, M, rM), g = flist[f], j = u - f * M;
+                    flock_combine(p, S, N, M, e0, g * M + j, ei[I_N * G + g], T);
+                }
+                CHUNK_T1(4);
             }
-            CHUNK_T1(4);
         }
-        if (lane == 0) TS(ct == 0 ? 10 : 28 + (ct >> 6), (long long)clock64());
+        if (lane == 0) TS(40 + (tid >> 6), (long long)clock64());   // this cow wave's flock work done
         if (ct == 0) TS(31, (long long)nf);
         lds_wait(fl + F_R, 1);    // the reset list
         const int nr = ei[NR_AT];

@@ -23,7 +23,7 @@ def trace(mode, E, n, m, prec, G=None, B=None, steps=4):
     g, blk, lds, kv = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int32()
     L.ch__geometry(b.handle, ctypes.byref(g), ctypes.byref(blk), ctypes.byref(lds), ctypes.byref(kv))
     grid = (E + g.value - 1) // g.value
-    ts = torch.zeros((grid, 64), dtype=torch.int64, device=b.device)
+    ts = torch.zeros((grid, 128), dtype=torch.int64, device=b.device)
     b.reset()
     for _ in range(250):   # steady state: resets have desynchronised the flocking parity
         b.step(random_actions=True, autoreset=True, terminal_obs=False)
@@ -56,7 +56,7 @@ def trace(mode, E, n, m, prec, G=None, B=None, steps=4):
             r2 = lambda k: (t[sel, k] - t[sel, 2]).mean()  # noqa: E731
             print(f"   cow waves [{name}, {int(sel.sum())} WGs]: E {r2(11):.0f} pairs {r2(18):.0f} A {r2(20):.0f} rows+sync {r2(21):.0f} "
                   f"D {r2(9):.0f} H(drone) {r2(6):.0f} delta {r2(16):.0f} Q {r2(17):.0f} flock {r2(10):.0f} "
-                  f"| last cow wave done {(t[sel][:, [10, 29, 30]].max(1) - t[sel, 2]).mean():.0f} "
+                  f"| cow waves done (mean per wave) {' '.join(f'{(t[sel, 40 + w] - t[sel, 2]).mean():.0f}' for w in range(1, blk.value // 64))} "
                   f"| drone book {r2(7):.0f} B1 {r2(13):.0f} end {r2(14):.0f}")
         print(f"   drone wave after H: dtaskB {rel(26):.0f} pre-fence {rel(27):.0f} published {rel(15):.0f} "
               f"reward {rel(19):.0f} metrics stored {rel(28):.0f} book {rel(7):.0f}")
@@ -80,12 +80,12 @@ def trace(mode, E, n, m, prec, G=None, B=None, steps=4):
         # workgroup's drone wave: wave 1 in the grid's first half, wave 3 in the second
         names = ("pairs", "cows", "rows", "delta", "flock")
         half = len(t) // 2
-        for w in (1, 2, 3):
+        for w in range(1, min(7, blk.value // 64)):
             sh = np.array([(w == 1) if k < half else (w == 3) for k in range(len(t))])
             for lab, sel in (("shared", sh), ("free", ~sh)):
                 if not sel.any():
                     continue
-                base = 32 + 10 * (w - 1)
+                base = 64 + 10 * (w - 1)
                 parts = []
                 for li, nm in enumerate(names):
                     c = t[sel, base + 2 * li].astype(np.float64)
@@ -110,7 +110,7 @@ def trace(mode, E, n, m, prec, G=None, B=None, steps=4):
         print(f"   flocking envs per WG: mean {nfv.mean():.2f} | slow WGs' nf {nfv[slow].tolist()} | cycles by nf: " +
               " ".join(f"{v}:{cyc[nfv == v].mean():.0f}" for v in np.unique(nfv)))
         for k in slow:
-            print(f"     slow WG {k}: flock end per cow wave {t[k, 10] - t[k, 2]} {t[k, 29] - t[k, 2]} {t[k, 30] - t[k, 2]}")
+            print(f"     slow WG {k}: flock end per cow wave {[int(t[k, 40 + w] - t[k, 2]) for w in range(1, blk.value // 64)]}")
         for k in slow:
             print(f"     slow WG {k}: cyc {cyc[k]:.0f} chain {chain[k]:.0f} tail {tail[k]:.0f} B0 {t[k, 3] - t[k, 2]} "
                   f"terms {t[k, 5] - t[k, 4]} H {t[k, 6] - t[k, 5]} book {t[k, 7] - t[k, 6]} B1 {t[k, 13] - t[k, 7]} "
@@ -155,7 +155,7 @@ def back_to_back(mode="ctde", E=4096, n=4, m=16, prec="f64", k=12):
     g, blk, lds, kv = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int32()
     L.ch__geometry(b.handle, ctypes.byref(g), ctypes.byref(blk), ctypes.byref(lds), ctypes.byref(kv))
     grid = (E + g.value - 1) // g.value
-    ts = torch.zeros((k, grid, 64), dtype=torch.int64, device=b.device)
+    ts = torch.zeros((k, grid, 128), dtype=torch.int64, device=b.device)
     b.reset()
     for _ in range(250):
         b.step(random_actions=True, autoreset=True, terminal_obs=False)
