@@ -309,9 +309,11 @@ int ch_create(const ch_config* c, int64_t n_envs, int32_t device, ch_handle** ou
             h->lds = V2Layout(16, 4, 16, h->P, c->mode, (int)h->rsize).bytes();
             h->block = 512;
         }
-        // measured (tools/geom_sweep.py, MI355X): the dataflow kernel wins for CTDE with up to 8 drones;
-        // MARL and the 9..12-drone CTDE configs are still faster on the team-per-env kernel
-        if (c->mode == CH_MODE_MARL || h->NC > 8) h->kernel = 1;
+        // measured (tools/ab/marl.py, MI355X, 4096 envs): the dataflow kernel wins for every CTDE size
+        // (2x8 19.4 vs 41.1 us, 8x16 39.7 vs 55.8, 12x16 59.9 vs 67.1) and for MARL with up to 16
+        // cattle (3x8 25.8 vs 43.2); MARL 4x32 (BASELINE configs[4]) is still faster on the
+        // team-per-env kernel (87.6 vs 92-95 us: its 496-pair alpha table per env)
+        if (c->mode == CH_MODE_MARL && h->M > 16) h->kernel = 1;
         if (h->lds > budget) h->kernel = 1;   // one env's pair table alone exceeds the budget
         std::vector<uint16_t> pl((size_t)std::max(h->P, 1));
         for (int i = 0, r = 0; i < h->M; ++i)
