@@ -159,7 +159,123 @@ static void quat_mul(const double* a, const double* b, double* o) {
     o[3] = a[3] * b[3] - a[0] * b[0] - a[1] * b[1] - a[2] * b[2];
 }
 
-static void drone_substep(const och_config* c, double* p, double* q, double* v, double* w, const double* rpm, double dt) {
+/* ---------------------------------------------------------------------------------------------
+ * Physics variants (BaseAviary.py:420-450): extra link forces applied after _physics, in the
+ * reference's call order (ground effect, drag, downwash), each rotated from LINK_FRAME to world on
+ * its own like p.applyExternalForce does; DYN replaces _physics + stepSimulation by the explicit
+ * model _dynamics (1043-1102) + _integrateQ (1104-1118).  cf2x.urdf:5 coefficients.
+ * ------------------------------------------------------------------------------------------- */
+static const double GND_EFF_COEFF = 11.36859, PROP_RADIUS = 2.31348e-2, ARM = 0.0397;
+static const double DRAG_XY = 9.1785e-7, DRAG_Z = 10.311e-7;
+static const double DW_C1 = 2267.18, DW_C2 = .16, DW_C3 = -.11;
+static const double THRUST2WEIGHT = 2.25;
+
+enum { PH_PYB = 0, PH_DYN = 1, PH_GND = 2, PH_DRAG = 3, PH_DW = 4, PH_ALL = 5 };
+static int ph_gnd(int ph) { return ph == PH_GND || ph == PH_ALL; }
+static int ph_drag(int ph) { return ph == PH_DRAG || ph == PH_ALL; }
+static int ph_dw(int ph) { return ph == PH_DW || ph == PH_ALL; }
+
+/* GND_EFF_H_CLIP (BaseAviary.py:163-173): 0.25 r_prop sqrt(15 MAX_RPM^2 KF c_gnd / MAX_THRUST) */
+double och_gnd_eff_h_clip(void) {
+    const double gravity = G * MASS;
+    const double max_rpm = sqrt((THRUST2WEIGHT * gravity) / (4 * KF));
+    const double max_thrust = (4 * KF * (max_rpm * max_rpm));
+    return 0.25 * PROP_RADIUS * sqrt((15 * (max_rpm * max_rpm) * KF * GND_EFF_COEFF) / max_thrust);
+}
+
+typedef struct phys_ctx {
+    int physics;
+    const double* last_rpm;        /* [4] last_clipped_action of this drone */
+    const double (*pos)[3];        /* all drones' positions at the start of the substep */
+    int n, self;
+    double h_clip;
+} phys_ctx;
+
+static void physics_forces(const phys_ctx* x, const double* p, const double* q, const double* v, const double* R,
+                           const double* rpm, double* F, double* Tw) {
+    if (ph_gnd(x->physics)) {   /* _groundEffect (943-980) */
+        double rpy[3]; och_euler_from_quat(q, rpy);
+        double g[4];
+        for (int i = 0; i < 4; ++i) {
+            double h = p[2] + (R[6] * PROP[i][0] + R[7] * PROP[i][1] + R[8] * 0.0);   /* prop link COM z */
+            if (h < x->h_clip) h = x->h_clip;
+            double r = PROP_RADIUS / (4 * h);
+            g[i] = rpm[i] * rpm[i] * KF * GND_EFF_COEFF * (r * r);
+        }
+        if (fabs(rpy[0]) < M_PI / 2 && fabs(rpy[1]) < M_PI / 2) {
+            for (int i = 0; i < 4; ++i) {
+                double fw[3] = {R[2] * g[i], R[5] * g[i], R[8] * g[i]};
+                double rw[3] = {R[0] * PROP[i][0] + R[1] * PROP[i][1], R[3] * PROP[i][0] + R[4] * PROP[i][1],
+                                R[6] * PROP[i][0] + R[7] * PROP[i][1]};
+                double t[3]; cross3(rw, fw, t);
+                for (int k = 0; k < 3; ++k) { F[k] += fw[k]; Tw[k] += t[k]; }
+            }
+        }
+    }
+    if (ph_drag(x->physics)) {  /* _drag (982-1011) on last_clipped_action, applied at link 4 (the COM) */
+        const double* lr = x->last_rpm;
+        double sum = 0;
+        for (int i = 0; i < 4; ++i) sum += (2 * M_PI * lr[i]) / 60;
+        const double dv[3] = {(-DRAG_XY * sum) * v[0], (-DRAG_XY * sum) * v[1], (-DRAG_Z * sum) * v[2]};
+        double b[3];   /* base_rot.T @ (drag_factors * vel): body frame */
+        for (int k = 0; k < 3; ++k) b[k] = R[0 + k] * dv[0] + R[3 + k] * dv[1] + R[6 + k] * dv[2];
+        for (int k = 0; k < 3; ++k) F[k] += R[3 * k + 0] * b[0] + R[3 * k + 1] * b[1] + R[3 * k + 2] * b[2];
+    }
+    if (ph_dw(x->physics)) {    /* _downwash (1013-1041): one link-4 force per drone above within 10 m */
+        const double* me = x->pos[x->self];
+        for (int i = 0; i < x->n; ++i) {
+            const double dz = x->pos[i][2] - me[2];
+            const double ex = x->pos[i][0] - me[0], ey = x->pos[i][1] - me[1];
+            const double dxy = sqrt(ex * ex + ey * ey);
+            if (dz > 0 && dxy < 10) {
+                const double r = PROP_RADIUS / (4 * dz);
+                const double alpha = DW_C1 * (r * r);
+                const double beta = DW_C2 * dz + DW_C3;
+                const double u = dxy / beta;
+                const double fz = -alpha * exp(-.5 * (u * u));
+                F[0] += R[2] * fz; F[1] += R[5] * fz; F[2] += R[8] * fz;
+            }
+        }
+    }
+}
+
+/* _dynamics (BaseAviary.py:1043-1102) + _integrateQ (1104-1118): explicit Euler on the body rates
+ * rr; the returned world angular velocity is rotation(old quat) @ rr, what resetBaseVelocity stores. */
+static void dyn_substep(double* p, double* q, double* v, double* w, double* rr, const double* rpm, double dt) {
+    double R[9]; och_matrix_from_quat(q, R);
+    double f[4], z[4];
+    for (int i = 0; i < 4; ++i) { f[i] = rpm[i] * rpm[i] * KF; z[i] = rpm[i] * rpm[i] * KM; }
+    const double T = f[0] + f[1] + f[2] + f[3];
+    const double fw[3] = {R[2] * T, R[5] * T, R[8] * T - G * MASS};
+    const double zt = -z[0] + z[1] - z[2] + z[3];
+    const double ls = ARM / sqrt(2.0);
+    const double xt = (f[0] + f[1] - f[2] - f[3]) * ls, yt = (-f[0] + f[1] + f[2] - f[3]) * ls;
+    const double Jr[3] = {JX * rr[0], JY * rr[1], JZ * rr[2]};
+    double c[3]; cross3(rr, Jr, c);
+    const double tq[3] = {xt - c[0], yt - c[1], zt - c[2]};
+    const double jinv[3] = {1.0 / JX, 1.0 / JY, 1.0 / JZ};   /* np.linalg.inv(diag J), pinned by the fixture */
+    for (int i = 0; i < 3; ++i) {
+        v[i] = v[i] + dt * (fw[i] / MASS);
+        rr[i] = rr[i] + dt * (jinv[i] * tq[i]);
+    }
+    for (int i = 0; i < 3; ++i) p[i] = p[i] + dt * v[i];
+    const double on = sqrt(rr[0] * rr[0] + rr[1] * rr[1] + rr[2] * rr[2]);
+    if (!(fabs(on) <= 1e-8)) {   /* np.isclose(omega_norm, 0): atol 1e-8 */
+        const double th = on * dt / 2, co = cos(th), si = sin(th), k = 2 / on;
+        const double P = rr[0], Q = rr[1], Rz = rr[2];
+        const double L[4][4] = {{0, Rz, -Q, P}, {-Rz, 0, P, Q}, {Q, -P, 0, Rz}, {-P, -Q, -Rz, 0}};
+        double o[4];
+        for (int i = 0; i < 4; ++i) {
+            double m[4];
+            for (int j = 0; j < 4; ++j) m[j] = (i == j ? co : 0.0) + (k * (L[i][j] * .5)) * si;
+            o[i] = m[0] * q[0] + m[1] * q[1] + m[2] * q[2] + m[3] * q[3];
+        }
+        for (int i = 0; i < 4; ++i) q[i] = o[i];
+    }
+    for (int i = 0; i < 3; ++i) w[i] = R[3 * i + 0] * rr[0] + R[3 * i + 1] * rr[1] + R[3 * i + 2] * rr[2];
+}
+static void drone_substep(const och_config* c, double* p, double* q, double* v, double* w, const double* rpm, double dt,
+                          const phys_ctx* x) {
     double R[9]; och_matrix_from_quat(q, R);
     double F[3] = {0, 0, 0}, Tw[3] = {0, 0, 0};
     for (int i = 0; i < 4; ++i) {
@@ -174,6 +290,7 @@ static void drone_substep(const och_config* c, double* p, double* q, double* v, 
     double tz = (-t0 + t1 - t2 + t3);
     if (c->torque_world) Tw[2] += tz;
     else { Tw[0] += R[2] * tz; Tw[1] += R[5] * tz; Tw[2] += R[8] * tz; }
+    if (x) physics_forces(x, p, q, v, R, rpm, F, Tw);
     F[2] += -MASS * G;
     double k = c->damping;
     if (k != 0.0) {
@@ -705,6 +822,8 @@ void och_reset(const och_config* c, och_state* s) {
         s->dq[i][0] = s->dq[i][1] = s->dq[i][2] = 0; s->dq[i][3] = 1;
         for (int k = 0; k < 3; ++k) { s->dv[i][k] = 0; s->dw[i][k] = 0; }
         s->active[i] = (uint8_t)(i < n);
+        for (int k = 0; k < 4; ++k) s->last_rpm[i][k] = 0;   /* _housekeeping (565, 581-582) */
+        for (int k = 0; k < 3; ++k) s->rpy_rates[i][k] = 0;
         if (!c->compat) for (int k = 0; k < 3; ++k) { s->pid_last_rpy[i][k] = 0; s->pid_int_pos[i][k] = 0; s->pid_int_rpy[i][k] = 0; }
     }
     s->spawn_index += 1;
@@ -757,9 +876,22 @@ int och_step(const och_config* c, och_state* s, const float* actions, float* obs
         och_pid_vel(s->dp[k], s->dq[k], s->dv[k], tp, tr, tv, dt_ctrl, s->pid_last_rpy[k], s->pid_int_pos[k],
                     s->pid_int_rpy[k], rpm[k]);
     }
+    const int ph = c->physics;
+    const double h_clip = och_gnd_eff_h_clip();
     for (int sub = 0; sub < substeps; ++sub) {
-        for (int k = 0; k < n; ++k) drone_substep(c, s->dp[k], s->dq[k], s->dv[k], s->dw[k], rpm[k], dt);
-        for (int j = 0; j < c->m; ++j) { s->cp[j][0] += s->cv[j][0] * dt; s->cp[j][1] += s->cv[j][1] * dt; }
+        double pos0[OCH_NMAX][3];   /* self.pos as of this substep's start (downwash) */
+        memcpy(pos0, s->dp, sizeof(pos0));
+        for (int k = 0; k < n; ++k) {
+            if (ph == PH_DYN) {
+                dyn_substep(s->dp[k], s->dq[k], s->dv[k], s->dw[k], s->rpy_rates[k], rpm[k], dt);
+            } else {
+                phys_ctx x = {ph, s->last_rpm[k], (const double (*)[3])pos0, n, k, h_clip};
+                drone_substep(c, s->dp[k], s->dq[k], s->dv[k], s->dw[k], rpm[k], dt, ph == PH_PYB ? NULL : &x);
+            }
+        }
+        if (ph != PH_DYN)   /* no p.stepSimulation under DYN: the cattle bodies do not move (447-448) */
+            for (int j = 0; j < c->m; ++j) { s->cp[j][0] += s->cv[j][0] * dt; s->cp[j][1] += s->cv[j][1] * dt; }
+        for (int k = 0; k < n; ++k) memcpy(s->last_rpm[k], rpm[k], sizeof(rpm[k]));   /* 450 */
     }
     if (s->step_counter_A % 2 == 0) {
         double cp[2 * OCH_MMAX], cv[2 * OCH_MMAX], nv[2 * OCH_MMAX], dxy[2 * OCH_NMAX];

@@ -31,6 +31,8 @@ typedef struct och_config {
     const double* spawn_table;   /* [n_scen][n_cows][2] */
     int32_t spawn_scenarios, spawn_cows;
     int32_t marl_wrapper;     /* MARL: 1 = RLlibMultiAgentWrapper.step semantics, 0 = bare env.step */
+    int32_t physics;          /* Physics enum order (utils/enums.py:13-21): 0 PYB, 1 DYN, 2 PYB_GND,
+                                 3 PYB_DRAG, 4 PYB_DW, 5 PYB_GND_DRAG_DW */
 } och_config;
 
 typedef struct och_state {
@@ -44,6 +46,8 @@ typedef struct och_state {
     uint8_t active[OCH_NMAX];
     int64_t episode;                    /* resets so far (Philox counter for reset draws) */
     int64_t env_id;                     /* global env index (Philox key part) */
+    double last_rpm[OCH_NMAX][4];       /* last_clipped_action (BaseAviary.py:450, 565): drag input */
+    double rpy_rates[OCH_NMAX][3];      /* DYN body rates (BaseAviary.py:581-582, 1075) */
 } och_state;
 
 #ifdef __cplusplus
@@ -60,6 +64,7 @@ void och_pid_vel(const double* pos, const double* quat, const double* vel, const
 double och_simple_spacing(double r, int level);
 double och_complex_spacing(double r, int level);
 double och_cattle_spacing(double r);
+double och_gnd_eff_h_clip(void);   /* BaseAviary.py:173 */
 
 /* whole env */
 int  och_obs_rows(const och_config* c);

@@ -30,7 +30,7 @@ class Config(ctypes.Structure):
                 ("compat", ctypes.c_int32), ("damping", ctypes.c_double), ("torque_world", ctypes.c_int32),
                 ("gyro", ctypes.c_int32), ("seed", ctypes.c_uint64),
                 ("spawn_table", ctypes.POINTER(ctypes.c_double)), ("spawn_scenarios", ctypes.c_int32),
-                ("spawn_cows", ctypes.c_int32), ("marl_wrapper", ctypes.c_int32)]
+                ("spawn_cows", ctypes.c_int32), ("marl_wrapper", ctypes.c_int32), ("physics", ctypes.c_int32)]
 
 
 D3 = ctypes.c_double * 3
@@ -47,7 +47,8 @@ class State(ctypes.Structure):
                 ("prev_cent", ctypes.c_double), ("has_prev", ctypes.c_int32),
                 ("clock", ctypes.c_double), ("level", ctypes.c_int32), ("tally", ctypes.c_int32),
                 ("spawn_index", ctypes.c_int32), ("active", ctypes.c_uint8 * NMAX),
-                ("episode", ctypes.c_int64), ("env_id", ctypes.c_int64)]
+                ("episode", ctypes.c_int64), ("env_id", ctypes.c_int64),
+                ("last_rpm", (ctypes.c_double * 4) * NMAX), ("rpy_rates", (ctypes.c_double * 3) * NMAX)]
 
 
 _lib = None
@@ -80,7 +81,13 @@ def lib():
         _lib.och_random_actions.argtypes = [P(Config), ctypes.c_int64, ctypes.c_int64, fp]
         _lib.och_batch_rollout.argtypes = [P(Config), P(State), ctypes.c_int64, ctypes.c_int64, ctypes.c_int]
         _lib.och_batch_rollout.restype = ctypes.c_double
+        _lib.och_gnd_eff_h_clip.argtypes = []
+        _lib.och_gnd_eff_h_clip.restype = ctypes.c_double
     return _lib
+
+
+def gnd_eff_h_clip():
+    return lib().och_gnd_eff_h_clip()
 
 
 def _dp(a):
@@ -146,7 +153,7 @@ class Env:
 
     def __init__(self, mode, n_ctor, m, spawn_table, min_drones=None, max_drones=None, start_level=None,
                  compat=True, seed=0x5EED, env_id=0, damping=0.04, torque_world=True, gyro=True,
-                 ctrl_freq=60, pyb_freq=240, marl_wrapper=True):
+                 ctrl_freq=60, pyb_freq=240, marl_wrapper=True, physics=0):
         self.table = np.ascontiguousarray(spawn_table, np.float64)
         if start_level is None:
             start_level = 7 if mode == 0 else 0
@@ -156,7 +163,7 @@ class Env:
                           start_level=start_level, ctrl_freq=ctrl_freq, pyb_freq=pyb_freq,
                           compat=int(compat), damping=damping, torque_world=int(torque_world), gyro=int(gyro),
                           seed=seed, spawn_table=_dp(self.table), spawn_scenarios=self.table.shape[0],
-                          spawn_cows=self.table.shape[1], marl_wrapper=int(marl_wrapper))
+                          spawn_cows=self.table.shape[1], marl_wrapper=int(marl_wrapper), physics=int(physics))
         self.st = State()
         lib().och_init(ctypes.byref(self.cfg), ctypes.byref(self.st), env_id)
         self.rows = lib().och_obs_rows(ctypes.byref(self.cfg))
@@ -217,6 +224,13 @@ class Env:
         st.has_prev = int(s["has_prev"]); st.prev_cent = float(s["prev_cent"]) if st.has_prev else 0.0
         st.clock = float(s["clock"]); st.level = int(s["level"]); st.tally = int(s["tally"])
         st.spawn_index = int(s["spawn_index"])
+        lr = np.asarray(s["last_rpm"]) if "last_rpm" in s else np.zeros((NMAX, 4))
+        rr = np.asarray(s["rpy_rates"]) if "rpy_rates" in s else np.zeros((NMAX, 3))
+        for i in range(NMAX):
+            for k in range(4):
+                st.last_rpm[i][k] = lr[i][k]
+            for k in range(3):
+                st.rpy_rates[i][k] = rr[i][k]
 
     def get_state(self):
         st = self.st
@@ -228,7 +242,7 @@ class Env:
                 "step_counter_A": st.step_counter_A, "prev_cent": st.prev_cent if st.has_prev else np.nan,
                 "has_prev": st.has_prev, "clock": st.clock, "level": st.level, "tally": st.tally,
                 "spawn_index": st.spawn_index, "active": np.array(list(st.active), np.uint8),
-                "episode": st.episode}
+                "episode": st.episode, "last_rpm": a(st.last_rpm, 4), "rpy_rates": a(st.rpy_rates, 3)}
 
 
 def batch_rollout(mode, n, m, spawn_table, E, T, threads=0, seed=0x5EED, compat=True):

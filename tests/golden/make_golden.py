@@ -18,7 +18,9 @@ task_ctde.npz      ``_computeReward`` → ``_computeTerminated`` → ``_computeT
                    (sb3_envs/BaseAviary.py:458-460, CattleAviary.py:213-552) on synthetic states, all levels.
 task_marl.npz      the RLlib wrapper's per-agent call sequence (marl_wrapper.py:77-119 over
                    MARLCattleAviary.py:110-383) on synthetic states, all levels.
-ctde_roll_*.npz    whole ``CattleAviary.step`` rollouts incl. auto-resets (stub physics in the loop).
+ctde_roll_*.npz    whole ``CattleAviary.step`` rollouts incl. auto-resets (stub physics in the loop);
+                   ``*_dyn`` / ``*_pyb_gnd`` / ``*_pyb_drag`` / ``*_pyb_dw`` / ``*_pyb_gnd_drag_dw``: the physics
+                   variants (BaseAviary.py:420-450, 943-1118), ``--physics`` regenerates only these.
 marl_roll_*.npz    whole ``RLlibMultiAgentWrapper.step`` rollouts.
 reset.npz          ``reset`` bookkeeping: spawn-index sequence, drone initial positions, cattle spawn table.
 """
@@ -58,12 +60,13 @@ W = refstubs.WORLD
 NMAX, MMAX = 12, 32
 
 
-def make_ctde(n, m, level=7):
+def make_ctde(n, m, level=7, physics=None):
     orig = CA_mod.CurriculumLearning
     CA_mod.CurriculumLearning = lambda _lvl: CurriculumLearning(level)
     try:
         with quiet():
-            env = CA_mod.CattleAviary(num_drones=n, num_cattle=m)
+            kw = {} if physics is None else {"physics": physics}
+            env = CA_mod.CattleAviary(num_drones=n, num_cattle=m, **kw)
     finally:
         CA_mod.CurriculumLearning = orig
     env.MIN_NUM_DRONES = env.MAX_NUM_DRONES = n
@@ -88,7 +91,7 @@ def make_marl(n, m, level=0):
 # State capture / injection (stub world bodies are the physics state)
 # --------------------------------------------------------------------------------------
 
-def capture(env, marl_agents=None):
+def capture(env, marl_agents=None, physics_state=False):
     n, m = env.NUM_DRONES, env.NUM_CATTLE
     s = {
         "n": n, "m": m,
@@ -115,6 +118,14 @@ def capture(env, marl_agents=None):
         b = W.bodies[int(env.CATTLE_IDS[j])]
         s["cow_pos"][j] = b.pos[:2]
         s["cow_vel"][j] = b.vel[:2]
+    if physics_state:
+        # BaseAviary.step's per-drone physics-variant state: last_clipped_action (drag, 450) and
+        # the DYN body rates (581-582, 1043-1075)
+        s["last_rpm"] = np.zeros((NMAX, 4))
+        s["rpy_rates"] = np.zeros((NMAX, 3))
+        s["last_rpm"][:n] = env.last_clipped_action
+        if hasattr(env, "rpy_rates"):
+            s["rpy_rates"][:n] = env.rpy_rates
     if marl_agents is not None:
         for a in marl_agents:
             s["active"][int(a.split("_")[1])] = 1
@@ -429,6 +440,61 @@ def gen_ctde_rollout(rng, n, m, steps, level=7, tag=None, hover=False):
     print(name, steps, "steps; resets at", rec["reset_at"][:6], "nan rewards", int(np.isnan(out["reward"]).sum()))
 
 
+PHYSICS_IDS = {"pyb": 0, "dyn": 1, "pyb_gnd": 2, "pyb_drag": 3, "pyb_dw": 4, "pyb_gnd_drag_dw": 5}
+
+
+def gen_physics_rollout(rng, physics, n, m, steps, scale=1.0, tag=None, stack=None):
+    """CattleAviary.step under a physics variant (sb3_envs/BaseAviary.py:420-450): DYN explicit
+    dynamics (1043-1118), ground effect (943-980), drag (982-1011), downwash (1013-1041).  The
+    captured state carries last_clipped_action and rpy_rates; J_INV is stored to pin its value."""
+    from gym_pybullet_drones.utils.enums import Physics
+    env = make_ctde(n, m, physics=Physics(physics))
+    with quiet():
+        obs, _ = env.reset()
+    if stack is not None:   # drones stacked (dz, dxy per index) so the downwash / ground terms are large
+        z0, dz, dxy = stack
+        xyz = np.array([[dxy * i, 0.0, z0 + dz * i] for i in range(n)])
+        cows = np.array([W.bodies[int(env.CATTLE_IDS[j])].pos[:2] for j in range(m)])
+        _inject(env, xyz, cows)
+    rec = {"state": [], "action": [], "obs": [], "reward": [], "terminated": [], "truncated": [], "reset_at": []}
+    for t in range(steps):
+        a = (rng.uniform(-1, 1, (n, 4)) * scale).astype(np.float32)
+        rec["state"].append(capture(env, physics_state=True))
+        with quiet():
+            obs, r, te, tr, _ = env.step(a)
+        rec["action"].append(a); rec["obs"].append(obs); rec["reward"].append(r)
+        rec["terminated"].append(te); rec["truncated"].append(tr)
+        if te or tr:
+            with quiet():
+                env.reset()
+            rec["reset_at"].append(t)
+    out = {"action": np.array(rec["action"]), "obs": np.array(rec["obs"]), "reward": np.array(rec["reward"]),
+           "terminated": np.array(rec["terminated"], np.uint8), "truncated": np.array(rec["truncated"], np.uint8),
+           "reset_at": np.array(rec["reset_at"], np.int64), "level": np.int64(7),
+           "physics": np.int64(PHYSICS_IDS[physics]), "j_inv": np.asarray(env.J_INV),
+           "gnd_eff_h_clip": np.float64(env.GND_EFF_H_CLIP)}
+    out.update({"state_" + k: v for k, v in stack_states(rec["state"]).items()})
+    name = tag or f"ctde_roll_n{n}_m{m}_l7_{physics}"
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    print(name, steps, "steps; resets at", rec["reset_at"][:6])
+
+
+def gen_physics():
+    rng = np.random.default_rng(20251107)
+    np.random.seed(777)
+    import random
+    random.seed(777)
+    gen_physics_rollout(rng, "dyn", 4, 8, 200)
+    gen_physics_rollout(rng, "pyb_gnd", 4, 8, 200)
+    gen_physics_rollout(rng, "pyb_drag", 4, 8, 200)
+    gen_physics_rollout(rng, "pyb_dw", 5, 8, 200)
+    gen_physics_rollout(rng, "pyb_gnd_drag_dw", 6, 16, 200)
+    gen_physics_rollout(rng, "pyb_dw", 4, 8, 60, scale=0.2, stack=(0.27, 0.12, 0.25),
+                        tag="ctde_roll_n4_m8_l7_pyb_dw_stacked")
+    gen_physics_rollout(rng, "pyb_gnd_drag_dw", 3, 8, 60, scale=0.2, stack=(0.19, 0.1, 0.22),
+                        tag="ctde_roll_n3_m8_l7_pyb_gnd_drag_dw_low")
+
+
 def gen_marl_rollout(rng, n, m, steps, level=0, tag=None):
     """Whole RLlibMultiAgentWrapper.step (marl_wrapper.py:77-119) — no auto-reset unless __all__."""
     env = make_marl(n, m, level=level)
@@ -518,4 +584,8 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if "--physics" in sys.argv:   # the physics-variant fixtures only (own seeds)
+        gen_physics()
+    else:
+        main()
+        gen_physics()

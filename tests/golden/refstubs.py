@@ -264,6 +264,20 @@ def _make_pybullet():
         for i in range(3):
             b.torque[i] += t[i]
     p.applyExternalTorque = applyExternalTorque
+
+    def getLinkStates(bid, linkIndices, computeLinkVelocity=0, computeForwardKinematics=0, **k):
+        # linkWorldPosition (entry 0) = the link's centre of mass: the prop offsets of cf2x.urdf
+        # (links 0-3, inertial origins at +-0.028) or the base origin (link 4)
+        b = WORLD.bodies[int(bid)]
+        R = _R(b.quat)
+        out = []
+        for li in linkIndices:
+            off = PROP_OFFSETS[li] if 0 <= li <= 3 else (0.0, 0.0, 0.0)
+            pos = tuple(np.array(b.pos) + R @ np.array(off))
+            out.append((pos, tuple(b.quat), (0.0, 0.0, 0.0), (0.0, 0.0, 0.0, 1.0), pos, tuple(b.quat),
+                        tuple(b.vel), tuple(b.angv)))
+        return out
+    p.getLinkStates = getLinkStates
     p.stepSimulation = lambda **k: _step_world()
     p.changeDynamics = lambda *a, **k: None
     return p

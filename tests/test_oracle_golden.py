@@ -86,7 +86,9 @@ def test_rollout_step_matches_reference(fname, spawn16):
     mode = 0 if fname.startswith("ctde") else 1
     s0 = state_at(d, "state_", 0)
     n, m = int(s0["n"]), int(s0["m"])
-    env = O.Env(mode, n, m, spawn16, start_level=int(s0["ctor_level"]))
+    physics = int(d["physics"]) if "physics" in d.files else 0
+    env = O.Env(mode, n, m, spawn16, start_level=int(s0["ctor_level"]) if "ctor_level" in s0 else 7,
+                physics=physics)
     resets = set(d["reset_at"].tolist())
     T = len(d["action"])
     for t in range(T):
@@ -113,6 +115,16 @@ def test_rollout_step_matches_reference(fname, spawn16):
             assert close(g["cow_vel"][:m], nx["cow_vel"][:m], 1e-12, 1e-14)[0], t
             for k in ("step_counter", "step_counter_A", "level", "tally"):
                 assert g[k] == nx[k], (t, k)
+            if physics:
+                assert close(g["last_rpm"][:n], nx["last_rpm"][:n], 1e-9, 1e-9)[0], t
+                assert close(g["rpy_rates"][:n], nx["rpy_rates"][:n], 1e-9, 1e-12)[0], t
+
+
+def test_physics_constants_match_reference():
+    """GND_EFF_H_CLIP (BaseAviary.py:173) and J_INV = inv(diag J) (1199) as the reference computes them."""
+    d = load("ctde_roll_n4_m8_l7_dyn.npz")
+    assert O.gnd_eff_h_clip() == float(d["gnd_eff_h_clip"])
+    assert np.array_equal(np.diag(d["j_inv"]), 1.0 / np.array([1.4e-5, 1.4e-5, 2.17e-5]))
 
 
 def test_reset_bookkeeping_matches_reference(spawn16):
