@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CH_ABI_VERSION 1
+#define CH_ABI_VERSION 2
 
 enum {
     CH_OK = 0,
@@ -46,6 +46,15 @@ enum {
 
 enum { CH_MODE_CTDE = 0, CH_MODE_MARL = 1 };
 enum { CH_PREC_F64 = 0, CH_PREC_F32 = 1 };
+/* Physics enum, in the reference's order (utils/enums.py:13-21; dispatch BaseAviary.py:420-450) */
+enum {
+    CH_PHYS_PYB = 0,          /* _physics + p.stepSimulation (default) */
+    CH_PHYS_DYN = 1,          /* explicit _dynamics + _integrateQ (BaseAviary.py:1043-1118); cattle stay put */
+    CH_PHYS_PYB_GND = 2,      /* + _groundEffect (943-980) */
+    CH_PHYS_PYB_DRAG = 3,     /* + _drag (982-1011) */
+    CH_PHYS_PYB_DW = 4,       /* + _downwash (1013-1041) */
+    CH_PHYS_PYB_GND_DRAG_DW = 5
+};
 
 /* Flags for ch_step_io.flags */
 #define CH_STEP_AUTORESET      0x1u  /* reset finished envs in the same launch (SB3 VecEnv semantics) */
@@ -79,6 +88,9 @@ typedef struct ch_config {
                                  (config/cattle_positions.yaml, 100 x 16; extended for > 16 cows) */
     int32_t spawn_scenarios;
     int32_t spawn_cows;
+    int32_t physics;          /* CH_PHYS_* (CattleAviary ctor `physics`, CattleAviary.py:21); the variants
+                                 run on the team-per-env step kernel */
+    int32_t _pad;
 } ch_config;
 
 typedef struct ch_handle ch_handle;
@@ -128,7 +140,8 @@ int ch_step(ch_handle* h, const ch_step_io* io, void* stream);
 /* Full SoA state, for checkpoint/resume and parity state-injection.  Layout of the two host
  * buffers (counts from ch_state_size):
  *   doubles: drone[22][E][N] (px py pz qx qy qz qw vx vy vz wx wy wz pid_last_rpy[3]
- *            pid_int_pos[3] pid_int_rpy[3]), cattle[4][E][M] (x y vx vy), env[2][E] (prev_cent clock)
+ *            pid_int_pos[3] pid_int_rpy[3]), cattle[4][E][M] (x y vx vy), env[2][E] (prev_cent clock),
+ *            phys[7][E][N] (last_clipped_action[4] = drag input, DYN body rates rpy_rates[3])
  *   int32:   env[10][E] (n, step_counter, step_counter_A, has_prev, level, tally, spawn_index,
  *            active_mask, episode, step_index = ch_step calls so far = the Philox action counter) */
 int ch_state_size(const ch_handle* h, int64_t* n_doubles, int64_t* n_ints);

@@ -15,7 +15,9 @@ CH_PREC_F64, CH_PREC_F32 = 0, 1
 CH_STEP_AUTORESET, CH_STEP_RANDOM_ACTIONS = 0x1, 0x2
 METRIC_NAMES = ("steps", "episodes", "return_sum", "length_sum", "terminated", "truncated", "nan_rewards",
                 "effectiveness_sum")
-ABI_VERSION = 1
+ABI_VERSION = 2
+# Physics enum (utils/enums.py:13-21, include/cattleherd.h CH_PHYS_*)
+PHYSICS = {"pyb": 0, "dyn": 1, "pyb_gnd": 2, "pyb_drag": 3, "pyb_dw": 4, "pyb_gnd_drag_dw": 5}
 
 # every symbol include/cattleherd.h declares
 EXPORTS = ("ch_default_config", "ch_create", "ch_destroy", "ch_last_error", "ch_shape", "ch_reset", "ch_step",
@@ -31,7 +33,8 @@ class ChConfig(ctypes.Structure):
                 ("compat", ctypes.c_int32), ("precision", ctypes.c_int32), ("torque_world", ctypes.c_int32),
                 ("gyro", ctypes.c_int32), ("marl_wrapper", ctypes.c_int32), ("damping", ctypes.c_double), ("seed", ctypes.c_uint64),
                 ("env_id_offset", ctypes.c_int64), ("spawn_table", ctypes.POINTER(ctypes.c_double)),
-                ("spawn_scenarios", ctypes.c_int32), ("spawn_cows", ctypes.c_int32)]
+                ("spawn_scenarios", ctypes.c_int32), ("spawn_cows", ctypes.c_int32), ("physics", ctypes.c_int32),
+                ("_pad", ctypes.c_int32)]
 
 
 class ChStepIO(ctypes.Structure):

@@ -16,6 +16,7 @@ from . import _lib as L
 
 DRONE_COMPS = 22
 CATTLE_COMPS = 4
+PHYS_COMPS = 7   # last_clipped_action[4], DYN rpy_rates[3]
 ENV_INTS = ("n", "step_counter", "step_counter_A", "has_prev", "level", "tally", "spawn_index", "active_mask",
             "episode", "step_index")
 
@@ -24,7 +25,7 @@ class HerdBatch:
     def __init__(self, n_envs, num_drones, num_cattle, mode="ctde", device=None, compat=True, precision="f64",
                  min_drones=None, max_drones=None, curriculum_level=None, seed=0x5EED, env_id_offset=0,
                  damping=0.04, torque_world=True, gyro=True, ctrl_freq=60, pyb_freq=240, spawn_table=None,
-                 marl_wrapper=True):
+                 marl_wrapper=True, physics="pyb"):
         import torch
         if not torch.cuda.is_available():
             raise RuntimeError("HerdBatch needs a ROCm GPU (torch.cuda.is_available() is False); there is no CPU "
@@ -46,6 +47,10 @@ class HerdBatch:
         cfg.marl_wrapper = int(bool(marl_wrapper))
         cfg.ctrl_freq = int(ctrl_freq)
         cfg.pyb_freq = int(pyb_freq)
+        # Physics enum by name ("pyb", "dyn", "pyb_gnd", ...), by value, or an object with .value / .name
+        if hasattr(physics, "value"):
+            physics = physics.value
+        cfg.physics = L.PHYSICS[physics.lower()] if isinstance(physics, str) else int(physics)
         self._table = None
         if spawn_table is not None:
             self._table = np.ascontiguousarray(spawn_table, np.float64)
@@ -183,9 +188,11 @@ class HerdBatch:
         nd, nc = DRONE_COMPS * E * N, CATTLE_COMPS * E * M
         dr = d[:nd].reshape(DRONE_COMPS, E, N)
         ca = d[nd:nd + nc].reshape(CATTLE_COMPS, E, M)
-        er = d[nd + nc:].reshape(2, E)
+        er = d[nd + nc:nd + nc + 2 * E].reshape(2, E)
+        ph = d[nd + nc + 2 * E:].reshape(PHYS_COMPS, E, N)
         iv = ints.reshape(len(ENV_INTS), E)
-        s = {"drone_pos": dr[0:3].transpose(1, 2, 0), "drone_quat": dr[3:7].transpose(1, 2, 0),
+        s = {"last_rpm": ph[0:4].transpose(1, 2, 0), "rpy_rates": ph[4:7].transpose(1, 2, 0),
+             "drone_pos": dr[0:3].transpose(1, 2, 0), "drone_quat": dr[3:7].transpose(1, 2, 0),
              "drone_vel": dr[7:10].transpose(1, 2, 0), "drone_angv": dr[10:13].transpose(1, 2, 0),
              "pid_last_rpy": dr[13:16].transpose(1, 2, 0), "pid_int_pos": dr[16:19].transpose(1, 2, 0),
              "pid_int_rpy": dr[19:22].transpose(1, 2, 0),
@@ -203,8 +210,12 @@ class HerdBatch:
         nd, nc = DRONE_COMPS * E * N, CATTLE_COMPS * E * M
         dr = d[:nd].reshape(DRONE_COMPS, E, N)
         ca = d[nd:nd + nc].reshape(CATTLE_COMPS, E, M)
-        er = d[nd + nc:].reshape(2, E)
+        er = d[nd + nc:nd + nc + 2 * E].reshape(2, E)
+        ph = d[nd + nc + 2 * E:].reshape(PHYS_COMPS, E, N)
         iv = ints.reshape(len(ENV_INTS), E)
+        for key, lo, hi in (("last_rpm", 0, 4), ("rpy_rates", 4, 7)):
+            if key in s:
+                ph[lo:hi] = np.asarray(s[key], np.float64)[:, :N, :].transpose(2, 0, 1)
         for key, lo, hi in (("drone_pos", 0, 3), ("drone_quat", 3, 7), ("drone_vel", 7, 10), ("drone_angv", 10, 13),
                             ("pid_last_rpy", 13, 16), ("pid_int_pos", 16, 19), ("pid_int_rpy", 19, 22)):
             if key in s:

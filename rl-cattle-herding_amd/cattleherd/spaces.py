@@ -70,13 +70,13 @@ def agent_observation_space():
 
 
 def check_supported(drone_model, physics, obs, act):
-    """The HIP path implements the reference's default configuration (CattleAviary.py:15-27)."""
+    """The HIP path implements the reference's COKIN/VEL configuration (CattleAviary.py:15-27) under every Physics."""
     def val(x):
         return getattr(x, "value", x)
     if val(drone_model) not in ("cf2x", "cf2p"):
         raise ValueError("[ERROR] in BaseRLAviary.__init()__, no controller is available for the specified drone_model")
-    if val(physics) != "pyb":
-        raise NotImplementedError(f"physics={val(physics)!r}: only Physics.PYB is on the HIP path (DESIGN.md scope)")
+    if val(physics) not in ("pyb", "dyn", "pyb_gnd", "pyb_drag", "pyb_dw", "pyb_gnd_drag_dw"):
+        raise ValueError(f"physics={val(physics)!r} is not a Physics member (utils/enums.py:13-21)")
     if val(obs) != "cokin":
         raise ValueError("[ERROR] in BaseRLAviary._observationSpace()")
     if val(act) != "vel":

@@ -24,7 +24,8 @@ class CattleHerdVecEnv(_VecEnvBase):
     def __init__(self, n_envs, num_drones=2, num_cattle=1, obs="cokin", act="vel", drone_model="cf2x",
                  physics="pyb", device=None, **batch_kw):
         check_supported(drone_model, physics, obs, act)
-        self.batch = HerdBatch(n_envs, num_drones, num_cattle, mode="ctde", device=device, **batch_kw)
+        self.batch = HerdBatch(n_envs, num_drones, num_cattle, mode="ctde", device=device, physics=physics,
+                               **batch_kw)
         self.num_envs = n_envs
         self.num_drones = num_drones
         self.observation_space = ctde_observation_space()

@@ -33,6 +33,7 @@ struct ch_handle {
     void* rpy = nullptr;
     bool rpy_valid = false;
     void* cattle = nullptr;
+    void* phys = nullptr;   // [kPhysComps][E][NC]: last_clipped_action, DYN rpy_rates
     void* envr = nullptr;
     int* envi = nullptr;
     double* metrics = nullptr;
@@ -129,6 +130,14 @@ static double cattle_spacing_cc() {
     return fr0 / std::exp(-LAM * r0);
 }
 
+// GND_EFF_H_CLIP (BaseAviary.py:163-173): 0.25 r_prop sqrt(15 MAX_RPM^2 KF c_gnd / MAX_THRUST), cf2x.urdf:5
+static double gnd_eff_h_clip() {
+    const double G = 9.8, MASS = 0.027, KF = 3.16e-10, T2W = 2.25, C = 11.36859, PR = 2.31348e-2;
+    const double max_rpm = std::sqrt((T2W * (G * MASS)) / (4 * KF));
+    const double max_thrust = 4 * KF * (max_rpm * max_rpm);
+    return 0.25 * PR * std::sqrt((15 * (max_rpm * max_rpm) * KF * C) / max_thrust);
+}
+
 template <class R>
 static StepParams<R> params(ch_handle* h) {
     StepParams<R> p{};
@@ -148,6 +157,7 @@ static StepParams<R> params(ch_handle* h) {
     p.phase_mask = h->phase_mask;
     p.G = h->G; p.P = h->P; p.pairs = h->pairs;
     p.tstamp = h->tstamp;
+    p.physics = c.physics; p.gnd_h_clip = gnd_eff_h_clip(); p.phys = (R*)h->phys;
     return p;
 }
 
@@ -190,13 +200,14 @@ int ch_default_config(ch_config* c, int32_t mode, int32_t num_drones, int32_t nu
     c->seed = 0x5EEDull;
     c->env_id_offset = 0;
     c->spawn_table = nullptr;
+    c->physics = CH_PHYS_PYB;
     return CH_OK;
 }
 
 const char* ch_last_error(const ch_handle* h) { return h ? h->err.c_str() : g_create_err.c_str(); }
 
 static void free_all(ch_handle* h) {
-    void* ptrs[] = {h->drone, h->rpy, h->cattle, h->envr, h->envi, h->metrics, h->spawn, h->pairs};
+    void* ptrs[] = {h->drone, h->rpy, h->cattle, h->phys, h->envr, h->envi, h->metrics, h->spawn, h->pairs};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
 }
@@ -206,6 +217,8 @@ int ch_create(const ch_config* c, int64_t n_envs, int32_t device, ch_handle** ou
     *out = nullptr;
     if (c->abi_version != CH_ABI_VERSION) return fail(nullptr, CH_ERR_INVALID, "ch_create: abi_version mismatch");
     if (c->mode != CH_MODE_CTDE && c->mode != CH_MODE_MARL) return fail(nullptr, CH_ERR_INVALID, "ch_create: bad mode");
+    if (c->physics < CH_PHYS_PYB || c->physics > CH_PHYS_PYB_GND_DRAG_DW)
+        return fail(nullptr, CH_ERR_INVALID, "ch_create: physics must be one of CH_PHYS_* (utils/enums.py:13-21)");
     if (n_envs <= 0 || n_envs > (1ll << 28)) return fail(nullptr, CH_ERR_INVALID, "ch_create: n_envs out of range");
     if (c->num_drones < 1 || c->num_drones > kNMax)
         return fail(nullptr, CH_ERR_INVALID, "ch_create: num_drones must be in [1, 12] (GLOBAL_MAX_NUM_DRONES)");
@@ -269,6 +282,8 @@ int ch_create(const ch_config* c, int64_t n_envs, int32_t device, ch_handle** ou
     CTRY(hipMalloc(&h->drone, h->rsize * kDroneComps * E * h->NC));
     CTRY(hipMalloc(&h->rpy, h->rsize * 3 * E * h->NC));
     CTRY(hipMalloc(&h->cattle, h->rsize * kCattleComps * E * h->M));
+    CTRY(hipMalloc(&h->phys, h->rsize * kPhysComps * E * h->NC));
+    CTRY(hipMemset(h->phys, 0, h->rsize * kPhysComps * E * h->NC));
     CTRY(hipMalloc(&h->envr, h->rsize * kEnvReal * E));
     CTRY(hipMalloc(&h->envi, sizeof(int) * kEnvInt * E));
     CTRY(hipMalloc(&h->metrics, sizeof(double) * kMetricRows * E));
@@ -315,6 +330,7 @@ int ch_create(const ch_config* c, int64_t n_envs, int32_t device, ch_handle** ou
         // team-per-env kernel (87.6 vs 92-95 us: its 496-pair alpha table per env)
         if (c->mode == CH_MODE_MARL && h->M > 16) h->kernel = 1;
         if (h->lds > budget) h->kernel = 1;   // one env's pair table alone exceeds the budget
+        if (c->physics != CH_PHYS_PYB) h->kernel = 1;   // the physics variants run on the team-per-env kernel
         std::vector<uint16_t> pl((size_t)std::max(h->P, 1));
         for (int i = 0, r = 0; i < h->M; ++i)
             for (int j = i + 1; j < h->M; ++j) pl[r++] = (uint16_t)(i | (j << 8));
@@ -431,7 +447,9 @@ int ch_step(ch_handle* h, const ch_step_io* io, void* stream) {
 
 int ch_state_size(const ch_handle* h, int64_t* n_doubles, int64_t* n_ints) {
     if (!h) return fail(nullptr, CH_ERR_INVALID, "ch_state_size: NULL handle");
-    if (n_doubles) *n_doubles = (int64_t)kDroneComps * h->E * h->NC + (int64_t)kCattleComps * h->E * h->M + kEnvReal * h->E;
+    if (n_doubles)
+        *n_doubles = (int64_t)kDroneComps * h->E * h->NC + (int64_t)kCattleComps * h->E * h->M + kEnvReal * h->E +
+                     (int64_t)kPhysComps * h->E * h->NC;
     if (n_ints) *n_ints = (int64_t)kEnvInt * h->E;
     return CH_OK;
 }
@@ -442,17 +460,19 @@ int ch_get_state(ch_handle* h, double* hd, int32_t* hi, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     HIP_TRY(h, hipStreamSynchronize(st));
     const size_t nd = (size_t)kDroneComps * h->E * h->NC, nc = (size_t)kCattleComps * h->E * h->M,
-                 nr = (size_t)kEnvReal * h->E;
+                 nr = (size_t)kEnvReal * h->E, np_ = (size_t)kPhysComps * h->E * h->NC;
     if (hd) {
         if (h->rsize == sizeof(double)) {
             HIP_TRY(h, hipMemcpy(hd, h->drone, nd * 8, hipMemcpyDeviceToHost));
             HIP_TRY(h, hipMemcpy(hd + nd, h->cattle, nc * 8, hipMemcpyDeviceToHost));
             HIP_TRY(h, hipMemcpy(hd + nd + nc, h->envr, nr * 8, hipMemcpyDeviceToHost));
+            HIP_TRY(h, hipMemcpy(hd + nd + nc + nr, h->phys, np_ * 8, hipMemcpyDeviceToHost));
         } else {
-            std::vector<float> f(nd + nc + nr);
+            std::vector<float> f(nd + nc + nr + np_);
             HIP_TRY(h, hipMemcpy(f.data(), h->drone, nd * 4, hipMemcpyDeviceToHost));
             HIP_TRY(h, hipMemcpy(f.data() + nd, h->cattle, nc * 4, hipMemcpyDeviceToHost));
             HIP_TRY(h, hipMemcpy(f.data() + nd + nc, h->envr, nr * 4, hipMemcpyDeviceToHost));
+            HIP_TRY(h, hipMemcpy(f.data() + nd + nc + nr, h->phys, np_ * 4, hipMemcpyDeviceToHost));
             for (size_t i = 0; i < f.size(); ++i) hd[i] = f[i];
         }
     }
@@ -468,17 +488,19 @@ int ch_set_state(ch_handle* h, const double* hd, const int32_t* hi, void* stream
     h->obs_zero_ptr = nullptr;   // NUM_DRONES may change: the next step writes every obs block in full
     h->rpy_valid = false;
     const size_t nd = (size_t)kDroneComps * h->E * h->NC, nc = (size_t)kCattleComps * h->E * h->M,
-                 nr = (size_t)kEnvReal * h->E;
+                 nr = (size_t)kEnvReal * h->E, np_ = (size_t)kPhysComps * h->E * h->NC;
     if (hd) {
         if (h->rsize == sizeof(double)) {
             HIP_TRY(h, hipMemcpy(h->drone, hd, nd * 8, hipMemcpyHostToDevice));
             HIP_TRY(h, hipMemcpy(h->cattle, hd + nd, nc * 8, hipMemcpyHostToDevice));
             HIP_TRY(h, hipMemcpy(h->envr, hd + nd + nc, nr * 8, hipMemcpyHostToDevice));
+            HIP_TRY(h, hipMemcpy(h->phys, hd + nd + nc + nr, np_ * 8, hipMemcpyHostToDevice));
         } else {
-            std::vector<float> f(hd, hd + nd + nc + nr);
+            std::vector<float> f(hd, hd + nd + nc + nr + np_);
             HIP_TRY(h, hipMemcpy(h->drone, f.data(), nd * 4, hipMemcpyHostToDevice));
             HIP_TRY(h, hipMemcpy(h->cattle, f.data() + nd, nc * 4, hipMemcpyHostToDevice));
             HIP_TRY(h, hipMemcpy(h->envr, f.data() + nd + nc, nr * 4, hipMemcpyHostToDevice));
+            HIP_TRY(h, hipMemcpy(h->phys, f.data() + nd + nc + nr, np_ * 4, hipMemcpyHostToDevice));
         }
     }
     if (hi) HIP_TRY(h, hipMemcpy(h->envi, hi, sizeof(int) * kEnvInt * h->E, hipMemcpyHostToDevice));
@@ -495,7 +517,7 @@ int ch__set_debug(ch_handle* h, double* dev) {
 /* Internal diagnostics: step kernel version (1 = team-per-env ch_kernels.hip, 2 = role-split ch_step.hip). */
 int ch__set_kernel(ch_handle* h, int32_t version) {
     if (!h || (version != 1 && version != 2)) return CH_ERR_INVALID;
-    if (version == 2 && h->lds > 150 * 1024) return CH_ERR_UNSUPPORTED;
+    if (version == 2 && (h->lds > 150 * 1024 || h->cfg.physics != CH_PHYS_PYB)) return CH_ERR_UNSUPPORTED;
     h->kernel = version;
     return CH_OK;
 }

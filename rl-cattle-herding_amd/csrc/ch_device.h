@@ -196,9 +196,14 @@ __device__ __forceinline__ void pid_vel(const R pos[3], const R q[4], const R ve
 }
 
 // ---- _physics (BaseAviary.py:907-939) + one p.stepSimulation substep (448): btMultiBody model ----
-template <class R>
+struct NoExtraForces {
+    template <class R> __device__ __forceinline__ void operator()(const R*, R*, R*) const {}
+};
+// `extra(M, F, Tw)` adds the physics-variant link forces (BaseAviary.py:424-445) after the motor
+// model and before gravity, in the reference's applyExternalForce order.
+template <class R, class X = NoExtraForces>
 __device__ __forceinline__ void drone_substep(R p[3], R q[4], R v[3], R w[3], const R rpm[4], R dt, R damping,
-                                              bool torque_world, bool gyro) {
+                                              bool torque_world, bool gyro, const X& extra = X()) {
     const R PX[4] = {R(0.028), R(-0.028), R(-0.028), R(0.028)}, PY[4] = {R(-0.028), R(-0.028), R(0.028), R(0.028)};
     R M[9];
     quat_to_mat(q, M);
@@ -217,6 +222,7 @@ __device__ __forceinline__ void drone_substep(R p[3], R q[4], R v[3], R w[3], co
     R tz = (-t0 + t1 - t2 + t3);
     if (torque_world) Tw[2] += tz;
     else { Tw[0] += M[2] * tz; Tw[1] += M[5] * tz; Tw[2] += M[8] * tz; }
+    extra(M, F, Tw);
     F[2] += R(-kMass * kG);
     const R k = damping;
     if (k != R(0)) {
@@ -268,6 +274,114 @@ __device__ __forceinline__ void drone_substep(R p[3], R q[4], R v[3], R w[3], co
     R n = sqrt(o[0] * o[0] + o[1] * o[1] + o[2] * o[2] + o[3] * o[3]);
 #pragma unroll
     for (int i = 0; i < 4; ++i) q[i] = divc(o[i], n);   // one reciprocal, four corrected quotients
+}
+
+// ---- physics variants (BaseAviary.py:420-450, 943-1118); cf2x.urdf:5 coefficients ----------------
+constexpr double kGndCoeff = 11.36859, kPropRadius = 2.31348e-2, kArm = 0.0397;
+constexpr double kDragXY = 9.1785e-7, kDragZ = 10.311e-7;
+constexpr double kDw1 = 2267.18, kDw2 = .16, kDw3 = -.11;
+
+// _groundEffect (943-980): per-prop thrust boost below the clip height, skipped when tilted past 90 deg;
+// each force is applied at its prop link (LINK_FRAME +z) so it also adds a torque about the COM.
+template <class R>
+__device__ __forceinline__ void ground_effect(const R p[3], const R q[4], const R M[9], const R rpm[4], R h_clip,
+                                              R F[3], R Tw[3]) {
+    const R PX[4] = {R(0.028), R(-0.028), R(-0.028), R(0.028)}, PY[4] = {R(-0.028), R(-0.028), R(0.028), R(0.028)};
+    R rpy[3];
+    quat_to_euler(q, rpy);
+    if (!(fabs(rpy[0]) < R(kPi / 2) && fabs(rpy[1]) < R(kPi / 2))) return;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        R h = p[2] + (M[6] * PX[i] + M[7] * PY[i]);   // prop link COM height
+        if (h < h_clip) h = h_clip;
+        const R r = R(kPropRadius) / (R(4) * h);
+        const R g = rpm[i] * rpm[i] * R(kKF) * R(kGndCoeff) * (r * r);
+        const R fw[3] = {M[2] * g, M[5] * g, M[8] * g};
+        const R rw[3] = {M[0] * PX[i] + M[1] * PY[i], M[3] * PX[i] + M[4] * PY[i], M[6] * PX[i] + M[7] * PY[i]};
+        F[0] += fw[0]; F[1] += fw[1]; F[2] += fw[2];
+        Tw[0] += rw[1] * fw[2] - rw[2] * fw[1];
+        Tw[1] += rw[2] * fw[0] - rw[0] * fw[2];
+        Tw[2] += rw[0] * fw[1] - rw[1] * fw[0];
+    }
+}
+
+// _drag (982-1011): rotor drag from the previous substep's rpm (last_clipped_action), in the body
+// frame, applied at the COM link
+template <class R>
+__device__ __forceinline__ void rotor_drag(const R v[3], const R M[9], const R last_rpm[4], R F[3]) {
+    R sum = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sum += (R(2 * kPi) * last_rpm[i]) / R(60);
+    const R dv[3] = {(R(-kDragXY) * sum) * v[0], (R(-kDragXY) * sum) * v[1], (R(-kDragZ) * sum) * v[2]};
+    R b[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) b[k] = M[0 + k] * dv[0] + M[3 + k] * dv[1] + M[6 + k] * dv[2];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) F[k] += M[3 * k + 0] * b[0] + M[3 * k + 1] * b[1] + M[3 * k + 2] * b[2];
+}
+
+// _downwash (1013-1041): one term per drone above (dz > 0) within 10 m horizontally; `o` is that
+// drone's position at the start of the substep
+template <class R>
+__device__ __forceinline__ void downwash_term(const R me[3], const R o[3], const R M[9], R F[3]) {
+    const R dz = o[2] - me[2];
+    const R ex = o[0] - me[0], ey = o[1] - me[1];
+    const R dxy = sqrt(ex * ex + ey * ey);
+    if (dz > R(0) && dxy < R(10)) {
+        const R r = R(kPropRadius) / (R(4) * dz);
+        const R alpha = R(kDw1) * (r * r);
+        const R beta = R(kDw2) * dz + R(kDw3);
+        const R u = dxy / beta;
+        const R fz = -alpha * m_exp(R(-.5) * (u * u));
+        F[0] += M[2] * fz; F[1] += M[5] * fz; F[2] += M[8] * fz;
+    }
+}
+
+// Physics.DYN: _dynamics (1043-1102) + _integrateQ (1104-1118).  Explicit Euler on the body rates rr
+// (persistent rpy_rates); the stored angular velocity is rotation(old quat) @ rr.
+template <class R>
+__device__ __forceinline__ void dyn_substep(R p[3], R q[4], R v[3], R w[3], R rr[3], const R rpm[4], R dt) {
+    R M[9];
+    quat_to_mat(q, M);
+    R f[4], z[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { f[i] = rpm[i] * rpm[i] * R(kKF); z[i] = rpm[i] * rpm[i] * R(kKM); }
+    const R T = f[0] + f[1] + f[2] + f[3];
+    const R fw[3] = {M[2] * T, M[5] * T, M[8] * T - R(kG * kMass)};
+    const R zt = -z[0] + z[1] - z[2] + z[3];
+    const R ls = R(kArm) / sqrt(R(2));
+    const R xt = (f[0] + f[1] - f[2] - f[3]) * ls, yt = (-f[0] + f[1] + f[2] - f[3]) * ls;
+    const R J[3] = {R(kJx), R(kJy), R(kJz)};
+    const R Jr[3] = {J[0] * rr[0], J[1] * rr[1], J[2] * rr[2]};
+    const R c[3] = {rr[1] * Jr[2] - rr[2] * Jr[1], rr[2] * Jr[0] - rr[0] * Jr[2], rr[0] * Jr[1] - rr[1] * Jr[0]};
+    const R tq[3] = {xt - c[0], yt - c[1], zt - c[2]};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        v[i] = v[i] + dt * (fw[i] / R(kMass));
+        rr[i] = rr[i] + dt * ((R(1) / J[i]) * tq[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) p[i] = p[i] + dt * v[i];
+    const R on = sqrt(rr[0] * rr[0] + rr[1] * rr[1] + rr[2] * rr[2]);
+    if (!(fabs(on) <= R(1e-8))) {   // np.isclose(omega_norm, 0): atol 1e-8
+        R si, co;
+        m_sincos(on * dt / R(2), &si, &co);
+        const R k = R(2) / on;
+        const R P = rr[0], Q = rr[1], Z = rr[2];
+        const R L[4][4] = {{0, Z, -Q, P}, {-Z, 0, P, Q}, {Q, -P, 0, Z}, {-P, -Q, -Z, 0}};
+        R o[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            R m[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) m[j] = (i == j ? co : R(0)) + (k * (L[i][j] * R(.5))) * si;
+            o[i] = m[0] * q[0] + m[1] * q[1] + m[2] * q[2] + m[3] * q[3];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) q[i] = o[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) w[i] = M[3 * i + 0] * rr[0] + M[3 * i + 1] * rr[1] + M[3 * i + 2] * rr[2];
 }
 
 // ---- flocking: MathematicalFlock (flockUtils.py:11-382) ----------------------------------------

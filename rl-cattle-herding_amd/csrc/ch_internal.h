@@ -11,6 +11,7 @@ constexpr int kNMax = 12;          // GLOBAL_MAX_NUM_DRONES (BaseAviary.py:112)
 constexpr int kMMax = 64;          // cattle per env supported by the team mapping (TEAM <= 64)
 constexpr int kDroneComps = 22;    // px py pz qx qy qz qw vx vy vz wx wy wz pid[9]
 constexpr int kCattleComps = 4;    // x y vx vy
+constexpr int kPhysComps = 7;      // last_clipped_action[4] (drag input), DYN rpy_rates[3]
 constexpr int kEnvReal = 2;        // prev_cent, clock
 constexpr int kEnvInt = 10;        // n sc scA has_prev level tally spawn active episode step_index
 constexpr int kMetricCurReturn = CH_METRIC_COUNT;      // running episode return
@@ -51,6 +52,9 @@ struct StepParams {
     int G, P;                 // v2: envs per workgroup, cow pairs per env
     const uint16_t* pairs;    // v2: [P] unordered cow pairs (i | j << 8) in tri() order
     long long* tstamp;        // diagnostics only: [grid][16] per-workgroup phase timestamps (ch__set_tstamp)
+    int physics;              // CH_PHYS_* (v1 kernel only; ch_api.cpp selects v1 for the variants)
+    double gnd_h_clip;        // GND_EFF_H_CLIP (BaseAviary.py:173)
+    R* phys;                  // [kPhysComps][E][NC]
 };
 
 // one curriculum level (curriculum_learning.py:10-194); the table kLevels lives in ch_device.h

@@ -108,6 +108,11 @@ __device__ __forceinline__ void reset_env(const StepParams<R>& p, Slot<R, TEAM>&
     if (t < p.NC) {
         R x, y, z;
         reset_drone(p, (long long)e * p.NC + t, t, n_new, x, y, z);
+        if (p.physics != CH_PHYS_PYB) {   // last_clipped_action, rpy_rates = 0 (_housekeeping, BaseAviary.py:565, 581-582)
+            const long long DS = (long long)p.E * p.NC;
+#pragma unroll
+            for (int c = 0; c < kPhysComps; ++c) p.phys[c * DS + (long long)e * p.NC + t] = R(0);
+        }
         S.dx[t] = x; S.dy[t] = y;
         *own_z = z;
     }
@@ -118,7 +123,51 @@ __device__ __forceinline__ void reset_env(const StepParams<R>& p, Slot<R, TEAM>&
     }
 }
 
-template <class R, int TEAM, bool RESET_ONLY, int MODE>
+// Physics variants (BaseAviary.py:420-450) for the drone on this lane: `base` is lane 0 of the env's
+// team, n its live drones.  The downwash term reads the other drones' substep-start positions by
+// cross-lane shuffle (every lane of the branch joins each shuffle: the loop bound p.NC is uniform).
+template <class R>
+__device__ __forceinline__ void variant_substeps(const StepParams<R>& p, long long di, int base, int n, R pos[3],
+                                                 R q[4], R v[3], R w[3], const R rpm[4]) {
+    const long long DS = (long long)p.E * p.NC;
+    R lr[4], rr[3];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) lr[c] = p.phys[c * DS + di];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) rr[c] = p.phys[(4 + c) * DS + di];
+    const int ph = p.physics;
+    const bool gnd = ph == CH_PHYS_PYB_GND || ph == CH_PHYS_PYB_GND_DRAG_DW;
+    const bool drag = ph == CH_PHYS_PYB_DRAG || ph == CH_PHYS_PYB_GND_DRAG_DW;
+    const bool dw = ph == CH_PHYS_PYB_DW || ph == CH_PHYS_PYB_GND_DRAG_DW;
+    const R h_clip = R(p.gnd_h_clip);
+    for (int s = 0; s < p.substeps; ++s) {
+        if (ph == CH_PHYS_DYN) {
+            dyn_substep(pos, q, v, w, rr, rpm, R(p.dt));
+        } else {
+            // extra() runs before drone_substep moves the body: pos/q/v are the substep-start state
+            auto extra = [&](const R* M, R* F, R* Tw) {
+                if (gnd) ground_effect(pos, q, M, rpm, h_clip, F, Tw);
+                if (drag) rotor_drag(v, M, lr, F);
+                if (dw) {
+                    for (int i = 0; i < p.NC; ++i) {
+                        const R o[3] = {__shfl(pos[0], base + i, 64), __shfl(pos[1], base + i, 64),
+                                        __shfl(pos[2], base + i, 64)};
+                        if (i < n) downwash_term(pos, o, M, F);
+                    }
+                }
+            };
+            drone_substep(pos, q, v, w, rpm, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0, extra);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) lr[c] = rpm[c];   // last_clipped_action (BaseAviary.py:450)
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) p.phys[c * DS + di] = lr[c];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) p.phys[(4 + c) * DS + di] = rr[c];
+}
+
+template <class R, int TEAM, bool RESET_ONLY, int MODE, bool PHYS = false>
 __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
     constexpr int EPB = 64 / TEAM;
     __shared__ Slot<R, TEAM> slots[EPB];
@@ -184,8 +233,12 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
             R rpm[4];
             if (!(p.phase_mask & 1)) {
                 pid_vel(pos, q, v, Rm, rpy, a, R(p.dt_ctrl), pid, rpm, p.debug ? p.debug + di * 16 : nullptr);
-                for (int s = 0; s < p.substeps; ++s)
-                    drone_substep(pos, q, v, w, rpm, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0);
+                if constexpr (PHYS) {
+                    variant_substeps(p, di, slot * TEAM, n, pos, q, v, w, rpm);
+                } else {
+                    for (int s = 0; s < p.substeps; ++s)
+                        drone_substep(pos, q, v, w, rpm, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0);
+                }
             }
             R* D = p.drone;
             D[0 * DS + di] = pos[0]; D[1 * DS + di] = pos[1]; D[2 * DS + di] = pos[2];
@@ -207,7 +260,9 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
             R x = ld(p.cattle, 0, CS, ci), y = ld(p.cattle, 1, CS, ci);
             cvx = ld(p.cattle, 2, CS, ci); cvy = ld(p.cattle, 3, CS, ci);
             const R dt = R(p.dt);
-            for (int s = 0; s < p.substeps; ++s) { x += cvx * dt; y += cvy * dt; }
+            // no p.stepSimulation under Physics.DYN: the cattle bodies keep their positions (BaseAviary.py:447-448)
+            if (!PHYS || p.physics != CH_PHYS_DYN)
+                for (int s = 0; s < p.substeps; ++s) { x += cvx * dt; y += cvy * dt; }
             p.cattle[0 * CS + ci] = x; p.cattle[1 * CS + ci] = y;
             S.cx[t] = x; S.cy[t] = y; S.cvx[t] = cvx; S.cvy[t] = cvy;
         }
@@ -536,6 +591,16 @@ template <class R, bool RESET_ONLY, int MODE>
 static void launch_mode(const StepParams<R>& p, int team, hipStream_t st) {
     int epb = 64 / team;
     dim3 grid((p.E + epb - 1) / epb), block(64);
+    if constexpr (!RESET_ONLY) {
+        if (p.physics != CH_PHYS_PYB) {   // variant instantiations (BaseAviary.py:420-450)
+            switch (team) {
+                case 16: hipLaunchKernelGGL((k_env<R, 16, false, MODE, true>), grid, block, 0, st, p); break;
+                case 32: hipLaunchKernelGGL((k_env<R, 32, false, MODE, true>), grid, block, 0, st, p); break;
+                default: hipLaunchKernelGGL((k_env<R, 64, false, MODE, true>), grid, block, 0, st, p); break;
+            }
+            return;
+        }
+    }
     switch (team) {
         case 16: hipLaunchKernelGGL((k_env<R, 16, RESET_ONLY, MODE>), grid, block, 0, st, p); break;
         case 32: hipLaunchKernelGGL((k_env<R, 32, RESET_ONLY, MODE>), grid, block, 0, st, p); break;

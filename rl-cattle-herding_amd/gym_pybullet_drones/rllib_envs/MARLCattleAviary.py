@@ -37,7 +37,7 @@ class MARLCattleAviary:
         self.batch = HerdBatch(1, num_drones, num_cattle, mode="marl", device=device, compat=compat,
                                precision=precision, min_drones=self.MIN_NUM_DRONES, max_drones=self.MAX_NUM_DRONES,
                                curriculum_level=curriculum_level, seed=seed, env_id_offset=env_id,
-                               ctrl_freq=ctrl_freq, pyb_freq=pyb_freq, marl_wrapper=_wrapper_semantics)
+                               ctrl_freq=ctrl_freq, pyb_freq=pyb_freq, physics=physics, marl_wrapper=_wrapper_semantics)
         self._num_drones_ctor = num_drones
         self.NUM_DRONES = min(self.MAX_NUM_DRONES, num_drones)
         self.action_space = agent_action_space()

@@ -54,7 +54,7 @@ class CattleAviary(_EnvBase):
         self.batch = HerdBatch(1, num_drones, num_cattle, mode="ctde", device=device, compat=compat,
                                precision=precision, min_drones=self.MIN_NUM_DRONES, max_drones=self.MAX_NUM_DRONES,
                                curriculum_level=curriculum_level, seed=seed, env_id_offset=env_id,
-                               ctrl_freq=ctrl_freq, pyb_freq=pyb_freq)
+                               ctrl_freq=ctrl_freq, pyb_freq=pyb_freq, physics=physics)
         self._num_drones_ctor = num_drones
         self.NUM_DRONES = num_drones
         self.action_space = ctde_action_space(num_drones)

@@ -21,15 +21,16 @@ class FakeBatch:
     def __init__(self, n_envs, num_drones, num_cattle, mode="ctde", device=None, compat=True, precision="f64",
                  min_drones=None, max_drones=None, curriculum_level=None, seed=0x5EED, env_id_offset=0,
                  damping=0.04, torque_world=True, gyro=True, ctrl_freq=60, pyb_freq=240, spawn_table=None,
-                 marl_wrapper=True):
-        from cattleherd._lib import spawn_table as st
+                 marl_wrapper=True, physics="pyb"):
+        from cattleherd._lib import PHYSICS, spawn_table as st
         self.torch = torch
         self.device = torch.device("cpu")
         self.mode = 0 if mode == "ctde" else 1
         table = st(num_cattle) if spawn_table is None else spawn_table
         self.envs = [O.Env(self.mode, num_drones, num_cattle, table, min_drones=min_drones, max_drones=max_drones,
                            start_level=curriculum_level, compat=compat, seed=seed, env_id=env_id_offset + e,
-                           ctrl_freq=ctrl_freq, pyb_freq=pyb_freq, marl_wrapper=marl_wrapper)
+                           ctrl_freq=ctrl_freq, pyb_freq=pyb_freq, marl_wrapper=marl_wrapper,
+                           physics=PHYSICS[getattr(physics, "value", physics)])
                      for e in range(n_envs)]
         self.cfg = _Cfg(ctrl_freq, curriculum_level)
         self.n_envs, self.num_drones, self.num_cattle = n_envs, num_drones, num_cattle

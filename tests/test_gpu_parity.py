@@ -37,7 +37,8 @@ def test_rollout_fixture_parity(fname):
     T = len(d["action"])
     states = [state_at(d, "state_", t) for t in range(T)]
     n, m, lvl = int(states[0]["n"]), int(states[0]["m"]), int(states[0]["ctor_level"])
-    b = _batch(mode, n, m, T, lvl)
+    physics = int(d["physics"]) if "physics" in d.files else 0   # Physics enum (BaseAviary.py:420-450)
+    b = _batch(mode, n, m, T, lvl, physics=physics)
     b.reset()
     _inject(b, states)
     acts = torch.tensor(d["action"], device=b.device)
@@ -59,6 +60,9 @@ def test_rollout_fixture_parity(fname):
     nxt = stack([states[t + 1] for t in idx])
     for k in ("drone_pos", "drone_quat", "drone_vel", "drone_angv", "pid_int_rpy", "pid_int_pos", "pid_last_rpy"):
         assert close(g[k][idx, :n], nxt[k][:, :n], 1e-9, 1e-12)[0], k
+    if physics:
+        assert close(g["last_rpm"][idx, :n], nxt["last_rpm"][:, :n], 1e-9, 1e-9)[0]
+        assert close(g["rpy_rates"][idx, :n], nxt["rpy_rates"][:, :n], 1e-9, 1e-12)[0]
     assert close(g["cow_pos"][idx, :m], nxt["cow_pos"][:, :m], 1e-12, 1e-13)[0]
     assert close(g["cow_vel"][idx, :m], nxt["cow_vel"][:, :m], 1e-12, 1e-14)[0]
     for k in ("step_counter", "step_counter_A", "level", "tally"):
@@ -66,13 +70,13 @@ def test_rollout_fixture_parity(fname):
     b.close()
 
 
-def _oracle_states(mode, n, m, E, table, steps, seed, level, compat=True):
+def _oracle_states(mode, n, m, E, table, steps, seed, level, compat=True, physics=0):
     """E oracle envs, each advanced a different number of random steps (diverse states)."""
     import oracle as O
     envs, states = [], []
     rng = np.random.default_rng(seed)
     for e in range(E):
-        env = O.Env(mode, n, m, table, start_level=level, env_id=e, compat=compat)
+        env = O.Env(mode, n, m, table, start_level=level, env_id=e, compat=compat, physics=physics)
         env.reset()
         for t in range(int(rng.integers(0, steps))):
             env.step(rng.uniform(-1, 1, (n, 4)).astype(np.float32), autoreset=True)
@@ -154,6 +158,111 @@ def test_random_rollout_with_autoreset_vs_oracle(mode, n, m):
     assert close(st["cow_pos"], want["cow_pos"][:, :m], 1e-7, 1e-8)[0]
     ok, err = close(st["drone_pos"][:, :n], want["drone_pos"][:, :n], 1e-3, 1e-3)
     assert ok, err
+    b.close()
+
+
+PHYSICS_CASES = [(1, 0, 4, 16), (2, 0, 4, 16), (3, 0, 4, 16), (4, 0, 6, 8), (5, 0, 4, 16), (5, 1, 4, 16),
+                 (1, 1, 3, 8), (5, 0, 12, 16)]
+
+
+@pytest.mark.parametrize("physics,mode,n,m", PHYSICS_CASES)
+def test_physics_variant_step_vs_oracle(physics, mode, n, m):
+    """Physics variants (DYN 1, PYB_GND 2, PYB_DRAG 3, PYB_DW 4, PYB_GND_DRAG_DW 5;
+    BaseAviary.py:420-450, 943-1118): one launch over E diverse oracle states, including the
+    carried last_clipped_action and DYN body rates, vs the oracle stepping each state."""
+    import torch
+    from cattleherd._lib import spawn_table
+    table = spawn_table(m)
+    E = 48
+    level = 7 if mode == 0 else 0
+    envs, states = _oracle_states(mode, n, m, E, table, 160, seed=physics * 1000 + n * 100 + m, level=level,
+                                  physics=physics)
+    b = _batch(mode, n, m, E, level, physics=physics)
+    b.reset()
+    b.set_state(stack([{k: v for k, v in s.items() if k != "episode"} for s in states]))
+    rng = np.random.default_rng(11)
+    acts = rng.uniform(-1, 1, (E, n, 4)).astype(np.float32)
+    obs, rew, te, tr = b.step(torch.tensor(acts, device=b.device), autoreset=False)
+    torch.cuda.synchronize()
+    ref = [env.step(acts[e], autoreset=False) for e, env in enumerate(envs)]
+    R, K = b.obs_rows, b.reward_cols
+    assert close(obs.cpu().numpy(), np.stack([r[0] for r in ref]).reshape(E, R, 86), 1e-6, 1e-7)[0]
+    assert close(rew.cpu().numpy(), np.stack([r[1] for r in ref]).reshape(E, K).astype(np.float32), 1e-6, 1e-6)[0]
+    assert np.array_equal(te.cpu().numpy(), np.stack([r[2] for r in ref]).reshape(E, K))
+    assert np.array_equal(tr.cpu().numpy(), np.stack([r[3] for r in ref]).reshape(E, K))
+    g = b.get_state()
+    want = stack([env.get_state() for env in envs])
+    for k in ("drone_pos", "drone_quat", "drone_vel", "drone_angv", "pid_int_rpy", "pid_int_pos", "pid_last_rpy",
+              "rpy_rates"):
+        assert close(g[k][:, :n], want[k][:, :n], 1e-9, 1e-12)[0], k
+    assert close(g["last_rpm"][:, :n], want["last_rpm"][:, :n], 1e-12, 1e-9)[0]
+    assert close(g["cow_pos"], want["cow_pos"][:, :m], 1e-12, 1e-13)[0]
+    assert close(g["cow_vel"], want["cow_vel"][:, :m], 1e-12, 1e-14)[0]
+    b.close()
+
+
+def _oracle_view(g, e, nmax):
+    """Env e of a HerdBatch.get_state() dict in the oracle's NMAX-padded layout."""
+    out = {}
+    for k, v in g.items():
+        x = np.asarray(v[e])
+        if k in ("drone_pos", "drone_quat", "drone_vel", "drone_angv", "pid_last_rpy", "pid_int_pos", "pid_int_rpy",
+                 "last_rpm", "rpy_rates", "active"):
+            pad = np.zeros((nmax,) + x.shape[1:], x.dtype)
+            pad[:x.shape[0]] = x
+            if k == "drone_quat":
+                pad[x.shape[0]:, 3] = 1
+            x = pad
+        out[k] = x
+    return out
+
+
+@pytest.mark.parametrize("physics", [1, 5])
+def test_physics_variant_rollout_with_autoreset_vs_oracle(physics):
+    """240 lockstep steps of device Philox actions with in-kernel auto-reset under DYN and
+    PYB_GND_DRAG_DW: before every step the oracle envs take the device state (so 1-ulp ocml/glibc
+    differences cannot grow through the closed loop), then both step; actions, flags and reset timing
+    exact, obs / reward / state to the per-step tolerances, the carried variant state zeroed on reset."""
+    import torch
+    import oracle as O
+    from cattleherd._lib import spawn_table
+    n, m, E, T = 4, 16, 16, 240
+    table = spawn_table(m)
+    b = _batch(0, n, m, E, None, physics=physics)
+    b.reset()
+    envs = [O.Env(0, n, m, table, env_id=e, physics=physics) for e in range(E)]
+    o0 = np.stack([env.reset() for env in envs])
+    assert close(b.obs.cpu().numpy(), o0, 1e-6, 1e-7)[0]
+    resets = 0
+    for t in range(T):
+        g = b.get_state()
+        for e, env in enumerate(envs):
+            env.set_state(_oracle_view(g, e, O.NMAX))
+        b.step(random_actions=True, autoreset=True)
+        torch.cuda.synchronize()
+        acts = b.actions.cpu().numpy()
+        ref = []
+        for e, env in enumerate(envs):
+            a = env.random_actions(t)
+            assert np.array_equal(a, acts[e]), (t, e)
+            ref.append(env.step(a, autoreset=True))
+        assert close(b.obs.cpu().numpy(), np.stack([r[0] for r in ref]), 1e-6, 1e-7)[0], t
+        assert close(b.reward.cpu().numpy()[:, 0], np.array([r[1][0] for r in ref], np.float32), 1e-6, 1e-6)[0], t
+        assert np.array_equal(b.terminated.cpu().numpy()[:, 0], np.array([r[2][0] for r in ref])), t
+        assert np.array_equal(b.truncated.cpu().numpy()[:, 0], np.array([r[3][0] for r in ref])), t
+        dn = np.array([bool(r[4]) for r in ref])
+        assert np.array_equal(b.reset_happened.cpu().numpy().astype(bool), dn), t
+        resets += int(dn.sum())
+        if dn.any():
+            st = b.get_state()
+            assert np.all(st["last_rpm"][dn] == 0) and np.all(st["rpy_rates"][dn] == 0)
+    st = b.get_state()
+    want = stack([env.get_state() for env in envs])
+    assert resets > 0
+    assert np.array_equal(st["episode"], want["episode"])
+    for k in ("drone_pos", "drone_quat", "drone_vel", "last_rpm", "rpy_rates"):
+        assert close(st[k][:, :n], want[k][:, :n], 1e-9, 1e-9)[0], k
+    assert close(st["cow_pos"], want["cow_pos"][:, :m], 1e-12, 1e-13)[0]
     b.close()
 
 
