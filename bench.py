@@ -137,6 +137,8 @@ def main():
     ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
     ap.add_argument("--envs", type=int, default=None, help="override envs per GPU")
     ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
+    ap.add_argument("--physics", default="pyb", choices=["pyb", "dyn", "pyb_gnd", "pyb_drag", "pyb_dw", "pyb_gnd_drag_dw"],
+                    help="Physics variant (BaseAviary.py:420-450); the headline is the reference default pyb")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--policy", action="store_true",
@@ -157,7 +159,8 @@ def main():
     mode, E, n, m, desc = WORKLOADS[args.workload]
     if args.envs:
         E = args.envs
-    b = HerdBatch(E, n, m, mode=mode, precision=args.precision, env_id_offset=D.env_offset(rank, E))
+    b = HerdBatch(E, n, m, mode=mode, precision=args.precision, env_id_offset=D.env_offset(rank, E),
+                  physics=args.physics)
     b.reset()
     stream = torch.cuda.current_stream()
     for _ in range(args.warmup):
@@ -203,8 +206,11 @@ def main():
     kern_us = s_ev.elapsed_time(e_ev) / nk * 1000.0
     rb = 8 if args.precision == "f64" else 4
     bytes_step = algorithmic_bytes(mode, n, m, b.obs_rows, rb)
+    if args.physics != "pyb":
+        bytes_step += 2 * 7 * rb * n   # carried last_clipped_action + rpy_rates, read and written
     achieved = bytes_step * E / (kern_us * 1e-6) / 1e9
-    traffic, traffic_src = pmc_traffic(args.workload, args.precision) if E == WORKLOADS[args.workload][1] else (None, None)
+    traffic, traffic_src = (pmc_traffic(args.workload, args.precision)
+                            if E == WORKLOADS[args.workload][1] and args.physics == "pyb" else (None, None))
     kname = kernel_name(b)
 
     out = None
@@ -218,6 +224,7 @@ def main():
             "data": "synthetic: Philox4x32 random VEL actions in-kernel, spawn table from config/cattle_positions.yaml",
             "launch": f"HIP graph of {chunk} steps per replay" if graph is not None else "one host launch per step",
             "config": {"workload": desc, "envs_per_gpu": E, "num_drones": n, "num_cattle": m, "mode": mode,
+                       "physics": args.physics,
                        "parallelism": f"env-sharded x{world} (no per-step collective)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
