@@ -69,3 +69,21 @@ def test_invalid_configs_rejected():
     assert b"pyb_freq is not divisible" in L.ch_last_error(None)
     c = _lib.default_config(0, 1, 4)
     assert L.ch_create(ctypes.byref(c), 8, 0, ctypes.byref(h)) == _lib.CH_ERR_UNSUPPORTED
+
+
+def test_physics_field_default_and_range():
+    """ch_config.physics (CH_PHYS_*, utils/enums.py:13-21): PYB by default, out-of-range rejected
+    before any device call."""
+    from cattleherd import _lib
+    L = _lib.lib()
+    c = _lib.ChConfig()
+    c.physics = 7
+    assert L.ch_default_config(ctypes.byref(c), 0, 4, 16) == 0
+    assert c.physics == _lib.PHYSICS["pyb"] == 0
+    assert _lib.ChConfig.physics.offset == _lib.ChConfig.spawn_cows.offset + 4
+    assert ctypes.sizeof(_lib.ChConfig) % 8 == 0
+    h = ctypes.c_void_p()
+    for bad in (-1, 6):
+        c.physics = bad
+        assert L.ch_create(ctypes.byref(c), 8, 0, ctypes.byref(h)) == _lib.CH_ERR_INVALID
+        assert b"physics" in L.ch_last_error(None)

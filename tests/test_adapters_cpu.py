@@ -96,3 +96,22 @@ def test_vec_env_autoreset_infos(patched):
             assert "TimeLimit.truncated" in infos[e]
     assert saw_done
     assert venv.get_attr("EPISODE_LEN_SEC") == [80] * 4 and venv.env_is_wrapped(object) == [False] * 4
+
+
+def test_physics_argument_reaches_the_batch(patched):
+    """CattleAviary(physics=Physics.DYN) selects the explicit model (BaseAviary.py:1043-1118): no
+    p.stepSimulation, so the cattle keep their positions; PYB moves them at their velocity."""
+    ca, _, ve = patched
+    from cattleherd.spaces import Physics
+    moved = {}
+    for ph in (Physics.DYN, Physics.PYB):
+        env = ca.CattleAviary(num_drones=4, num_cattle=8, physics=ph)
+        env.reset()
+        p0 = env.batch.get_state()["cow_pos"].copy()
+        env.step(np.zeros((4, 4), np.float32))
+        moved[ph] = float(np.abs(env.batch.get_state()["cow_pos"] - p0).max())
+    assert moved[Physics.DYN] == 0.0 and moved[Physics.PYB] > 0.0
+    venv = ve.CattleHerdVecEnv(2, num_drones=4, num_cattle=8, physics="pyb_gnd_drag_dw")
+    assert venv.reset().shape == (2, 12, 86)
+    with pytest.raises(ValueError):
+        ca.CattleAviary(num_drones=4, num_cattle=8, physics="rk4")

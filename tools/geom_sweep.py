@@ -29,6 +29,9 @@ def main():
     configs = [("ctde", 4096, 4, 16), ("ctde", 4096, 2, 8), ("ctde", 1024, 2, 8), ("marl", 4096, 4, 32),
                ("ctde", 4096, 12, 16)]
     precs = sys.argv[1:] or ["f64"]
+    if len(sys.argv) >= 5:   # one config: mode E n m [prec]
+        configs = [(sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]))]
+        precs = sys.argv[5:] or ["f64"]
     for prec in precs:
         for mode, E, n, m in configs:
             b = HerdBatch(E, n, m, mode=mode, precision=prec)
@@ -39,8 +42,8 @@ def main():
             L.ch__set_kernel(b.handle, ctypes.c_int32(1))
             row.append(f"v1={time_launches(b):.1f}")
             L.ch__set_kernel(b.handle, ctypes.c_int32(2))
-            for G in (1, 2, 4, 8, 16, 32):
-                for B in (64, 128, 256):
+            for G in (1, 2, 3, 4, 8, 16, 32):
+                for B in (128, 192, 256, 320, 384, 512):
                     if L.ch__set_geometry(b.handle, ctypes.c_int32(G), ctypes.c_int32(B)) != 0:
                         continue
                     row.append(f"G{G}/B{B}={time_launches(b):.1f}")

@@ -26,8 +26,12 @@ def time_launches(b, k=200):
 def main():
     import ctypes
     configs = [("ctde", 4096, 4, 16), ("ctde", 4096, 2, 8), ("marl", 4096, 4, 32), ("ctde", 1024, 2, 8)]
+    precs = ("f64", "f32")
+    if len(sys.argv) >= 5:   # one config: mode E n m [prec]
+        configs = [(sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]))]
+        precs = tuple(sys.argv[5:]) or precs
     masks = [(0, "full"), (1, "-drones"), (2, "-flock"), (4, "-task"), (8, "-obs"), (1 | 2 | 4 | 8, "loads/stores only")]
-    for prec in ("f64", "f32"):
+    for prec in precs:
         for mode, E, n, m in configs:
             for kern in (1, 2):
                 b = HerdBatch(E, n, m, mode=mode, precision=prec)
