@@ -49,16 +49,38 @@ def algorithmic_bytes(mode, n, m, rows, real_bytes):
     return drone + actions + cattle + env + metrics + obs + flags
 
 
-def pmc_traffic(workload, dtype):
-    """HBM bytes per launch of the step kernel from the newest committed rocprofv3 --pmc pass
-    (profiles/rNN/traffic_<workload>_<dtype>.json, written by tools/parse_pmc.py), or None."""
+def pmc_record(workload, dtype):
+    """The newest committed rocprofv3 --pmc record of the step kernel
+    (profiles/rNN/traffic_<workload>_<dtype>.json, written by tools/parse_pmc.py), or ({}, None)."""
     import glob
     hits = sorted(glob.glob(os.path.join(PROFILES, "r*", f"traffic_{workload}_{dtype}.json")))
     if not hits:
-        return None, None
+        return {}, None
     with open(hits[-1]) as fh:
-        d = json.load(fh)
-    return d.get("traffic_bytes_per_launch"), os.path.relpath(hits[-1], ROOT)
+        return json.load(fh), os.path.relpath(hits[-1], ROOT)
+
+
+def pmc_traffic(workload, dtype):
+    """HBM bytes per launch of the step kernel from the newest committed PMC record, or None."""
+    d, src = pmc_record(workload, dtype)
+    return d.get("traffic_bytes_per_launch"), src
+
+
+def valu_issue(workload, dtype, kern_us):
+    """Compute-side view of the same kernel: fp64/fp32 VALU wave-instructions per launch (PMC
+    SQ_INSTS_VALU) priced at their issue cost on a SIMD-32 (wave64: 4 cycles fp64, 2 fp32; the
+    MI355X guide's constants table) over all SIMDs (256 CUs x 4) at 2.4 GHz for this launch time."""
+    d, src = pmc_record(workload, dtype)
+    if "sq_insts_valu" not in d:
+        return None
+    cyc = 4 if dtype == "f64" else 2
+    simd_cycles = 256 * 4 * kern_us * 1e-6 * 2.4e9
+    return {"valu_insts_per_launch": d["sq_insts_valu"], "salu_insts_per_launch": d.get("sq_insts_salu"),
+            "issue_cycles_per_inst": cyc, "issue_frac": d["sq_insts_valu"] * cyc / simd_cycles,
+            "active_frac": (d["sq_active_inst_valu"] * 4 / simd_cycles) if "sq_active_inst_valu" in d else None,
+            "source": src,
+            "note": "issue_frac = VALU issue cycles / SIMD cycles (upper bound: counts every VALU op at the "
+                    "wide rate); active_frac from SQ_ACTIVE_INST_VALU (quad-cycles, summed over waves)"}
 
 
 def kernel_name(b):
@@ -230,6 +252,8 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_src, "algorithmic_bytes_per_launch": bytes_step * E,
                          "kernel": kname, "kernel_us": kern_us, "bytes_per_env_step": bytes_step},
+            "valu": (valu_issue(args.workload, args.precision, kern_us)
+                     if E == WORKLOADS[args.workload][1] and args.physics == "pyb" else None),
             "rollout_metrics": {"episodes": mv[1], "mean_return": (mv[2] / mv[1]) if mv[1] else None,
                                 "nan_rewards": mv[6], "terminated": mv[4], "truncated": mv[5]},
         }

@@ -52,6 +52,10 @@ def main():
                    "write_kib": m["WRITE_SIZE"],
                    "traffic_bytes_per_launch": (2.0 * m["FETCH_SIZE"] + m["WRITE_SIZE"]) * 1024.0,
                    "note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB -> bytes, mean over dispatches"}
+            # instruction counters of the same kernel (per launch; SQ_ACTIVE_INST_* in quad-cycles)
+            for c in ("SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_ACTIVE_INST_VALU", "SQ_BUSY_CYCLES"):
+                if c in m:
+                    out[c.lower()] = m[c]
             with open(a.json, "w") as fh:
                 json.dump(out, fh, indent=1)
             print(json.dumps(out))
