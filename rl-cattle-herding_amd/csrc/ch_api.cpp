@@ -330,7 +330,6 @@ int ch_create(const ch_config* c, int64_t n_envs, int32_t device, ch_handle** ou
         // team-per-env kernel (87.6 vs 92-95 us: its 496-pair alpha table per env)
         if (c->mode == CH_MODE_MARL && h->M > 16) h->kernel = 1;
         if (h->lds > budget) h->kernel = 1;   // one env's pair table alone exceeds the budget
-        if (c->physics != CH_PHYS_PYB) h->kernel = 1;   // the physics variants run on the team-per-env kernel
         std::vector<uint16_t> pl((size_t)std::max(h->P, 1));
         for (int i = 0, r = 0; i < h->M; ++i)
             for (int j = i + 1; j < h->M; ++j) pl[r++] = (uint16_t)(i | (j << 8));
@@ -517,7 +516,7 @@ int ch__set_debug(ch_handle* h, double* dev) {
 /* Internal diagnostics: step kernel version (1 = team-per-env ch_kernels.hip, 2 = role-split ch_step.hip). */
 int ch__set_kernel(ch_handle* h, int32_t version) {
     if (!h || (version != 1 && version != 2)) return CH_ERR_INVALID;
-    if (version == 2 && (h->lds > 150 * 1024 || h->cfg.physics != CH_PHYS_PYB)) return CH_ERR_UNSUPPORTED;
+    if (version == 2 && h->lds > 150 * 1024) return CH_ERR_UNSUPPORTED;
     h->kernel = version;
     return CH_OK;
 }

@@ -281,15 +281,27 @@ constexpr double kGndCoeff = 11.36859, kPropRadius = 2.31348e-2, kArm = 0.0397;
 constexpr double kDragXY = 9.1785e-7, kDragZ = 10.311e-7;
 constexpr double kDw1 = 2267.18, kDw2 = .16, kDw3 = -.11;
 
+// |roll| < pi/2 and |pitch| < pi/2 of getEulerFromQuaternion(q) (quat_to_euler), without its atan2/asin:
+// off the gimbal-lock branches |asin(sarg)| < pi/2 always, and |atan2(Y, X)| < fl(pi/2) exactly when
+// X > 0 unless |Y| / X is so large that atan2 rounds to fl(pi/2) (then atan2 decides, as it does for the
+// X = +0, Y = 0 corner); NaN fails every test like the reference's comparison.
+template <class R> __device__ __forceinline__ bool upright(const R q[4]) {
+    const R x = q[0], y = q[1], z = q[2], w = q[3];
+    const R sarg = R(-2.0) * (x * z - w * y);
+    if (!(sarg > R(-0.99999) && sarg < R(0.99999))) return false;
+    const R Y = R(2) * (y * z + w * x), X = w * w - x * x - y * y + z * z;
+    if (X > R(0) && fabs(Y) <= X * R(1e12)) return true;
+    if (!(X >= R(0))) return false;
+    return fabs(m_atan2(Y, X)) < R(kPi / 2);
+}
+
 // _groundEffect (943-980): per-prop thrust boost below the clip height, skipped when tilted past 90 deg;
 // each force is applied at its prop link (LINK_FRAME +z) so it also adds a torque about the COM.
 template <class R>
 __device__ __forceinline__ void ground_effect(const R p[3], const R q[4], const R M[9], const R rpm[4], R h_clip,
                                               R F[3], R Tw[3]) {
     const R PX[4] = {R(0.028), R(-0.028), R(-0.028), R(0.028)}, PY[4] = {R(-0.028), R(-0.028), R(0.028), R(0.028)};
-    R rpy[3];
-    quat_to_euler(q, rpy);
-    if (!(fabs(rpy[0]) < R(kPi / 2) && fabs(rpy[1]) < R(kPi / 2))) return;
+    if (!upright(q)) return;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         R h = p[2] + (M[6] * PX[i] + M[7] * PY[i]);   // prop link COM height
@@ -382,6 +394,42 @@ __device__ __forceinline__ void dyn_substep(R p[3], R q[4], R v[3], R w[3], R rr
     }
 #pragma unroll
     for (int i = 0; i < 3; ++i) w[i] = M[3 * i + 0] * rr[0] + M[3 * i + 1] * rr[1] + M[3 * i + 2] * rr[2];
+}
+
+// Physics variants (BaseAviary.py:420-450) for the drone on this lane, all substeps of one control
+// step.  `base` is the lane of the env's drone 0, `nsh` a wave-uniform bound (>= n) on its drones and
+// n its live drones; lr / rr carry last_clipped_action and the DYN body rates in and out.  The
+// downwash term reads the other drones' substep-start positions by cross-lane shuffle: the loop bound
+// is wave-uniform, so every lane of the branch joins each shuffle.
+template <class R>
+__device__ __forceinline__ void variant_substeps(const StepParams<R>& p, int base, int nsh, int n, R pos[3], R q[4],
+                                                 R v[3], R w[3], const R rpm[4], R lr[4], R rr[3]) {
+    const int ph = p.physics;
+    const bool gnd = ph == CH_PHYS_PYB_GND || ph == CH_PHYS_PYB_GND_DRAG_DW;
+    const bool drag = ph == CH_PHYS_PYB_DRAG || ph == CH_PHYS_PYB_GND_DRAG_DW;
+    const bool dw = ph == CH_PHYS_PYB_DW || ph == CH_PHYS_PYB_GND_DRAG_DW;
+    const R h_clip = R(p.gnd_h_clip);
+    for (int s = 0; s < p.substeps; ++s) {
+        if (ph == CH_PHYS_DYN) {
+            dyn_substep(pos, q, v, w, rr, rpm, R(p.dt));
+        } else {
+            // extra() runs before drone_substep moves the body: pos/q/v are the substep-start state
+            auto extra = [&](const R* M, R* F, R* Tw) {
+                if (gnd) ground_effect(pos, q, M, rpm, h_clip, F, Tw);
+                if (drag) rotor_drag(v, M, lr, F);
+                if (dw) {
+                    for (int i = 0; i < nsh; ++i) {
+                        const R o[3] = {__shfl(pos[0], base + i, 64), __shfl(pos[1], base + i, 64),
+                                        __shfl(pos[2], base + i, 64)};
+                        if (i < n) downwash_term(pos, o, M, F);
+                    }
+                }
+            };
+            drone_substep(pos, q, v, w, rpm, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0, extra);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) lr[c] = rpm[c];   // last_clipped_action (BaseAviary.py:450)
+    }
 }
 
 // ---- flocking: MathematicalFlock (flockUtils.py:11-382) ----------------------------------------

@@ -123,50 +123,6 @@ __device__ __forceinline__ void reset_env(const StepParams<R>& p, Slot<R, TEAM>&
     }
 }
 
-// Physics variants (BaseAviary.py:420-450) for the drone on this lane: `base` is lane 0 of the env's
-// team, n its live drones.  The downwash term reads the other drones' substep-start positions by
-// cross-lane shuffle (every lane of the branch joins each shuffle: the loop bound p.NC is uniform).
-template <class R>
-__device__ __forceinline__ void variant_substeps(const StepParams<R>& p, long long di, int base, int n, R pos[3],
-                                                 R q[4], R v[3], R w[3], const R rpm[4]) {
-    const long long DS = (long long)p.E * p.NC;
-    R lr[4], rr[3];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) lr[c] = p.phys[c * DS + di];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) rr[c] = p.phys[(4 + c) * DS + di];
-    const int ph = p.physics;
-    const bool gnd = ph == CH_PHYS_PYB_GND || ph == CH_PHYS_PYB_GND_DRAG_DW;
-    const bool drag = ph == CH_PHYS_PYB_DRAG || ph == CH_PHYS_PYB_GND_DRAG_DW;
-    const bool dw = ph == CH_PHYS_PYB_DW || ph == CH_PHYS_PYB_GND_DRAG_DW;
-    const R h_clip = R(p.gnd_h_clip);
-    for (int s = 0; s < p.substeps; ++s) {
-        if (ph == CH_PHYS_DYN) {
-            dyn_substep(pos, q, v, w, rr, rpm, R(p.dt));
-        } else {
-            // extra() runs before drone_substep moves the body: pos/q/v are the substep-start state
-            auto extra = [&](const R* M, R* F, R* Tw) {
-                if (gnd) ground_effect(pos, q, M, rpm, h_clip, F, Tw);
-                if (drag) rotor_drag(v, M, lr, F);
-                if (dw) {
-                    for (int i = 0; i < p.NC; ++i) {
-                        const R o[3] = {__shfl(pos[0], base + i, 64), __shfl(pos[1], base + i, 64),
-                                        __shfl(pos[2], base + i, 64)};
-                        if (i < n) downwash_term(pos, o, M, F);
-                    }
-                }
-            };
-            drone_substep(pos, q, v, w, rpm, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0, extra);
-        }
-#pragma unroll
-        for (int c = 0; c < 4; ++c) lr[c] = rpm[c];   // last_clipped_action (BaseAviary.py:450)
-    }
-#pragma unroll
-    for (int c = 0; c < 4; ++c) p.phys[c * DS + di] = lr[c];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) p.phys[(4 + c) * DS + di] = rr[c];
-}
-
 template <class R, int TEAM, bool RESET_ONLY, int MODE, bool PHYS = false>
 __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
     constexpr int EPB = 64 / TEAM;
@@ -234,7 +190,17 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
             if (!(p.phase_mask & 1)) {
                 pid_vel(pos, q, v, Rm, rpy, a, R(p.dt_ctrl), pid, rpm, p.debug ? p.debug + di * 16 : nullptr);
                 if constexpr (PHYS) {
-                    variant_substeps(p, di, slot * TEAM, n, pos, q, v, w, rpm);
+                    const long long PS = (long long)p.E * p.NC;
+                    R lr[4], rr[3];
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) lr[c] = p.phys[c * PS + di];
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) rr[c] = p.phys[(4 + c) * PS + di];
+                    variant_substeps(p, slot * TEAM, p.NC, n, pos, q, v, w, rpm, lr, rr);
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) p.phys[c * PS + di] = lr[c];
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) p.phys[(4 + c) * PS + di] = rr[c];
                 } else {
                     for (int s = 0; s < p.substeps; ++s)
                         drone_substep(pos, q, v, w, rpm, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0);

@@ -342,7 +342,7 @@ __device__ __forceinline__ void flock_combine(const StepParams<R>& p, V2Smem<R>&
 
 // GT/NT/MT > 0 specialise the kernel for one geometry (envs per workgroup, drones, cattle): the LDS
 // carve and all index arithmetic then fold to immediates, which keeps the kernel within the SGPR file.
-template <class R, int MODE, int GT, int NT, int MT>
+template <class R, int MODE, int GT, int NT, int MT, bool PHYS = false>
 __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
     extern __shared__ __align__(16) unsigned char smem[];
     constexpr bool marl = MODE == 1;
@@ -372,6 +372,7 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
     const int dg = dlane ? tid / N : 0, dk = tid - dg * N;
     const long long di = (long long)e0 * N + tid;
     R pos[3], q[4], v[3], w[3], pid[9], rpy_in[3] = {0, 0, 0};
+    R ph_lr[4] = {0, 0, 0, 0}, ph_rr[3] = {0, 0, 0};   // PHYS: last_clipped_action, DYN rpy_rates
     int stepi = 0, n0 = 0, act0 = 0;
     R spx_r[3] = {0, 0, 0}, spy_r[3] = {0, 0, 0};   // cow waves: prefetched spawn positions
     if (tid < 64) {
@@ -393,6 +394,12 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
                 for (int c = 0; c < 3; ++c) rpy_in[c] = p.rpy[c * DS + di];
             }
             stepi = p.envi[9 * E + e0 + dg];   // ch_step calls on this env so far: the Philox action counter
+            if constexpr (PHYS) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) ph_lr[c] = p.phys[c * DS + di];
+#pragma unroll
+                for (int c = 0; c < 3; ++c) ph_rr[c] = p.phys[(4 + c) * DS + di];
+            }
         }
     } else {
         const float rM0 = 1.0f / (float)M;
@@ -401,7 +408,9 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
             R x = p.cattle[0 * CS + ci], y = p.cattle[1 * CS + ci];
             const R vx = p.cattle[2 * CS + ci], vy = p.cattle[3 * CS + ci];
             const R dt = R(p.dt);
-            for (int s = 0; s < p.substeps; ++s) { x += vx * dt; y += vy * dt; }   // frictionless cube (trace-pinned)
+            // frictionless cube (trace-pinned); no p.stepSimulation under Physics.DYN (BaseAviary.py:447-448)
+            if (!PHYS || p.physics != CH_PHYS_DYN)
+                for (int s = 0; s < p.substeps; ++s) { x += vx * dt; y += vy * dt; }
             CH_ST(&p.cattle[0 * CS + ci], x); CH_ST(&p.cattle[1 * CS + ci], y);
             S.cx[u] = x; S.cy[u] = y; S.cvx[u] = vx; S.cvy[u] = vy;
         }
@@ -480,8 +489,16 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
             if (!(p.phase_mask & 1)) {
                 R rpm[4];
                 pid_vel(pos, q, v, Rm, rpy, a, R(p.dt_ctrl), pid, rpm, p.debug ? p.debug + di * 16 : nullptr);
-                for (int s = 0; s < p.substeps; ++s)
-                    drone_substep(pos, q, v, w, rpm, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0);
+                if constexpr (PHYS) {
+                    variant_substeps(p, dg * N, N, n, pos, q, v, w, rpm, ph_lr, ph_rr);
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) CH_ST(&p.phys[c * DS + di], ph_lr[c]);
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) CH_ST(&p.phys[(4 + c) * DS + di], ph_rr[c]);
+                } else {
+                    for (int s = 0; s < p.substeps; ++s)
+                        drone_substep(pos, q, v, w, rpm, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0);
+                }
             }
             R* D = p.drone;
 #pragma unroll
@@ -918,6 +935,10 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
                 if (k == 0) ei[I_NEWN * G + g] = n;
                 R x, y, z;
                 reset_drone(p, (long long)e0 * N + ud, k, n, x, y, z);
+                if constexpr (PHYS) {   // last_clipped_action, rpy_rates = 0 (_housekeeping, BaseAviary.py:565, 581-582)
+#pragma unroll
+                    for (int c = 0; c < kPhysComps; ++c) CH_ST(&p.phys[c * DS + (long long)e0 * N + ud], R(0));
+                }
                 {   // identity attitude: Euler angles (+0, -0, +0) for the next step's cache
                     const long long dd = (long long)e0 * N + ud;
                     CH_ST(&p.rpy[dd], R(0)); CH_ST(&p.rpy[DS + dd], -R(0)); CH_ST(&p.rpy[2 * DS + dd], R(0));
@@ -974,17 +995,17 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
     if (tid == 0) { TS(14, (long long)clock64()); TS(1, (long long)wall_clock64()); }
 }
 
-template <class R, int MODE, int GT, int NT, int MT>
+template <class R, int MODE, int GT, int NT, int MT, bool PHYS = false>
 static hipError_t launch_v2_kernel(const StepParams<R>& p, int block, size_t lds, hipStream_t st) {
     static bool attr_set = false;   // one-time opt-in to > 64 KiB of dynamic LDS
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_step2<R, MODE, GT, NT, MT>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_step2<R, MODE, GT, NT, MT, PHYS>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
     dim3 grid((p.E + p.G - 1) / p.G);
-    hipLaunchKernelGGL((k_step2<R, MODE, GT, NT, MT>), grid, dim3(block), lds, st, p);
+    hipLaunchKernelGGL((k_step2<R, MODE, GT, NT, MT, PHYS>), grid, dim3(block), lds, st, p);
     return hipGetLastError();
 }
 
@@ -992,6 +1013,10 @@ static hipError_t launch_v2_kernel(const StepParams<R>& p, int block, size_t lds
 template <class R>
 hipError_t launch_step_v2(const StepParams<R>& p, int block, size_t lds, hipStream_t st) {
     const int G = p.G, N = p.NC, M = p.M;
+    if (p.physics != CH_PHYS_PYB) {   // physics variants (BaseAviary.py:420-450): runtime-geometry instantiation
+        if (p.mode == 1) return launch_v2_kernel<R, 1, 0, 0, 0, true>(p, block, lds, st);
+        return launch_v2_kernel<R, 0, 0, 0, 0, true>(p, block, lds, st);
+    }
     if (p.mode == 1) {
         if (G == 4 && N == 4 && M == 32) return launch_v2_kernel<R, 1, 4, 4, 32>(p, block, lds, st);     // configs[4]
         return launch_v2_kernel<R, 1, 0, 0, 0>(p, block, lds, st);

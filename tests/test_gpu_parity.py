@@ -345,7 +345,12 @@ def test_full_size_properties():
                                              (0, 12, 16, 300, None), (1, 3, 8, 257, None), (0, 8, 64, 40, None),
                                              (0, 4, 16, 1000, (4, 128)), (0, 4, 16, 999, (2, 128)),
                                              (0, 4, 16, 1001, (8, 256)), (0, 4, 16, 1003, (16, 512)), (1, 5, 16, 333, (3, 128)),
-                                             (0, 2, 8, 700, (1, 256))])
+                                             (0, 2, 8, 700, (1, 256)),
+                                             # physics variants (BaseAviary.py:420-450): DYN, GND, DRAG, DW, all
+                                             (0, 4, 16, 4096, "dyn"), (0, 4, 16, 1000, "pyb_gnd"),
+                                             (0, 4, 16, 1000, "pyb_drag"), (0, 6, 8, 1000, "pyb_dw"),
+                                             (0, 4, 16, 4096, "pyb_gnd_drag_dw"), (1, 4, 16, 333, "pyb_gnd_drag_dw"),
+                                             (1, 3, 8, 257, "dyn")])
 def test_step_kernels_v1_v2_bit_identical(mode, n, m, E, geom):
     """The role-split v2 step kernel (ch_step.hip, the default) and the team-per-env v1 kernel
     (ch_kernels.hip) compute the same arithmetic in the same order: 150 random-action steps with
@@ -353,8 +358,11 @@ def test_step_kernels_v1_v2_bit_identical(mode, n, m, E, geom):
     import ctypes
     import torch
     from cattleherd import _lib
-    hs = [_batch(mode, n, m, E, None) for _ in range(2)]
+    physics = geom if isinstance(geom, str) else "pyb"
+    geom = None if isinstance(geom, str) else geom
+    hs = [_batch(mode, n, m, E, None, physics=physics) for _ in range(2)]
     assert _lib.lib().ch__set_kernel(hs[0].handle, ctypes.c_int32(1)) == 0
+    assert _lib.lib().ch__set_kernel(hs[1].handle, ctypes.c_int32(2)) == 0
     if geom is not None:
         assert _lib.lib().ch__set_geometry(hs[1].handle, ctypes.c_int32(geom[0]), ctypes.c_int32(geom[1])) == 0
     for h in hs:
