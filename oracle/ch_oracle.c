@@ -277,30 +277,45 @@ static void dyn_substep(double* p, double* q, double* v, double* w, double* rr, 
 static void drone_substep(const och_config* c, double* p, double* q, double* v, double* w, const double* rpm, double dt,
                           const phys_ctx* x) {
     double R[9]; och_matrix_from_quat(q, R);
-    double F[3] = {0, 0, 0}, Tw[3] = {0, 0, 0};
-    for (int i = 0; i < 4; ++i) {
-        double f = rpm[i] * rpm[i] * KF;
-        double fw[3] = {R[2] * f, R[5] * f, R[8] * f};
-        double rb[3] = {PROP[i][0], PROP[i][1], 0.0};
-        double rw[3] = {R[0] * rb[0] + R[1] * rb[1], R[3] * rb[0] + R[4] * rb[1], R[6] * rb[0] + R[7] * rb[1]};
-        double t[3]; cross3(rw, fw, t);
-        for (int k = 0; k < 3; ++k) { F[k] += fw[k]; Tw[k] += t[k]; }
-    }
+    double F[3] = {0, 0, 0}, Tw[3] = {0, 0, 0}, tb[3];
     double t0 = rpm[0] * rpm[0] * KM, t1 = rpm[1] * rpm[1] * KM, t2 = rpm[2] * rpm[2] * KM, t3 = rpm[3] * rpm[3] * KM;
     double tz = (-t0 + t1 - t2 + t3);
-    if (c->torque_world) Tw[2] += tz;
-    else { Tw[0] += R[2] * tz; Tw[1] += R[5] * tz; Tw[2] += R[8] * tz; }
-    if (x) physics_forces(x, p, q, v, R, rpm, F, Tw);
+    const int body = !x && c->torque_world;
+    if (body) {
+        /* PYB with the world-frame motor torque (the default): the four +z prop forces (LINK_FRAME at
+         * (px, py, 0), cf2x.urdf:42-78) reduced to the body frame in closed form.  Their world torque
+         * sum(R P_i x R e_z f_i) = R sum(P_i x e_z f_i) comes back to the body as (sum py f, -sum px f, 0);
+         * the world-frame yaw torque tz e_z is R^T e_z tz = tz (R[6], R[7], R[8]). */
+        double f[4];
+        for (int i = 0; i < 4; ++i) f[i] = rpm[i] * rpm[i] * KF;
+        const double T = ((f[0] + f[1]) + f[2]) + f[3];
+        F[0] = R[2] * T; F[1] = R[5] * T; F[2] = R[8] * T;
+        tb[0] = 0.028 * (((-f[0] - f[1]) + f[2]) + f[3]) + R[6] * tz;
+        tb[1] = 0.028 * (((-f[0] + f[1]) + f[2]) - f[3]) + R[7] * tz;
+        tb[2] = R[8] * tz;
+    } else {
+        for (int i = 0; i < 4; ++i) {
+            double f = rpm[i] * rpm[i] * KF;
+            double fw[3] = {R[2] * f, R[5] * f, R[8] * f};
+            double rb[3] = {PROP[i][0], PROP[i][1], 0.0};
+            double rw[3] = {R[0] * rb[0] + R[1] * rb[1], R[3] * rb[0] + R[4] * rb[1], R[6] * rb[0] + R[7] * rb[1]};
+            double t[3]; cross3(rw, fw, t);
+            for (int k = 0; k < 3; ++k) { F[k] += fw[k]; Tw[k] += t[k]; }
+        }
+        if (c->torque_world) Tw[2] += tz;
+        else { Tw[0] += R[2] * tz; Tw[1] += R[5] * tz; Tw[2] += R[8] * tz; }
+        if (x) physics_forces(x, p, q, v, R, rpm, F, Tw);
+    }
     F[2] += -MASS * G;
     double k = c->damping;
     if (k != 0.0) {
         double sp = norm3(v);
         for (int i = 0; i < 3; ++i) F[i] -= MASS * v[i] * (k + k * sp);
     }
-    double wb[3], tb[3];
+    double wb[3];
     for (int i = 0; i < 3; ++i) {
         wb[i] = R[0 + i] * w[0] + R[3 + i] * w[1] + R[6 + i] * w[2];
-        tb[i] = R[0 + i] * Tw[0] + R[3 + i] * Tw[1] + R[6 + i] * Tw[2];
+        if (!body) tb[i] = R[0 + i] * Tw[0] + R[3 + i] * Tw[1] + R[6 + i] * Tw[2];
     }
     const double J[3] = {JX, JY, JZ};
     if (k != 0.0) {

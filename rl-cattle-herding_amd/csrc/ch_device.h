@@ -8,6 +8,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 #include "ch_internal.h"
 
@@ -207,22 +208,37 @@ __device__ __forceinline__ void drone_substep(R p[3], R q[4], R v[3], R w[3], co
     const R PX[4] = {R(0.028), R(-0.028), R(-0.028), R(0.028)}, PY[4] = {R(-0.028), R(-0.028), R(0.028), R(0.028)};
     R M[9];
     quat_to_mat(q, M);
-    R F[3] = {0, 0, 0}, Tw[3] = {0, 0, 0};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        R f = rpm[i] * rpm[i] * R(kKF);
-        R fw[3] = {M[2] * f, M[5] * f, M[8] * f};
-        R rw[3] = {M[0] * PX[i] + M[1] * PY[i], M[3] * PX[i] + M[4] * PY[i], M[6] * PX[i] + M[7] * PY[i]};
-        R t[3] = {rw[1] * fw[2] - rw[2] * fw[1], rw[2] * fw[0] - rw[0] * fw[2], rw[0] * fw[1] - rw[1] * fw[0]};
-#pragma unroll
-        for (int k = 0; k < 3; ++k) { F[k] += fw[k]; Tw[k] += t[k]; }
-    }
+    R F[3] = {0, 0, 0}, Tw[3] = {0, 0, 0}, tb[3];
     R t0 = rpm[0] * rpm[0] * R(kKM), t1 = rpm[1] * rpm[1] * R(kKM), t2 = rpm[2] * rpm[2] * R(kKM),
       t3 = rpm[3] * rpm[3] * R(kKM);
     R tz = (-t0 + t1 - t2 + t3);
-    if (torque_world) Tw[2] += tz;
-    else { Tw[0] += M[2] * tz; Tw[1] += M[5] * tz; Tw[2] += M[8] * tz; }
-    extra(M, F, Tw);
+    // PYB with the world-frame motor torque (the default): the prop wrench in closed form in the body
+    // frame (the oracle's drone_substep, same operation order): torque (sum py f, -sum px f, 0) plus
+    // R^T e_z tz; force R e_z sum f.  Other cases accumulate per-link world forces (variants add theirs).
+    const bool body = std::is_same<X, NoExtraForces>::value && torque_world;
+    if (body) {
+        R f[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) f[i] = rpm[i] * rpm[i] * R(kKF);
+        const R T = ((f[0] + f[1]) + f[2]) + f[3];
+        F[0] = M[2] * T; F[1] = M[5] * T; F[2] = M[8] * T;
+        tb[0] = R(0.028) * (((-f[0] - f[1]) + f[2]) + f[3]) + M[6] * tz;
+        tb[1] = R(0.028) * (((-f[0] + f[1]) + f[2]) - f[3]) + M[7] * tz;
+        tb[2] = M[8] * tz;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            R f = rpm[i] * rpm[i] * R(kKF);
+            R fw[3] = {M[2] * f, M[5] * f, M[8] * f};
+            R rw[3] = {M[0] * PX[i] + M[1] * PY[i], M[3] * PX[i] + M[4] * PY[i], M[6] * PX[i] + M[7] * PY[i]};
+            R t[3] = {rw[1] * fw[2] - rw[2] * fw[1], rw[2] * fw[0] - rw[0] * fw[2], rw[0] * fw[1] - rw[1] * fw[0]};
+#pragma unroll
+            for (int k = 0; k < 3; ++k) { F[k] += fw[k]; Tw[k] += t[k]; }
+        }
+        if (torque_world) Tw[2] += tz;
+        else { Tw[0] += M[2] * tz; Tw[1] += M[5] * tz; Tw[2] += M[8] * tz; }
+        extra(M, F, Tw);
+    }
     F[2] += R(-kMass * kG);
     const R k = damping;
     if (k != R(0)) {
@@ -230,11 +246,11 @@ __device__ __forceinline__ void drone_substep(R p[3], R q[4], R v[3], R w[3], co
 #pragma unroll
         for (int i = 0; i < 3; ++i) F[i] -= R(kMass) * v[i] * (k + k * sp);
     }
-    R wb[3], tb[3];
+    R wb[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         wb[i] = M[0 + i] * w[0] + M[3 + i] * w[1] + M[6 + i] * w[2];
-        tb[i] = M[0 + i] * Tw[0] + M[3 + i] * Tw[1] + M[6 + i] * Tw[2];
+        if (!body) tb[i] = M[0 + i] * Tw[0] + M[3 + i] * Tw[1] + M[6 + i] * Tw[2];
     }
     const R J[3] = {R(kJx), R(kJy), R(kJz)};
     if (k != R(0)) {
