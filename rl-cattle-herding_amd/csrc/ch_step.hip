@@ -509,14 +509,17 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
             for (int c = 0; c < 3; ++c) { CH_ST(&D[(7 + c) * DS + di], v[c]); CH_ST(&D[(10 + c) * DS + di], w[c]); }
 #pragma unroll
             for (int c = 0; c < 9; ++c) CH_ST(&D[(13 + c) * DS + di], pid[c]);
+            S.dx[tid] = pos[0]; S.dy[tid] = pos[1]; S.dz[tid] = pos[2];
+        }
+        wave_sync();
+        lds_signal(fl + F_D);   // positions published: the cow waves' distance work starts now
+        // the Euler angles (obs row, next step's PID cache) are only the drone wave's: after the hand-off
+        if (live) {
             quat_to_euler(q, rpy_out);
 #pragma unroll
             for (int c = 0; c < 3; ++c) CH_ST(&p.rpy[c * DS + di], rpy_out[c]);
-            S.dx[tid] = pos[0]; S.dy[tid] = pos[1]; S.dz[tid] = pos[2];
         }
         if (live && wobs) obs_own(obs_wg + dg * RW, dk, pos[2], rpy_out, v, w);
-        wave_sync();
-        lds_signal(fl + F_D);
         if (tid == 0) TS(4, (long long)clock64());
         lds_wait(fl + F_E, W1);   // env scalars and the curriculum table (staged by the cow waves)
 
