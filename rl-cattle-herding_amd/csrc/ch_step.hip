@@ -1018,6 +1018,7 @@ hipError_t launch_step_v2(const StepParams<R>& p, int block, size_t lds, hipStre
     const int G = p.G, N = p.NC, M = p.M;
     if (p.physics != CH_PHYS_PYB) {   // physics variants (BaseAviary.py:420-450): runtime-geometry instantiation
         if (p.mode == 1) return launch_v2_kernel<R, 1, 0, 0, 0, true>(p, block, lds, st);
+        if (G == 16 && N == 4 && M == 16) return launch_v2_kernel<R, 0, 16, 4, 16, true>(p, block, lds, st);   // configs[3]
         return launch_v2_kernel<R, 0, 0, 0, 0, true>(p, block, lds, st);
     }
     if (p.mode == 1) {
