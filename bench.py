@@ -134,21 +134,47 @@ def policy_rollout(b, n, steps, warmup):
 
 
 def cpu_baseline(mode, n, m, seconds=12.0):
-    """The CPU oracle (scalar fp64 C port, OpenMP one env per thread) on a bounded sample."""
+    """The CPU oracle (scalar fp64 C port, OpenMP one env per thread) on a bounded sample, on every
+    core this process may use: OMP_NUM_THREADS when the pool sets it (16 per GPU on the MI355X
+    boxes), else the CPU affinity mask.  os.cpu_count() is reported beside it: on the GPU box it is
+    the whole machine, of which one GPU's job gets a share."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import numpy as np
     import oracle as O
     from cattleherd._lib import spawn_table
     table = spawn_table(m)
-    threads = max(1, min(16, os.cpu_count() or 1))
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    threads = int(omp) if omp.isdigit() and int(omp) > 0 else affinity
+    threads = max(1, min(threads, affinity))
     E = threads * 4
     secs, steps = O.batch_rollout(0 if mode == "ctde" else 1, n, m, table, E=E, T=20, threads=threads)
     T = max(20, int(seconds / max(secs, 1e-6) * 20))
     secs, steps = O.batch_rollout(0 if mode == "ctde" else 1, n, m, table, E=E, T=T, threads=threads)
-    del np
     return {"value": steps / secs, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "host_cpus": os.cpu_count(), "affinity_cpus": affinity, "omp_num_threads": omp or None,
             "sample": f"{E} envs x {T} random-action steps ({steps} env-steps, {secs:.1f} s) of the fp64 C oracle, "
-                      f"{threads} OpenMP threads"}
+                      f"{threads} OpenMP threads (one env per thread iteration)"}
+
+
+def launch_check(args):
+    """--launch-check: the multi-rank plumbing alone (no GPU): process group over ``--backend``, world
+    size, per-rank env ranges, the metric all-reduce and the max-over-ranks time."""
+    from cattleherd import distributed as D
+    rank, world, _ = D.world_info()
+    D.init(args.backend)
+    import torch.distributed as dist
+    seen = dist.get_world_size() if dist.is_initialized() else 1
+    if seen != args.gpus:
+        print(f"bench: --gpus {args.gpus} but the process group has {seen} ranks", file=sys.stderr)
+        sys.exit(3)
+    E = args.envs or WORKLOADS[args.workload][1]
+    lo = D.env_offset(rank, E)
+    mv, t = D.reduce_rollout([float(rank + 1)] * 8, 0.5 + rank, device="cpu")
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": seen, "backend": args.backend,
+                          "env_ranges": [[D.env_offset(r, E), D.env_offset(r, E) + E] for r in range(seen)],
+                          "metric_sum": float(mv[0]), "max_time": t, "rank0_range": [lo, lo + E]}), flush=True)
+    D.shutdown()
 
 
 def main():
@@ -167,32 +193,63 @@ def main():
                     help="also time a rollout driven by the on-device SB3 policy (model-v16-6 weights, CTDE only)")
     ap.add_argument("--graph", type=int, default=0,
                     help="steps per captured HIP graph in the timed loop (0 = one host launch per step)")
+    ap.add_argument("--backend", default="nccl", help="process-group backend (nccl = RCCL over xGMI)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="run only the multi-rank plumbing (process group, env ranges, all-reduce); no GPU")
     args = ap.parse_args()
 
+    # --gpus N from a plain `python bench.py`: one child process per GPU, started before this
+    # process touches the GPU (cattleherd.launch imports no torch)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        from cattleherd.launch import spawn_ranks
+        sys.exit(spawn_ranks(args.gpus, os.path.abspath(__file__), sys.argv[1:]))
+    if args.launch_check:
+        return launch_check(args)
+
     import torch
+    import torch.distributed as dist
     from cattleherd import distributed as D
     from cattleherd.env import HerdBatch
     rank, world, local = D.world_info()
     if world > 1:
-        D.init("nccl")          # RCCL over xGMI; one process per GPU
-    else:
-        torch.cuda.set_device(0)
+        D.init(args.backend, device_index=local)   # RCCL over xGMI; one process per GPU
+        world = dist.get_world_size()
+    torch.cuda.set_device(local if world > 1 else 0)
+    if world != args.gpus:
+        print(f"bench: --gpus {args.gpus} but the process group has {world} ranks", file=sys.stderr)
+        sys.exit(3)
 
     mode, E, n, m, desc = WORKLOADS[args.workload]
     if args.envs:
         E = args.envs
     b = HerdBatch(E, n, m, mode=mode, precision=args.precision, env_id_offset=D.env_offset(rank, E),
                   physics=args.physics)
-    b.reset()
+    print(f"bench: rank {rank}/{world} device {torch.cuda.current_device()} envs "
+          f"[{D.env_offset(rank, E)}, {D.env_offset(rank, E) + E})", file=sys.stderr, flush=True)
     stream = torch.cuda.current_stream()
+
+    # end of a rollout (SURVEY §8(d) "host sync at the end"): device reduction of the per-env metric
+    # rows, the RCCL all-reduce over xGMI (the rollout's only collective), one 64-byte copy to pinned
+    # memory and the stream sync
+    mbuf = torch.zeros(8, dtype=torch.float64, device=b.device)
+    mhost = torch.zeros(8, dtype=torch.float64).pin_memory()
+
+    def end_of_rollout():
+        b.metrics_device(reset=True, out=mbuf)
+        if world > 1:
+            dist.all_reduce(mbuf)
+        mhost.copy_(mbuf, non_blocking=True)
+        stream.synchronize()
+        return mhost.numpy().copy()
+
+    b.reset()
     for _ in range(args.warmup):
         b.step(random_actions=True, autoreset=True, terminal_obs=False)
     # the timed loop: K steps as whole graph replays of `chunk` steps (plus single launches for the rest)
     chunk = args.graph if args.graph > 0 and args.steps >= args.graph else 0
     graph = b.capture_rollout(chunk) if chunk else None
-    if graph is not None:   # capture launched one real step; keep warm-up semantics
-        torch.cuda.synchronize()
-    b.metrics(reset=True)
+    end_of_rollout()   # warm: reduction kernel, pinned copy, first collective; zeroes the metric rows
+    b.sync()
 
     def run(k):
         done = 0
@@ -208,12 +265,18 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     run(args.steps)
-    # end-of-rollout metrics: RCCL all-reduce over xGMI, the only collective of the rollout
-    mv, _ = D.reduce_rollout(torch.tensor(b.metrics(reset=True), dtype=torch.float64), 0.0, device=b.device)
+    mv = end_of_rollout()
     torch.cuda.synchronize()
     D.barrier()
     dt = time.perf_counter() - t0
     _, dt = D.reduce_rollout([0.0], dt, device=b.device)   # max over ranks
+    b.sync()   # raises if a step kernel recorded a device error (hand-off timeout)
+
+    # the end-of-rollout path on its own (included once in the timed region above)
+    torch.cuda.synchronize()
+    te = time.perf_counter()
+    end_of_rollout()
+    rollout_end_us = (time.perf_counter() - te) * 1e6
 
     # live per-launch kernel timing with HIP events on the launch stream (roofline): one event pair
     # around nk back-to-back launches (an event between every two launches would break the queue's
@@ -245,6 +308,7 @@ def main():
             "vs_baseline": None, "dtype": args.precision, "agent_steps_per_s": value * n,
             "data": "synthetic: Philox4x32 random VEL actions in-kernel, spawn table from config/cattle_positions.yaml",
             "launch": f"HIP graph of {chunk} steps per replay" if graph is not None else "one host launch per step",
+            "rollout_end_us": rollout_end_us,
             "config": {"workload": desc, "envs_per_gpu": E, "num_drones": n, "num_cattle": m, "mode": mode,
                        "physics": args.physics,
                        "parallelism": f"env-sharded x{world} (no per-step collective)"},

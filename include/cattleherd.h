@@ -157,6 +157,16 @@ enum {
 };
 int ch_metrics(ch_handle* h, double* host_out, int32_t reset_after, void* stream);
 
+/* The same sums written to a DEVICE buffer double[CH_METRIC_COUNT] on `stream`, without a host sync:
+ * the input of the end-of-rollout RCCL all-reduce (bench.py).  Replaces the same reference code. */
+int ch_metrics_device(ch_handle* h, double* dev_out, int32_t reset_after, void* stream);
+
+/* Wait for `stream` and report the handle's sticky device error word: CH_ERR_DEVICE if a step kernel
+ * recorded a failure (e.g. an LDS hand-off that timed out), CH_OK otherwise.  ch_metrics and
+ * ch_get_state report it too.  (The reference's analogue: an exception out of env.step,
+ * marl_wrapper.py:87-95.) */
+int ch_sync(ch_handle* h, void* stream);
+
 /* Number of built-in spawn scenarios / cows, and a copy of the table (host double[S][C][2]):
  * config/cattle_positions.yaml, 100 scenarios x 16 cows (BaseAviary.py:88-94). */
 int ch_builtin_spawn_table(double* out, int32_t* scenarios, int32_t* cows);

@@ -729,9 +729,12 @@ void och_task(const och_config* c, och_state* s, double* reward, uint8_t* termin
             for (int i = 0; i < n; ++i) {
                 reward[i] = r1[i]; terminated[i] = d1[i]; truncated[i] = (uint8_t)trunc_marl(c, s, &g, i);
             }
+            s->step_counter += 1;   /* rllib_envs/BaseAviary.py:436, after the dicts */
             return;
         }
-        /* the wrapper's recomputation for active agents (marl_wrapper.py:104-113) */
+        /* env.step counts its step before returning (rllib_envs/BaseAviary.py:436); the wrapper's
+         * recomputation for active agents (marl_wrapper.py:104-113) sees the incremented counter */
+        s->step_counter += 1;
         for (int i = 0; i < n; ++i) {
             if (!s->active[i]) continue;
             reward[i] = reward_marl(c, s, &g, i);
@@ -915,8 +918,8 @@ int och_step(const och_config* c, och_state* s, const float* actions, float* obs
         och_flock_update(cp, cv, c->m, dxy, n, nv);
         for (int j = 0; j < c->m; ++j) { s->cv[j][0] = nv[2 * j]; s->cv[j][1] = nv[2 * j + 1]; }
     }
-    och_task(c, s, reward, terminated, truncated);
-    s->step_counter += (c->mode == 0) ? substeps : 1;
+    och_task(c, s, reward, terminated, truncated);   /* MARL: counts the step itself (436) */
+    if (c->mode == 0) s->step_counter += substeps;   /* sb3_envs/BaseAviary.py:464 */
     int done;
     if (c->mode == 0) done = terminated[0] || truncated[0];
     else if (c->marl_wrapper) { done = 1; for (int i = 0; i < n; ++i) if (s->active[i]) done = 0; }

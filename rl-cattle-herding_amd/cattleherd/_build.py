@@ -11,7 +11,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(ROOT, "csrc")
 BUILD = os.path.join(ROOT, "build")
 LIB = os.path.join(PKG, "libcattleherd.so")
-SOURCES = ["ch_kernels.hip", "ch_step.hip", "ch_policy.hip", "ch_api.cpp"]
+SOURCES = ["ch_kernels.hip", "ch_step.hip", "ch_policy.hip", "ch_aux.hip", "ch_api.cpp"]
 HEADERS = ["ch_device.h", "ch_internal.h", "ch_common.h", "ch_spawn_table.inc"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("CH_OFFLOAD_ARCH", "gfx950")

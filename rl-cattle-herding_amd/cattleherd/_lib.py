@@ -21,7 +21,8 @@ PHYSICS = {"pyb": 0, "dyn": 1, "pyb_gnd": 2, "pyb_drag": 3, "pyb_dw": 4, "pyb_gn
 
 # every symbol include/cattleherd.h declares
 EXPORTS = ("ch_default_config", "ch_create", "ch_destroy", "ch_last_error", "ch_shape", "ch_reset", "ch_step",
-           "ch_state_size", "ch_get_state", "ch_set_state", "ch_metrics", "ch_builtin_spawn_table",
+           "ch_state_size", "ch_get_state", "ch_set_state", "ch_metrics", "ch_metrics_device", "ch_sync",
+           "ch_builtin_spawn_table",
            "ch_spawn_table", "ch_mlp_forward", "ch_policy_forward")
 CH_ACT_NONE, CH_ACT_TANH, CH_ACT_RELU = 0, 1, 2
 
@@ -82,6 +83,8 @@ def lib():
     L.ch_get_state.argtypes = [vp, vp, vp, vp]
     L.ch_set_state.argtypes = [vp, vp, vp, vp]
     L.ch_metrics.argtypes = [vp, vp, i32, vp]
+    L.ch_metrics_device.argtypes = [vp, vp, i32, vp]
+    L.ch_sync.argtypes = [vp, vp]
     L.ch_builtin_spawn_table.argtypes = [vp, P(i32), P(i32)]
     L.ch_spawn_table.argtypes = [i32, vp, P(i32), P(i32)]
     L.ch_mlp_forward.argtypes = [P(ChMlp), vp, i64, vp, vp]

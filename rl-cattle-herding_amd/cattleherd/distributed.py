@@ -38,6 +38,8 @@ def init(backend="nccl", device_index=None):
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group(backend)
+        if dist.get_world_size() != world:
+            raise RuntimeError(f"process group has {dist.get_world_size()} ranks, WORLD_SIZE says {world}")
     return rank, world, local
 
 

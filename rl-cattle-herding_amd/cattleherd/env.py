@@ -143,20 +143,20 @@ class HerdBatch:
 
     def invalidate_obs(self):
         """The caller modified ``self.obs``: the next step writes every observation block in full."""
-        L.check(L.lib().ch__obs_invalidate(self.handle), self.handle)
+        L.check(L.lib().ch__obs_invalidate(self.handle, self._stream()), self.handle)
 
     def capture_rollout(self, steps, autoreset=True, terminal_obs=False):
         """Capture ``steps`` random-action steps into a HIP graph (torch.cuda.CUDAGraph); ``replay()``
         then runs them with one launch from the host.  Every launch parameter is constant across steps
-        (the Philox counter lives in the env state), so a replay is exactly ``steps`` calls of
-        ``step(random_actions=True)``.  Used by bench.py to take the host out of the step loop."""
+        (the Philox counter lives in the env state) and the state-dependent switches (Euler cache,
+        observation bytes) are device words the kernel reads at run time, so a replay is exactly
+        ``steps`` calls of ``step(random_actions=True)``, also after reset()/set_state()/invalidate_obs().
+        Nothing runs at capture time."""
         torch = self.torch
         side = torch.cuda.Stream(device=self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.stream(side):
-            self.step(random_actions=True, autoreset=autoreset, terminal_obs=terminal_obs)   # first launch: attrs
-            torch.cuda.synchronize(self.device)
             with torch.cuda.graph(graph, stream=side):
                 for _ in range(steps):
                     self.step(random_actions=True, autoreset=autoreset, terminal_obs=terminal_obs)
@@ -236,9 +236,24 @@ class HerdBatch:
         self.set_state_raw(d, ints)
 
     def metrics(self, reset=False):
+        """Rollout metric sums (L.METRIC_NAMES) as float64 numpy: one device reduction, a 72-byte copy
+        and a stream sync; raises if a step kernel recorded a device error."""
         out = np.zeros(len(L.METRIC_NAMES), np.float64)
         L.check(L.lib().ch_metrics(self.handle, out.ctypes.data, int(bool(reset)), self._stream()), self.handle)
         return out
+
+    def metrics_device(self, reset=False, out=None):
+        """The same sums into a float64 device tensor on the current stream, no host sync (the input of
+        the end-of-rollout RCCL all-reduce)."""
+        if out is None:
+            out = self.torch.empty(len(L.METRIC_NAMES), dtype=self.torch.float64, device=self.device)
+        L.check(L.lib().ch_metrics_device(self.handle, ctypes.c_void_p(out.data_ptr()), int(bool(reset)),
+                                          self._stream()), self.handle)
+        return out
+
+    def sync(self):
+        """Wait for this batch's stream; raises ChError if a step kernel recorded a device error."""
+        L.check(L.lib().ch_sync(self.handle, self._stream()), self.handle)
 
     def close(self):
         if getattr(self, "handle", None) is not None and self.handle.value:

@@ -31,7 +31,7 @@ struct ch_handle {
     // step (it needs them for the observation anyway) and read by the next one instead of
     // recomputing atan2/asin/atan2; any other writer of the state clears rpy_valid.
     void* rpy = nullptr;
-    bool rpy_valid = false;
+    int* ctl = nullptr;   // device [4]: StepParams::ctl (Euler cache stale, obs bytes unknown, v2 done count)
     void* cattle = nullptr;
     void* phys = nullptr;   // [kPhysComps][E][NC]: last_clipped_action, DYN rpy_rates
     void* envr = nullptr;
@@ -51,6 +51,9 @@ struct ch_handle {
     int G = 1, block = 64, P = 0;
     size_t lds = 0;
     uint16_t* pairs = nullptr;
+    int* errw = nullptr;        // device error word (CH_DEVERR_* bits), sticky
+    double* mdev = nullptr;     // device [CH_METRIC_COUNT + 1]: reduced metrics + error word
+    double* mhost = nullptr;    // pinned host copy of mdev
     std::string err;
 };
 
@@ -151,14 +154,22 @@ static StepParams<R> params(ch_handle* h) {
     p.k0 = (uint32_t)c.seed; p.k1 = (uint32_t)(c.seed >> 32);
     p.env_off = c.env_id_offset;
     p.cs_cc = cattle_spacing_cc();
-    p.drone = (R*)h->drone; p.rpy = (R*)h->rpy; p.rpy_valid = h->rpy_valid; p.cattle = (R*)h->cattle; p.envr = (R*)h->envr; p.envi = h->envi;
+    p.drone = (R*)h->drone; p.rpy = (R*)h->rpy; p.ctl = h->ctl; p.cattle = (R*)h->cattle; p.envr = (R*)h->envr; p.envi = h->envi;
     p.metrics = h->metrics; p.spawn = h->spawn; p.n_scen = h->n_scen; p.n_cows = h->n_cows;
     p.debug = h->debug;
     p.phase_mask = h->phase_mask;
     p.G = h->G; p.P = h->P; p.pairs = h->pairs;
     p.tstamp = h->tstamp;
     p.physics = c.physics; p.gnd_h_clip = gnd_eff_h_clip(); p.phys = (R*)h->phys;
+    p.err = h->errw;
     return p;
+}
+
+// the v2 step's once-per-device function attribute, set outside any stream capture
+static hipError_t prepare_step(ch_handle* h) {
+    if (h->kernel != 2) return hipSuccess;
+    if (h->rsize == sizeof(double)) return launch_step_v2(params<double>(h), h->block, h->lds, nullptr, false);
+    return launch_step_v2(params<float>(h), h->block, h->lds, nullptr, false);
 }
 
 extern "C" {
@@ -207,9 +218,21 @@ int ch_default_config(ch_config* c, int32_t mode, int32_t num_drones, int32_t nu
 const char* ch_last_error(const ch_handle* h) { return h ? h->err.c_str() : g_create_err.c_str(); }
 
 static void free_all(ch_handle* h) {
-    void* ptrs[] = {h->drone, h->rpy, h->cattle, h->phys, h->envr, h->envi, h->metrics, h->spawn, h->pairs};
+    void* ptrs[] = {h->drone, h->rpy, h->cattle, h->phys, h->envr, h->envi, h->metrics, h->spawn, h->pairs,
+                    h->errw, h->mdev, h->ctl};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    if (h->mhost) (void)hipHostFree(h->mhost);
+}
+
+// the sticky device error word as a status (call after the stream has drained)
+static int device_status(ch_handle* h, int word) {
+    if (!word) return CH_OK;
+    return fail(h, CH_ERR_DEVICE,
+                "device error word " + std::to_string(word) +
+                    ((word & CH_DEVERR_HANDOFF) ? ": a step kernel's LDS hand-off timed out (ch_step.hip lds_wait); "
+                                                  "the results of that step are wrong"
+                                                : ""));
 }
 
 int ch_create(const ch_config* c, int64_t n_envs, int32_t device, ch_handle** out) {
@@ -287,6 +310,15 @@ int ch_create(const ch_config* c, int64_t n_envs, int32_t device, ch_handle** ou
     CTRY(hipMalloc(&h->envr, h->rsize * kEnvReal * E));
     CTRY(hipMalloc(&h->envi, sizeof(int) * kEnvInt * E));
     CTRY(hipMalloc(&h->metrics, sizeof(double) * kMetricRows * E));
+    {
+        const int ctl0[4] = {1, 1, 0, 0};   // no Euler cache yet; obs bytes unknown
+        CTRY(hipMalloc(&h->ctl, sizeof(ctl0)));
+        CTRY(hipMemcpy(h->ctl, ctl0, sizeof(ctl0), hipMemcpyHostToDevice));
+    }
+    CTRY(hipMalloc(&h->errw, sizeof(int)));
+    CTRY(hipMemset(h->errw, 0, sizeof(int)));
+    CTRY(hipMalloc(&h->mdev, sizeof(double) * (CH_METRIC_COUNT + 1)));
+    CTRY(hipHostMalloc(&h->mhost, sizeof(double) * (CH_METRIC_COUNT + 1), hipHostMallocDefault));
 
     std::vector<double> table;
     if (c->spawn_table) {
@@ -364,6 +396,7 @@ int ch_create(const ch_config* c, int64_t n_envs, int32_t device, ch_handle** ou
         CTRY(hipMemset(h->metrics, 0, sizeof(double) * kMetricRows * E));
     }
     (void)rc;
+    CTRY(prepare_step(h));
 #undef CTRY
     *out = h;
     return CH_OK;
@@ -402,7 +435,6 @@ int ch_reset(ch_handle* h, const uint8_t* mask_dev, float* obs_dev, void* stream
         e = launch_reset(p, h->team, st);
     }
     if (e != hipSuccess) return fail(h, CH_ERR_DEVICE, std::string("ch_reset launch: ") + hipGetErrorString(e));
-    h->rpy_valid = false;                                        // reset bodies: angles recomputed next step
     if (!mask_dev) h->obs_zero_ptr = obs_dev;                    // every block written in full
     else if (h->obs_zero_ptr != obs_dev) h->obs_zero_ptr = nullptr;   // some blocks of obs_dev unknown
     return CH_OK;
@@ -440,7 +472,6 @@ int ch_step(ch_handle* h, const ch_step_io* io, void* stream) {
     }
     if (e != hipSuccess) return fail(h, CH_ERR_DEVICE, std::string("ch_step launch: ") + hipGetErrorString(e));
     h->obs_zero_ptr = (h->phase_mask & 8) ? nullptr : io->obs;
-    h->rpy_valid = h->kernel == 2 && !(h->phase_mask & 1);   // v2 stored the angles of every live drone
     return CH_OK;
 }
 
@@ -476,7 +507,9 @@ int ch_get_state(ch_handle* h, double* hd, int32_t* hi, void* stream) {
         }
     }
     if (hi) HIP_TRY(h, hipMemcpy(hi, h->envi, sizeof(int) * kEnvInt * h->E, hipMemcpyDeviceToHost));
-    return CH_OK;
+    int word = 0;
+    HIP_TRY(h, hipMemcpy(&word, h->errw, sizeof(int), hipMemcpyDeviceToHost));
+    return device_status(h, word);
 }
 
 int ch_set_state(ch_handle* h, const double* hd, const int32_t* hi, void* stream) {
@@ -485,7 +518,10 @@ int ch_set_state(ch_handle* h, const double* hd, const int32_t* hi, void* stream
     hipStream_t st = (hipStream_t)stream;
     HIP_TRY(h, hipStreamSynchronize(st));
     h->obs_zero_ptr = nullptr;   // NUM_DRONES may change: the next step writes every obs block in full
-    h->rpy_valid = false;
+    {   // the same on the device, for steps replayed from a graph captured earlier
+        const int ctl[2] = {1, 1};
+        HIP_TRY(h, hipMemcpy(h->ctl, ctl, sizeof(ctl), hipMemcpyHostToDevice));
+    }
     const size_t nd = (size_t)kDroneComps * h->E * h->NC, nc = (size_t)kCattleComps * h->E * h->M,
                  nr = (size_t)kEnvReal * h->E, np_ = (size_t)kPhysComps * h->E * h->NC;
     if (hd) {
@@ -518,6 +554,7 @@ int ch__set_kernel(ch_handle* h, int32_t version) {
     if (!h || (version != 1 && version != 2)) return CH_ERR_INVALID;
     if (version == 2 && h->lds > 150 * 1024) return CH_ERR_UNSUPPORTED;
     h->kernel = version;
+    HIP_TRY(h, prepare_step(h));
     return CH_OK;
 }
 
@@ -535,6 +572,7 @@ int ch__set_geometry(ch_handle* h, int32_t G, int32_t block) {
     const size_t lds = V2Layout(G, h->NC, h->M, h->P, h->cfg.mode, (int)h->rsize).bytes();
     if (lds > 150 * 1024) return CH_ERR_UNSUPPORTED;
     h->G = G; h->block = block; h->lds = lds;
+    HIP_TRY(h, prepare_step(h));
     return CH_OK;
 }
 
@@ -551,9 +589,12 @@ int ch__geometry(const ch_handle* h, int32_t* G, int32_t* block, int64_t* lds, i
 /* Internal diagnostics: skip kernel phases (1 drones, 2 flock, 4 task, 8 obs) to attribute time. */
 /* Internal: forget which obs buffer holds valid constant-zero bytes (the caller wrote into it); the
  * next ch_step writes every obs block in full. */
-int ch__obs_invalidate(ch_handle* h) {
+int ch__obs_invalidate(ch_handle* h, void* stream) {
     if (!h) return CH_ERR_INVALID;
     h->obs_zero_ptr = nullptr;
+    // and on the device (ctl[1]), for steps replayed from a graph captured before this call
+    HIP_TRY(h, hipSetDevice(h->device));
+    HIP_TRY(h, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(h->ctl + 1), 1, 1, (hipStream_t)stream));
     return CH_OK;
 }
 
@@ -617,16 +658,28 @@ int ch_metrics(ch_handle* h, double* out, int32_t reset_after, void* stream) {
     if (!h || !out) return fail(h, CH_ERR_INVALID, "ch_metrics: NULL argument");
     HIP_TRY(h, hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
+    // device reduction on the caller's stream, then one 72-byte copy into pinned memory
+    HIP_TRY(h, launch_metrics_reduce(h->metrics, h->E, h->mdev, h->errw, h->mdev + CH_METRIC_COUNT, reset_after, st));
+    HIP_TRY(h, hipMemcpyAsync(h->mhost, h->mdev, sizeof(double) * (CH_METRIC_COUNT + 1), hipMemcpyDeviceToHost, st));
     HIP_TRY(h, hipStreamSynchronize(st));
-    std::vector<double> m((size_t)kMetricRows * h->E);
-    HIP_TRY(h, hipMemcpy(m.data(), h->metrics, m.size() * sizeof(double), hipMemcpyDeviceToHost));
-    for (int r = 0; r < CH_METRIC_COUNT; ++r) {
-        double s = 0;
-        for (int64_t e = 0; e < h->E; ++e) s += m[(size_t)r * h->E + e];
-        out[r] = s;
-    }
-    if (reset_after) HIP_TRY(h, hipMemset(h->metrics, 0, sizeof(double) * CH_METRIC_COUNT * h->E));
+    std::memcpy(out, h->mhost, sizeof(double) * CH_METRIC_COUNT);
+    return device_status(h, (int)h->mhost[CH_METRIC_COUNT]);
+}
+
+int ch_metrics_device(ch_handle* h, double* dev_out, int32_t reset_after, void* stream) {
+    if (!h || !dev_out) return fail(h, CH_ERR_INVALID, "ch_metrics_device: NULL argument");
+    HIP_TRY(h, hipSetDevice(h->device));
+    HIP_TRY(h, launch_metrics_reduce(h->metrics, h->E, dev_out, nullptr, nullptr, reset_after, (hipStream_t)stream));
     return CH_OK;
+}
+
+int ch_sync(ch_handle* h, void* stream) {
+    if (!h) return fail(nullptr, CH_ERR_INVALID, "ch_sync: NULL handle");
+    HIP_TRY(h, hipSetDevice(h->device));
+    HIP_TRY(h, hipStreamSynchronize((hipStream_t)stream));
+    int word = 0;
+    HIP_TRY(h, hipMemcpy(&word, h->errw, sizeof(int), hipMemcpyDeviceToHost));
+    return device_status(h, word);
 }
 
 }  // extern "C"

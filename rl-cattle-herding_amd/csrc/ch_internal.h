@@ -27,8 +27,11 @@ struct StepParams {
     long long env_off;
     double cs_cc;   // CattleSpacingRewardFunction continuation constant (host-evaluated)
     R* drone;       // [22][E][NC]
-    R* rpy;         // v2: [3][E][NC] Euler angles of the stored quaternion (valid iff rpy_valid)
-    int rpy_valid;
+    R* rpy;         // v2: [3][E][NC] Euler angles of the stored quaternion (valid unless ctl[0])
+    // device control words of the handle, read by the v2 step at its start (so a captured HIP graph
+    // sees state changes made after capture): [0] the Euler cache is stale, [1] the constant-zero
+    // observation bytes are unknown, [2] v2 workgroups finished (the last one clears [0] and [1])
+    int* ctl;
     R* cattle;      // [4][E][M]
     R* envr;        // [2][E]
     int* envi;      // [10][E]
@@ -55,7 +58,13 @@ struct StepParams {
     int physics;              // CH_PHYS_* (v1 kernel only; ch_api.cpp selects v1 for the variants)
     double gnd_h_clip;        // GND_EFF_H_CLIP (BaseAviary.py:173)
     R* phys;                  // [kPhysComps][E][NC]
+    int* err;                 // device error word of the handle (CH_DEVERR_* bits), read by ch_sync & co.
 };
+
+// device error word bits (ch_api.cpp reports them as CH_ERR_DEVICE)
+constexpr int CH_DEVERR_HANDOFF = 1;       // a v2 LDS hand-off wait ran out of spins (ch_step.hip lds_wait)
+// diagnostics phase_mask bits beyond 1/2/4/8 (skip drones / flock / task / obs)
+constexpr int CH_PHASE_FORCE_TIMEOUT = 64; // test only: the drone wave waits for a hand-off that never comes
 
 // one curriculum level (curriculum_learning.py:10-194); the table kLevels lives in ch_device.h
 struct Level {
@@ -114,8 +123,16 @@ struct MlpArgs {
 size_t mlp_lds_bytes();
 hipError_t launch_mlp(const MlpArgs& a, hipStream_t st);
 
+// ch_aux.hip: metric rows [kMetricRows][E] -> out[CH_METRIC_COUNT] (sums over envs, fixed order);
+// `err_word` (optional) is copied to err_out as a double; reset zeroes the summed rows
+hipError_t launch_metrics_reduce(double* metrics, long long E, double* out, const int* err_word, double* err_out,
+                                 int reset, hipStream_t st);
+
 template <class R> hipError_t launch_step(const StepParams<R>& p, int team, hipStream_t st);
 template <class R> hipError_t launch_reset(const StepParams<R>& p, int team, hipStream_t st);
-template <class R> hipError_t launch_step_v2(const StepParams<R>& p, int block, size_t lds, hipStream_t st);
+// launch = false only performs the once-per-device function-attribute opt-in (at ch_create, so that a
+// step captured into a HIP graph needs no host-side setup)
+template <class R> hipError_t launch_step_v2(const StepParams<R>& p, int block, size_t lds, hipStream_t st,
+                                             bool launch = true);
 
 }  // namespace ch

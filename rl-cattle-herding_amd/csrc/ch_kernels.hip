@@ -408,10 +408,12 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
                 const int lvl0 = level;
                 R rout[kNMax];
                 uint8_t tout[kNMax], trout[kNMax];
-                auto trunc_i = [&](int i) -> bool {
-                    return (S.dflags[i] & (F_ALT | F_COLL | F_ISO)) || cent > R(kMissionBoundary) || time_up;
+                // the wrapper sees step_counter after env.step's += 1 (rllib_envs/BaseAviary.py:436)
+                const bool time_up_w = (double)(sc + 1) / p.ctrl_freq > p.episode_len;
+                auto trunc_i = [&](int i, bool tu) -> bool {
+                    return (S.dflags[i] & (F_ALT | F_COLL | F_ISO)) || cent > R(kMissionBoundary) || tu;
                 };
-                auto reward_i = [&](int i) -> R {
+                auto reward_i = [&](int i, bool tu) -> R {
                     const Level& L = kLevels[level];
                     R a = S.pa[i], b = S.pb[i];
                     R sa, sb, ca, cb;
@@ -436,22 +438,22 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
                         R eor = marl_end_of_episode(kLevels, level, a, b, cent, eff, norm2(scx - S.dx[i], scy - S.dy[i]), n);
                         r += eor;
                         curriculum_success(kLevels, level, tally);
-                    } else if (trunc_i(i)) {
+                    } else if (trunc_i(i, tu)) {
                         r -= R(50);
                     }
                     return r;
                 };
                 R r1[kNMax];
                 uint8_t d1[kNMax];
-                for (int i = 0; i < n; ++i) r1[i] = reward_i(i);
+                for (int i = 0; i < n; ++i) r1[i] = reward_i(i, time_up);
                 for (int i = 0; i < n; ++i) d1[i] = term_call(kLevels, level, clock, inc, ms, cent, eff);
                 for (int i = 0; i < p.NC; ++i) { rout[i] = R(NAN); tout[i] = 0; trout[i] = 0; }
                 if (p.marl_wrapper) {
                     for (int i = 0; i < n; ++i) {
                         if (!((active >> i) & 1)) continue;
-                        rout[i] = reward_i(i);
+                        rout[i] = reward_i(i, time_up_w);
                         tout[i] = term_call(kLevels, level, clock, inc, ms, cent, eff);
-                        trout[i] = trunc_i(i);
+                        trout[i] = trunc_i(i, time_up_w);
                     }
                     int live = 0;
                     for (int i = 0; i < n; ++i)
@@ -462,7 +464,7 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
                     // bare env.step dicts; done = done["__all__"] = all(done.values())
                     done = 1;
                     for (int i = 0; i < n; ++i) {
-                        rout[i] = r1[i]; tout[i] = d1[i]; trout[i] = trunc_i(i);
+                        rout[i] = r1[i]; tout[i] = d1[i]; trout[i] = trunc_i(i, time_up);
                         done &= tout[i];
                     }
                 }
@@ -539,8 +541,11 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
     __syncthreads();
 
     // ---- observation + scalars back to HBM --------------------------------------------------
-    const bool write = valid && (!RESET_ONLY || do_reset) && !(p.phase_mask & 8);
-    if (write) write_obs(p.obs + (long long)e * p.rows * 86, p.rows, S, t, m_obs, cat_off);
+    const bool write = valid && (!RESET_ONLY || do_reset);
+    if (write && !(p.phase_mask & 8)) write_obs(p.obs + (long long)e * p.rows * 86, p.rows, S, t, m_obs, cat_off);
+    // this kernel does not keep the Euler-angle cache of the v2 step: mark it stale (every block
+    // stores the same word; the v2 step reads it at its start)
+    if (threadIdx.x == 0 && p.ctl) p.ctl[0] = 1;
     if (write && t == 0) {
         p.envi[0 * E + e] = n; p.envi[1 * E + e] = sc; p.envi[2 * E + e] = scA; p.envi[3 * E + e] = has_prev;
         p.envi[4 * E + e] = level; p.envi[5 * E + e] = tally; p.envi[6 * E + e] = spawn; p.envi[7 * E + e] = active;

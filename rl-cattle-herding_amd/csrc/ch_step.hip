@@ -23,6 +23,8 @@
 // (rare) run after the second barrier.  The SoA state layout is shared with ch_kernels.hip.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include "ch_common.h"
 #include "ch_device.h"
 #include "ch_internal.h"
@@ -74,14 +76,20 @@ __device__ __forceinline__ void lds_signal(int* f) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(f, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// spin until *f >= target (bounded: a broken hand-off ends the kernel with wrong data, never a hang)
 __device__ __forceinline__ int lds_peek(int* f) {
     return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-__device__ __forceinline__ void lds_wait(int* f, int target) {
+// a hand-off that never completed: the kernel goes on (never a hang) and the handle's device error
+// word records it; ch_metrics / ch_get_state / ch_sync return CH_ERR_DEVICE from then on
+__device__ __forceinline__ void handoff_failed(int* err) {
+    if (err && (threadIdx.x & 63) == 0) atomicOr(err, CH_DEVERR_HANDOFF);
+}
+// spin until *f >= target (bounded, about 0.1 s)
+__device__ __forceinline__ void lds_wait(int* f, int target, int* err) {
     int spins = 0;
     while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target && ++spins < (1 << 22))
         __builtin_amdgcn_s_sleep(1);
+    if (spins >= (1 << 22)) handoff_failed(err);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
@@ -97,10 +105,10 @@ __device__ __forceinline__ int grab(int* ctr, int n) {
 
 // barrier among the cow waves only (the drone wave keeps running); `global` also publishes their
 // global stores (needed before other cow lanes rewrite the same state)
-__device__ __forceinline__ void cow_sync(int* f, int waves, bool global) {
+__device__ __forceinline__ void cow_sync(int* f, int waves, bool global, int* err) {
     if (global) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     lds_signal(f);
-    lds_wait(f, waves);
+    lds_wait(f, waves, err);
     if (global) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
@@ -375,7 +383,9 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
     R ph_lr[4] = {0, 0, 0, 0}, ph_rr[3] = {0, 0, 0};   // PHYS: last_clipped_action, DYN rpy_rates
     int stepi = 0, n0 = 0, act0 = 0;
     R spx_r[3] = {0, 0, 0}, spy_r[3] = {0, 0, 0};   // cow waves: prefetched spawn positions
+    bool rpy_valid = false;
     if (tid < 64) {
+        rpy_valid = p.ctl[0] == 0;
         // the drone wave loads only what its chain reads, so the chain starts after one round trip; the
         // cow waves stage the env scalars, the curriculum table and the pair list meanwhile
         __builtin_amdgcn_s_setprio(3);   // the drone wave is the critical path: it wins issue on a shared SIMD
@@ -389,7 +399,7 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
             for (int c = 0; c < 3; ++c) { v[c] = p.drone[(7 + c) * DS + di]; w[c] = p.drone[(10 + c) * DS + di]; }
 #pragma unroll
             for (int c = 0; c < 9; ++c) pid[c] = p.drone[(13 + c) * DS + di];
-            if (p.rpy_valid) {   // Euler angles of this quaternion, stored by the previous step
+            if (rpy_valid) {   // Euler angles of this quaternion, stored by the previous step
 #pragma unroll
                 for (int c = 0; c < 3; ++c) rpy_in[c] = p.rpy[c * DS + di];
             }
@@ -438,7 +448,7 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
         if (flk) ei[FL_LIST + __popcll(bal & ((1ull << ct) - 1ull))] = g;
         if (ct == 0) { ei[NF_AT] = __popcll(bal); ei[NR_AT] = 0; }
         }
-        cow_sync(fl + F_E, W1, false);   // env scalars, flocking list, tables: seen by every cow wave
+        cow_sync(fl + F_E, W1, false, p.err);   // env scalars, flocking list, tables: seen by every cow wave
         if (ct == 0) TS(11, (long long)clock64());
         // spawn positions of the episode an auto-reset would start: scenario index + 1 (BaseAviary.py:600-606).
         // Loaded into registers here and parked in LDS after the pair loop, so the load latency hides
@@ -484,7 +494,7 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
             if (marl && !((act0 >> dk) & 1)) { a[0] = a[1] = a[2] = a[3] = 0.0f; }  // marl_wrapper.py:80-84
             R Rm[9], rpy[3];
             quat_to_mat(q, Rm);
-            if (p.rpy_valid) { rpy[0] = rpy_in[0]; rpy[1] = rpy_in[1]; rpy[2] = rpy_in[2]; }
+            if (rpy_valid) { rpy[0] = rpy_in[0]; rpy[1] = rpy_in[1]; rpy[2] = rpy_in[2]; }
             else quat_to_euler(q, rpy);
             if (!(p.phase_mask & 1)) {
                 R rpm[4];
@@ -521,7 +531,7 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
         }
         if (live && wobs) obs_own(obs_wg + dg * RW, dk, pos[2], rpy_out, v, w);
         if (tid == 0) TS(4, (long long)clock64());
-        lds_wait(fl + F_E, W1);   // env scalars and the curriculum table (staged by the cow waves)
+        lds_wait(fl + F_E, W1, p.err);   // env scalars and the curriculum table (staged by the cow waves)
 
         // per-drone reward terms (CattleAviary.py:230-246, 572-679) and neighbour obs (BaseRLAviary.py:303-317)
         if (live && task) {
@@ -556,7 +566,7 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
         }
         lds_signal(fl + F_T);
         if (tid == 0) TS(5, (long long)clock64());
-        lds_wait(fl + F_H, W1);
+        lds_wait(fl + F_H, W1 + ((p.phase_mask & CH_PHASE_FORCE_TIMEOUT) ? 1 : 0), p.err);
         if (tid == 0) TS(6, (long long)clock64());
         if (live && task) {
             // closest cow (CattleAviary.py:248-252) from the cow waves' distance table -> cattle term
@@ -636,10 +646,14 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
                 R& clock = f_clock;
                 const R inc = R(1.0) / R(p.ctrl_freq);
                 const int lvl0 = level;
-                auto trunc_i = [&](int i) -> bool {
-                    return (S.dflags[b0 + i] & 7) || cent > R(kMissionBoundary) || time_up;
+                // env.step counts its step (step_counter += 1, rllib_envs/BaseAviary.py:436) between its
+                // own dicts and the wrapper's recomputation, so the wrapper sees the time limit one step
+                // earlier (MARLCattleAviary.py:376)
+                const bool time_up_w = (double)(f_sc + 1) / p.ctrl_freq > p.episode_len;
+                auto trunc_i = [&](int i, bool tu) -> bool {
+                    return (S.dflags[b0 + i] & 7) || cent > R(kMissionBoundary) || tu;
                 };
-                auto reward_i = [&](int i) -> R {
+                auto reward_i = [&](int i, bool tu) -> R {
                     const Level& Lv = LT[level];
                     R a = S.pa[b0 + i], b = S.pb[b0 + i];
                     R sa, sb, ca, cb;
@@ -662,13 +676,13 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
                     if (term_call(LT, level, clock, inc, ms, cent, eff)) {
                         r += marl_end_of_episode(LT, level, a, b, cent, eff, norm2(scx - S.dx[b0 + i], scy - S.dy[b0 + i]), n);
                         curriculum_success(LT, level, tally);
-                    } else if (trunc_i(i)) {
+                    } else if (trunc_i(i, tu)) {
                         r -= R(50);
                     }
                     return r;
                 };
                 // env.step's own dicts (rllib_envs/BaseAviary.py:425-431)
-                for (int i = 0; i < n; ++i) S.mrew[b0 + i] = reward_i(i);
+                for (int i = 0; i < n; ++i) S.mrew[b0 + i] = reward_i(i, time_up);
                 for (int i = 0; i < n; ++i) S.md1[b0 + i] = term_call(LT, level, clock, inc, ms, cent, eff);
                 const int act0 = active;
                 if (p.marl_wrapper) {
@@ -678,9 +692,9 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
                         R rr = R(NAN);
                         uint8_t tt = 0, trr = 0;
                         if (i < n && ((act0 >> i) & 1)) {
-                            rr = reward_i(i);
+                            rr = reward_i(i, time_up_w);
                             tt = term_call(LT, level, clock, inc, ms, cent, eff);
-                            trr = trunc_i(i);
+                            trr = trunc_i(i, time_up_w);
                         }
                         p.reward[(long long)e * N + i] = (float)rr;
                         p.term[(long long)e * N + i] = tt;
@@ -697,7 +711,7 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
                     for (int i = 0; i < N; ++i) {
                         R rr = R(NAN);
                         uint8_t tt = 0, trr = 0;
-                        if (i < n) { rr = S.mrew[b0 + i]; tt = S.md1[b0 + i]; trr = trunc_i(i); done &= tt; }
+                        if (i < n) { rr = S.mrew[b0 + i]; tt = S.md1[b0 + i]; trr = trunc_i(i, time_up); done &= tt; }
                         p.reward[(long long)e * N + i] = (float)rr;
                         p.term[(long long)e * N + i] = tt;
                         p.trunc[(long long)e * N + i] = trr;
@@ -797,7 +811,7 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
         }
         // the constant-zero bytes of the observation blocks, when the host cannot vouch that this buffer
         // already holds them (first step into a buffer, after ch_set_state, ...; ch_api.cpp obs_zero_ptr)
-        if (wobs && p.obs_full)
+        if (wobs && (p.obs_full || p.ctl[1]))
             for (int g = 0; g < Gv; ++g) obs_zero_env(obs_wg + g * RW, ei[I_N * G + g], rows, cat_off, m_obs, ct, CW);
         lds_signal(fl + F_A);
         const float rM = 1.0f / (float)M;
@@ -820,7 +834,7 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
             CHUNK_T1(2);
         }
         if (ct == 0) TS(8, (long long)clock64());
-        lds_wait(fl + F_D, 1);
+        lds_wait(fl + F_D, 1, p.err);
         if (ct == 0) TS(9, (long long)clock64());
         for (;;) {   // per cow: distances, winding number, observation entries; then per env: herd centroid
             const int b = grab(fl + C_COWS, 64), u = b + lane;
@@ -861,7 +875,7 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
         }
         lds_signal(fl + F_H);
         // the alpha rows only feed the velocity update: they wait until the drone wave has its hand-off
-        lds_wait(fl + F_A, W1);   // every pair of the table
+        lds_wait(fl + F_A, W1, p.err);   // every pair of the table
         if (ct == 0) TS(20, (long long)clock64());
         for (;;) {   // alpha rows of the cows of flocking envs
             const int b = grab(fl + C_ROWS, 64), u = b + lane;
@@ -873,7 +887,7 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
             }
             CHUNK_T1(2);
         }
-        cow_sync(fl + F_W, W1, false);   // every alpha row read the pair table: its space now takes the drone terms
+        cow_sync(fl + F_W, W1, false, p.err);   // every alpha row read the pair table: its space now takes the drone terms
         if (ct == 0) TS(21, (long long)clock64());
         const int T = G * M * N, MN = M * N;
         const float rMN = 1.0f / (float)MN, rN = 1.0f / (float)N;
@@ -902,7 +916,7 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
         }
         if (ct == 0) TS(16, (long long)clock64());
         if (!fuse) {
-            cow_sync(fl + F_Q, W1, false);   // every drone term of every cow
+            cow_sync(fl + F_Q, W1, false, p.err);   // every drone term of every cow
             if (ct == 0) TS(17, (long long)clock64());
             for (;;) {   // cows of flocking envs only
                 const int b = grab(fl + C_FLOCK, 64), u = b + lane;
@@ -917,7 +931,7 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
         }
         if (lane == 0) TS(40 + (tid >> 6), (long long)clock64());   // this cow wave's flock work done
         if (ct == 0) TS(31, (long long)nf);
-        lds_wait(fl + F_R, 1);    // the reset list
+        lds_wait(fl + F_R, 1, p.err);    // the reset list
         const int nr = ei[NR_AT];
         if (nr) {   // uniform across the cow waves
             // ---- SB3 auto-reset of the listed envs (BaseAviary.reset, BaseAviary.py:280-331), rebuilt from
@@ -925,13 +939,13 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
             // computes rewards: R1 bodies + own-state rows, R2 neighbour and cattle entries, R3 copy.
             const int* rl = ei + RS_LIST;
             if (p.terminal_obs) {   // info["terminal_observation"]: the pre-reset observation, from HBM
-                cow_sync(fl + F_X0, W1, true);   // every cow wave's observation stores of this step are visible
+                cow_sync(fl + F_X0, W1, true, p.err);   // every cow wave's observation stores of this step are visible
                 for (int q = ct; q < nr * (RW >> 1); q += CW) {
                     const int k = q / (RW >> 1), o = rl[k] * (RW >> 1) + (q - k * (RW >> 1));
                     reinterpret_cast<float2*>(p.terminal_obs + (long long)e0 * RW)[o] = reinterpret_cast<const float2*>(obs_wg)[o];
                 }
             }
-            cow_sync(fl + F_X1, W1, true);   // terminal observation read; flock stores to the cattle state done
+            cow_sync(fl + F_X1, W1, true, p.err);   // terminal observation read; flock stores to the cattle state done
             for (int u = ct; u < nr * N; u += CW) {
                 const int k0 = qdiv(u, N, rN), g = rl[k0], k = u - k0 * N, ud = g * N + k;
                 const int n = reset_draw_n(p, ei[I_EPISODE * G + g], p.env_off + e0 + g);
@@ -966,7 +980,7 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
                              (uint32_t)ei[I_EPISODE * G + g], x, y, vx, vy);
                 S.cx[uc] = x; S.cy[uc] = y;
             }
-            cow_sync(fl + F_X2, W1, false);
+            cow_sync(fl + F_X2, W1, false, p.err);
             if (wobs) {
                 for (int u = ct; u < nr * N; u += CW) {
                     const int k0 = qdiv(u, N, rN), g = rl[k0], i = u - k0 * N;
@@ -987,7 +1001,7 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
     if (tid == 0) TS(13, (long long)clock64());
 
     // ---- env scalars back to HBM (the drone wave's env lanes hold them) -----------------------------
-    if (tid < Gv && wobs) {
+    if (tid < Gv) {
         const int e = e0 + tid;
         p.envi[0 * E + e] = f_n; p.envi[1 * E + e] = f_sc; p.envi[2 * E + e] = f_scA; p.envi[3 * E + e] = f_hp;
         p.envi[4 * E + e] = f_level; p.envi[5 * E + e] = f_tally; p.envi[6 * E + e] = f_spawn;
@@ -995,18 +1009,30 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
         p.envi[9 * E + e] += 1;   // ch_step calls on this env
         p.envr[0 * E + e] = f_prev; p.envr[1 * E + e] = f_clock;
     }
+    // the last workgroup to finish clears the control words: every workgroup read them at its start
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const unsigned done = atomicAdd(reinterpret_cast<unsigned*>(p.ctl + 2), 1u);
+        if (done == gridDim.x - 1) { p.ctl[0] = 0; p.ctl[1] = 0; p.ctl[2] = 0; }
+    }
     if (tid == 0) { TS(14, (long long)clock64()); TS(1, (long long)wall_clock64()); }
 }
 
 template <class R, int MODE, int GT, int NT, int MT, bool PHYS = false>
-static hipError_t launch_v2_kernel(const StepParams<R>& p, int block, size_t lds, hipStream_t st) {
-    static bool attr_set = false;   // one-time opt-in to > 64 KiB of dynamic LDS
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_step2<R, MODE, GT, NT, MT, PHYS>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+static hipError_t launch_v2_kernel(const StepParams<R>& p, int block, size_t lds, hipStream_t st, bool launch) {
+    // opt-in to > 64 KiB of dynamic LDS, once per device (the attribute is per device context)
+    static std::atomic<unsigned long long> attr_set{0};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const unsigned long long bit = 1ull << (dev & 63);
+    if (!(attr_set.load(std::memory_order_relaxed) & bit)) {
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_step2<R, MODE, GT, NT, MT, PHYS>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
-        attr_set = true;
+        attr_set.fetch_or(bit, std::memory_order_relaxed);
     }
+    if (!launch) return hipSuccess;
     dim3 grid((p.E + p.G - 1) / p.G);
     hipLaunchKernelGGL((k_step2<R, MODE, GT, NT, MT, PHYS>), grid, dim3(block), lds, st, p);
     return hipGetLastError();
@@ -1014,25 +1040,25 @@ static hipError_t launch_v2_kernel(const StepParams<R>& p, int block, size_t lds
 
 // geometry specialisations: the BASELINE configs at their default geometry (ch_api.cpp)
 template <class R>
-hipError_t launch_step_v2(const StepParams<R>& p, int block, size_t lds, hipStream_t st) {
+hipError_t launch_step_v2(const StepParams<R>& p, int block, size_t lds, hipStream_t st, bool launch) {
     const int G = p.G, N = p.NC, M = p.M;
     if (p.physics != CH_PHYS_PYB) {   // physics variants (BaseAviary.py:420-450): runtime-geometry instantiation
-        if (p.mode == 1) return launch_v2_kernel<R, 1, 0, 0, 0, true>(p, block, lds, st);
-        if (G == 16 && N == 4 && M == 16) return launch_v2_kernel<R, 0, 16, 4, 16, true>(p, block, lds, st);   // configs[3]
-        return launch_v2_kernel<R, 0, 0, 0, 0, true>(p, block, lds, st);
+        if (p.mode == 1) return launch_v2_kernel<R, 1, 0, 0, 0, true>(p, block, lds, st, launch);
+        if (G == 16 && N == 4 && M == 16) return launch_v2_kernel<R, 0, 16, 4, 16, true>(p, block, lds, st, launch);   // configs[3]
+        return launch_v2_kernel<R, 0, 0, 0, 0, true>(p, block, lds, st, launch);
     }
     if (p.mode == 1) {
-        if (G == 4 && N == 4 && M == 32) return launch_v2_kernel<R, 1, 4, 4, 32>(p, block, lds, st);     // configs[4]
-        return launch_v2_kernel<R, 1, 0, 0, 0>(p, block, lds, st);
+        if (G == 4 && N == 4 && M == 32) return launch_v2_kernel<R, 1, 4, 4, 32>(p, block, lds, st, launch);     // configs[4]
+        return launch_v2_kernel<R, 1, 0, 0, 0>(p, block, lds, st, launch);
     }
-    if (G == 8 && N == 4 && M == 16) return launch_v2_kernel<R, 0, 8, 4, 16>(p, block, lds, st);          // configs[3]
-    if (G == 16 && N == 4 && M == 16) return launch_v2_kernel<R, 0, 16, 4, 16>(p, block, lds, st);         // configs[3], 512 threads
-    if (G == 16 && N == 2 && M == 8) return launch_v2_kernel<R, 0, 16, 2, 8>(p, block, lds, st);          // configs[2]
-    if (G == 4 && N == 2 && M == 8) return launch_v2_kernel<R, 0, 4, 2, 8>(p, block, lds, st);            // configs[1]
-    return launch_v2_kernel<R, 0, 0, 0, 0>(p, block, lds, st);
+    if (G == 8 && N == 4 && M == 16) return launch_v2_kernel<R, 0, 8, 4, 16>(p, block, lds, st, launch);          // configs[3]
+    if (G == 16 && N == 4 && M == 16) return launch_v2_kernel<R, 0, 16, 4, 16>(p, block, lds, st, launch);         // configs[3], 512 threads
+    if (G == 16 && N == 2 && M == 8) return launch_v2_kernel<R, 0, 16, 2, 8>(p, block, lds, st, launch);          // configs[2]
+    if (G == 4 && N == 2 && M == 8) return launch_v2_kernel<R, 0, 4, 2, 8>(p, block, lds, st, launch);            // configs[1]
+    return launch_v2_kernel<R, 0, 0, 0, 0>(p, block, lds, st, launch);
 }
 
-template hipError_t launch_step_v2<double>(const StepParams<double>&, int, size_t, hipStream_t);
-template hipError_t launch_step_v2<float>(const StepParams<float>&, int, size_t, hipStream_t);
+template hipError_t launch_step_v2<double>(const StepParams<double>&, int, size_t, hipStream_t, bool);
+template hipError_t launch_step_v2<float>(const StepParams<float>&, int, size_t, hipStream_t, bool);
 
 }  // namespace ch

@@ -371,7 +371,7 @@ def gen_task_marl(rng):
                 _inject(env, dxyz, cows)
                 if it % 4 == 0:
                     env.prev_cent_dists = None
-                env.step_counter = int(rng.choice([0, 600, 2400, 2401]))
+                env.step_counter = int(rng.choice([0, 600, 2399, 2400, 2401]))
                 if lvl in (0, 1) and it % 3 == 1:
                     env.drone_spacing_clock = env.curriculum.current_curriculum["drone_spacing_hold_timer"] - 3 / 60
                 if it % 5 == 4:
@@ -386,6 +386,7 @@ def gen_task_marl(rng):
                         env._computeTerminated(i)
                     for i in range(env.NUM_DRONES):
                         env._computeTruncated(i)
+                    env.step_counter += 1   # rllib_envs/BaseAviary.py:436, before the wrapper's calls
                     # the wrapper's recomputation (returned values)
                     r = np.full(NMAX, np.nan); d = np.zeros(NMAX, np.uint8); t = np.zeros(NMAX, np.uint8)
                     for aid in list(w.agents):
@@ -586,6 +587,9 @@ def main():
 if __name__ == "__main__":
     if "--physics" in sys.argv:   # the physics-variant fixtures only (own seeds)
         gen_physics()
+    elif "--task-marl" in sys.argv:   # task_marl.npz only, own seed (regenerated for the step_counter order)
+        np.random.seed(12345)
+        gen_task_marl(np.random.default_rng(20261016))
     else:
         main()
         gen_physics()

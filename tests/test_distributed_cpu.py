@@ -82,3 +82,34 @@ def test_env_offset_and_world_defaults(monkeypatch):
     assert D.env_offset(3, 4096) == 3 * 4096
     sums, t = D.reduce_rollout(np.arange(4.0), 2.5)   # no process group: identity
     assert np.array_equal(sums, np.arange(4.0)) and t == 2.5
+
+
+def _bench(args, env=None):
+    import json
+    import subprocess
+    e = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], env=e, capture_output=True,
+                       text=True, timeout=240)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r.returncode, (json.loads(lines[-1]) if lines else None), r.stderr
+
+
+def test_bench_gpus_n_spawns_n_ranks():
+    """`python bench.py --gpus 2` (the entry point the driver calls) starts two rank processes itself
+    (cattleherd.launch) and the process group sees both; --launch-check runs that plumbing on gloo with
+    no GPU: world size, disjoint env ranges (CTDECattleHerder.py:91-97 sharding), the all-reduce."""
+    rc, out, err = _bench(["--gpus", "2", "--launch-check", "--backend", "gloo"])
+    assert rc == 0, err
+    assert out["n_gpus"] == 2 and out["env_ranges"] == [[0, 4096], [4096, 8192]]
+    assert out["metric_sum"] == 3.0 and out["max_time"] == 1.5
+
+
+def test_bench_world_size_mismatch_fails():
+    """--gpus N that disagrees with the launcher's WORLD_SIZE exits non-zero instead of reporting a
+    single-GPU run as N GPUs."""
+    rc, out, err = _bench(["--gpus", "2", "--launch-check", "--backend", "gloo"], env={"WORLD_SIZE": "1"})
+    assert rc == 3 and out is None
+    assert "process group has 1 ranks" in err

@@ -1,0 +1,118 @@
+"""GPU tests of the runtime around the step kernel (through the C ABI): HIP-graph replay against
+eager steps across reset/set_state/invalidate_obs, the device metric reduction against a host sum
+of the per-env rows, and the sticky device error word of a failed LDS hand-off.
+
+Reference anchors: the metrics are BaseAviary.update_evaluation_metrics' aggregate
+(sb3_envs/BaseAviary.py:1406-1435); the error path stands in for an exception out of env.step
+(marl_wrapper.py:87-95)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(mode, n, m, E, **kw):
+    from cattleherd.env import HerdBatch
+    return [HerdBatch(E, n, m, mode=mode, **kw) for _ in range(2)]
+
+
+def _outs(h):
+    return [x.clone() for x in (h.obs, h.reward, h.terminated, h.truncated, h.reset_happened)]
+
+
+def _same(a, b):
+    import torch
+    return all(torch.equal(torch.nan_to_num(x.float(), nan=7.0), torch.nan_to_num(y.float(), nan=7.0))
+               for x, y in zip(a, b))
+
+
+@pytest.mark.parametrize("mode,n,m,E", [("ctde", 4, 16, 4096), ("marl", 3, 8, 300), ("ctde", 6, 16, 257)])
+def test_graph_replay_equals_eager_across_state_changes(mode, n, m, E):
+    """A graph captured once keeps matching eager steps after reset(), set_state() and
+    invalidate_obs(): the Euler cache and the constant observation bytes are device words the
+    kernel reads at run time (ch_internal.h StepParams::ctl), not values baked in at capture."""
+    import torch
+    K = 7
+    eager, gr = _pair(mode, n, m, E, min_drones=2, max_drones=n)
+    for h in (eager, gr):
+        h.reset()
+    graph = gr.capture_rollout(K, terminal_obs=False)
+    for rnd in range(6):
+        for _ in range(K):
+            eager.step(random_actions=True, autoreset=True, terminal_obs=False)
+        graph.replay()
+        torch.cuda.synchronize()
+        assert _same(_outs(eager), _outs(gr)), rnd
+        s1, s2 = eager.get_state(), gr.get_state()
+        for k in s1:
+            assert np.array_equal(np.nan_to_num(s1[k]), np.nan_to_num(s2[k])), (rnd, k)
+        if rnd == 1:
+            for h in (eager, gr):
+                h.reset()
+        if rnd == 2:   # perturbed state injected into both (NUM_DRONES changes: dead rows move)
+            s = eager.get_state()
+            s["drone_quat"] = s["drone_quat"] + 1e-3
+            s["drone_quat"] /= np.linalg.norm(s["drone_quat"], axis=-1, keepdims=True)
+            s["n"] = np.where(np.arange(E) % 2 == 0, 2, n).astype(np.int32)
+            s["active_mask"] = (1 << s["n"]) - 1
+            for h in (eager, gr):
+                h.set_state(s)
+        if rnd == 3:
+            for h in (eager, gr):
+                h.obs.fill_(5.0)
+                h.invalidate_obs()
+    for h in (eager, gr):
+        h.close()
+
+
+def test_device_metrics_equal_host_sum_of_rows():
+    """ch_metrics (device reduction + pinned copy) and ch_metrics_device agree with each other and
+    with the metric rows summed on the host; reset_after zeroes the summed rows only."""
+    import torch
+    from cattleherd import _lib
+    from cattleherd.env import HerdBatch
+    E = 1000
+    b = HerdBatch(E, 4, 16, mode="ctde", curriculum_level=2)
+    b.reset()
+    for _ in range(700):   # level 2 terminates on approach: episodes end inside the rollout
+        b.step(random_actions=True, autoreset=True, terminal_obs=False)
+    dev = b.metrics_device(reset=False)
+    host = b.metrics(reset=False)
+    torch.cuda.synchronize()
+    assert np.array_equal(dev.cpu().numpy(), host)
+    assert host[_lib.METRIC_NAMES.index("steps")] == E * 700 and host[1] > 0
+    first = b.metrics(reset=True)
+    assert np.array_equal(first, host)
+    again = b.metrics(reset=False)
+    assert np.all(again == 0)
+    b.step(random_actions=True, autoreset=True, terminal_obs=False)
+    assert b.metrics()[0] == E
+    b.close()
+
+
+def test_handoff_timeout_is_reported_not_silent():
+    """A step whose LDS hand-off never completes (forced with the diagnostics phase bit 64) still
+    ends -- every wait is bounded -- and the handle then reports CH_ERR_DEVICE from ch_sync and
+    ch_metrics instead of returning wrong data silently.  A healthy handle reports nothing."""
+    import torch
+    from cattleherd import _lib
+    from cattleherd.env import HerdBatch
+    ok = HerdBatch(512, 4, 16, mode="ctde")
+    bad = HerdBatch(512, 4, 16, mode="ctde")
+    for h in (ok, bad):
+        h.reset()
+    assert _lib.lib().ch__set_phase_mask(bad.handle, ctypes.c_int32(64)) == 0
+    for h in (ok, bad):
+        h.step(random_actions=True)
+    ok.sync()
+    ok.metrics()
+    with pytest.raises(_lib.ChError) as ei:
+        bad.sync()
+    assert ei.value.code == _lib.CH_ERR_DEVICE and "hand-off" in str(ei.value)
+    with pytest.raises(_lib.ChError):
+        bad.metrics()
+    torch.cuda.synchronize()
+    for h in (ok, bad):
+        h.close()
