@@ -399,10 +399,10 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
             for (int c = 0; c < 3; ++c) { v[c] = p.drone[(7 + c) * DS + di]; w[c] = p.drone[(10 + c) * DS + di]; }
 #pragma unroll
             for (int c = 0; c < 9; ++c) pid[c] = p.drone[(13 + c) * DS + di];
-            if (rpy_valid) {   // Euler angles of this quaternion, stored by the previous step
+            // Euler angles of this quaternion, stored by the previous step (used iff the cache is
+            // valid; loaded regardless so the loads issue with the state's, not after ctl returns)
 #pragma unroll
-                for (int c = 0; c < 3; ++c) rpy_in[c] = p.rpy[c * DS + di];
-            }
+            for (int c = 0; c < 3; ++c) rpy_in[c] = p.rpy[c * DS + di];
             stepi = p.envi[9 * E + e0 + dg];   // ch_step calls on this env so far: the Philox action counter
             if constexpr (PHYS) {
 #pragma unroll
@@ -1010,8 +1010,8 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
         p.envr[0 * E + e] = f_prev; p.envr[1 * E + e] = f_clock;
     }
     // the last workgroup to finish clears the control words: every workgroup read them at its start
+    // (every read of ctl in this workgroup was consumed before the barrier above)
     if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         const unsigned done = atomicAdd(reinterpret_cast<unsigned*>(p.ctl + 2), 1u);
         if (done == gridDim.x - 1) { p.ctl[0] = 0; p.ctl[1] = 0; p.ctl[2] = 0; }
     }
