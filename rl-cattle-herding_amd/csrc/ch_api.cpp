@@ -49,6 +49,7 @@ struct ch_handle {
     int kernel = 2;
     long long* tstamp = nullptr;
     int G = 1, block = 64, P = 0;
+    bool pw = false;   // v2 with per-wave env tables (herds of kPwMinCattle cows and more)
     size_t lds = 0;
     uint16_t* pairs = nullptr;
     int* errw = nullptr;        // device error word (CH_DEVERR_* bits), sticky
@@ -158,7 +159,7 @@ static StepParams<R> params(ch_handle* h) {
     p.metrics = h->metrics; p.spawn = h->spawn; p.n_scen = h->n_scen; p.n_cows = h->n_cows;
     p.debug = h->debug;
     p.phase_mask = h->phase_mask;
-    p.G = h->G; p.P = h->P; p.pairs = h->pairs;
+    p.G = h->G; p.P = h->P; p.pairs = h->pairs; p.pw = h->pw;
     p.tstamp = h->tstamp;
     p.physics = c.physics; p.gnd_h_clip = gnd_eff_h_clip(); p.phys = (R*)h->phys;
     p.err = h->errw;
@@ -338,7 +339,7 @@ int ch_create(const ch_config* c, int64_t n_envs, int32_t device, ch_handle** ou
         CTRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
         if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, device) != hipSuccess)
             lds_max = 64 * 1024;
-        const size_t budget = std::min<size_t>((size_t)lds_max, 150 * 1024);
+        const size_t budget = std::min<size_t>((size_t)lds_max, 160 * 1024);
         // a drone wave (G*N <= 64 drone chains) plus three cow waves (G*M cows, one per lane when it fits)
         int G = std::max(1, std::min(64 / h->NC, 192 / h->M));
         G = (int)std::min<int64_t>(G, std::max<int64_t>(1, E / std::max(cus, 1)));
@@ -358,9 +359,24 @@ int ch_create(const ch_config* c, int64_t n_envs, int32_t device, ch_handle** ou
         }
         // measured (tools/ab/marl.py, MI355X, 4096 envs): the dataflow kernel wins for every CTDE size
         // (2x8 19.4 vs 41.1 us, 8x16 39.7 vs 55.8, 12x16 59.9 vs 67.1) and for MARL with up to 16
-        // cattle (3x8 25.8 vs 43.2); MARL 4x32 (BASELINE configs[4]) is still faster on the
-        // team-per-env kernel (87.6 vs 92-95 us: its 496-pair alpha table per env)
-        if (c->mode == CH_MODE_MARL && h->M > 16) h->kernel = 1;
+        // cattle (3x8 25.8 vs 43.2).  Above 16 cows one shared pair table per workgroup (15.9 KB per
+        // env at 32 cows) leaves room for 4 envs per CU; the per-wave env tables (V2Layout W) keep a
+        // CU's 16 envs in one workgroup instead.
+        if (h->M >= kPwMinCattle) {
+            h->kernel = 1;   // unless a per-wave geometry fits (physics variants stay on v1)
+            if (c->physics == CH_PHYS_PYB) {
+                const int cand[][2] = {{16, 512}, {8, 512}, {8, 256}, {4, 256}, {2, 128}, {1, 128}};
+                for (const auto& gb : cand) {
+                    const int g = gb[0], blk = gb[1];
+                    if (g * h->NC > 64 || g * h->M > 3 * (blk - 64)) continue;
+                    if (g > 1 && E < (int64_t)g * cus) continue;
+                    const size_t l = V2Layout(g, h->NC, h->M, h->P, c->mode, (int)h->rsize, blk / 64 - 1).bytes();
+                    if (l > budget) continue;
+                    h->G = g; h->block = blk; h->lds = l; h->pw = true; h->kernel = 2;
+                    break;
+                }
+            }
+        }
         if (h->lds > budget) h->kernel = 1;   // one env's pair table alone exceeds the budget
         std::vector<uint16_t> pl((size_t)std::max(h->P, 1));
         for (int i = 0, r = 0; i < h->M; ++i)
@@ -552,7 +568,7 @@ int ch__set_debug(ch_handle* h, double* dev) {
 /* Internal diagnostics: step kernel version (1 = team-per-env ch_kernels.hip, 2 = role-split ch_step.hip). */
 int ch__set_kernel(ch_handle* h, int32_t version) {
     if (!h || (version != 1 && version != 2)) return CH_ERR_INVALID;
-    if (version == 2 && h->lds > 150 * 1024) return CH_ERR_UNSUPPORTED;
+    if (version == 2 && h->lds > 160 * 1024) return CH_ERR_UNSUPPORTED;
     h->kernel = version;
     HIP_TRY(h, prepare_step(h));
     return CH_OK;
@@ -569,8 +585,8 @@ int ch__set_tstamp(ch_handle* h, long long* dev) {
 int ch__set_geometry(ch_handle* h, int32_t G, int32_t block) {
     if (!h || G < 1 || G > 64 || G * h->NC > 64 || block < 128 || block > CH_V2_MAX_BLOCK || block % 64) return CH_ERR_INVALID;
     if (G * h->M > 3 * (block - 64)) return CH_ERR_UNSUPPORTED;   // the cow waves prefetch <= 3 spawn slots per lane
-    const size_t lds = V2Layout(G, h->NC, h->M, h->P, h->cfg.mode, (int)h->rsize).bytes();
-    if (lds > 150 * 1024) return CH_ERR_UNSUPPORTED;
+    const size_t lds = V2Layout(G, h->NC, h->M, h->P, h->cfg.mode, (int)h->rsize, h->pw ? block / 64 - 1 : 0).bytes();
+    if (lds > 160 * 1024) return CH_ERR_UNSUPPORTED;
     h->G = G; h->block = block; h->lds = lds;
     HIP_TRY(h, prepare_step(h));
     return CH_OK;

@@ -22,8 +22,8 @@ __device__ __forceinline__ void curriculum_success(const Level* LT, int& level, 
 
 // _computeTerminated (CattleAviary.py:422-492; MARLCattleAviary.py:246-321)
 template <class R>
-__device__ __forceinline__ bool term_call(const Level* LT, int level, R& clock, R clock_inc, R min_spacing, R cent, R eff) {
-    const Level& L = LT[level];
+__device__ __forceinline__ bool term_call_L(const Level& L, int level, R& clock, R clock_inc, R min_spacing, R cent,
+                                            R eff) {
     if (level == 0 || level == 1) {
         R up = R(L.desired) + R(L.desired) * R(L.tol), lo = R(L.desired) - R(L.desired) * R(L.tol);
         if (min_spacing < up && min_spacing > lo) {
@@ -44,6 +44,10 @@ __device__ __forceinline__ bool term_call(const Level* LT, int level, R& clock, 
         }
     }
     return false;
+}
+template <class R>
+__device__ __forceinline__ bool term_call(const Level* LT, int level, R& clock, R clock_inc, R min_spacing, R cent, R eff) {
+    return term_call_L(LT[level], level, clock, clock_inc, min_spacing, cent, eff);
 }
 
 // NUM_DRONES of the episode that starts after `episode` resets (BaseAviary.py:307: random.randint over
@@ -127,9 +131,8 @@ __device__ __forceinline__ void reset_cow(const StepParams<R>& p, long long ci, 
 
 // end-of-episode bonus of MARLCattleAviary._endOfEpisodeReward (MARLCattleAviary.py:183-241)
 template <class R>
-__device__ __forceinline__ R marl_end_of_episode(const Level* LT, int level, R a, R b, R cent, R eff, R dist_to_herd,
-                                                int n) {
-    const Level& L2 = LT[level];
+__device__ __forceinline__ R marl_end_of_episode_L(const Level& L2, int level, R a, R b, R cent, R eff, R dist_to_herd,
+                                                  int n) {
     R eor = 0;
     if (level == 0 || level == 1) {
         R up = R(L2.desired) + R(L2.desired) * R(L2.tol), lo = R(L2.desired) - R(L2.desired) * R(L2.tol);
@@ -147,6 +150,11 @@ __device__ __forceinline__ R marl_end_of_episode(const Level* LT, int level, R a
         }
     }
     return eor;
+}
+template <class R>
+__device__ __forceinline__ R marl_end_of_episode(const Level* LT, int level, R a, R b, R cent, R eff, R dist_to_herd,
+                                                int n) {
+    return marl_end_of_episode_L(LT[level], level, a, b, cent, eff, dist_to_herd, n);
 }
 
 }  // namespace ch

@@ -504,10 +504,10 @@ __device__ __forceinline__ void pair_terms(R qix, R qiy, R pix, R piy, R qjx, R 
     cy += b * (pjy - piy);
 }
 
-// same as pair_terms with the neighbour offset z = qj - qi and its norm already at hand
+// same as pair_terms with the neighbour offset z = qj - qi and its norm already at hand; returns the bump
 template <class R>
-__device__ __forceinline__ void pair_terms_n(R n, R zx, R zy, R pix, R piy, R pjx, R pjy, R ra, R da, R& gx, R& gy,
-                                             R& cx, R& cy) {
+__device__ __forceinline__ R pair_terms_n(R n, R zx, R zy, R pix, R piy, R pjx, R pjy, R ra, R da, R& gx, R& gy,
+                                          R& cx, R& cy) {
     R den = sqrt(R(1) + R(kEps) * (n * n));
     R sn = divc(den - R(1), R(kEps));
     R b = bump(divc(sn, ra));
@@ -517,6 +517,7 @@ __device__ __forceinline__ void pair_terms_n(R n, R zx, R zy, R pix, R piy, R pj
     gy += ph * (zy / den);
     cx += b * (pjx - pix);
     cy += b * (pjy - piy);
+    return b;
 }
 
 // ---- spacing rewards: CattleAviary.py:572-679 -------------------------------------------------

@@ -59,6 +59,7 @@ struct StepParams {
     double gnd_h_clip;        // GND_EFF_H_CLIP (BaseAviary.py:173)
     R* phys;                  // [kPhysComps][E][NC]
     int* err;                 // device error word of the handle (CH_DEVERR_* bits), read by ch_sync & co.
+    int pw;                   // v2: per-wave env tables (V2Layout W = block / 64 - 1)
 };
 
 // device error word bits (ch_api.cpp reports them as CH_ERR_DEVICE)
@@ -81,25 +82,38 @@ struct Level {
 #endif
 constexpr int kV2EnvInts = 13;
 constexpr int kV2Flags = 16;         // LDS hand-off counters between the drone wave and the cow waves + work counters
+// W = 0: one alpha pair table for the whole workgroup (4 reals per pair, G*P pairs), reused for the
+// shepherd terms.  W > 0 ("per-wave env tables", large herds): each of the W cow waves owns a slot for
+// ONE env at a time -- 3 reals per pair (gradient x, y and the bump; the consensus term is recomputed
+// from the velocities when the rows are summed), reused for that env's shepherd terms -- so the LDS
+// no longer grows with G*P and a whole CU's envs fit in one workgroup.
 struct V2Layout {
     enum { CX = 0, DRONE, DCOW, ENVR, PAIRS, MET, IMG, EI, LEVELS, PAIRL, BYTES, NOFF };
-    int G, N, M, P, rows;
+    int G, N, M, P, rows, W;
+    size_t slot;   // W > 0: reals per wave slot
     size_t off[NOFF + 1];
     static __host__ __device__ size_t al(size_t x) { return (x + 15) & ~size_t(15); }
-    __host__ __device__ V2Layout(int G_, int N_, int M_, int P_, int mode, int rb) : G(G_), N(N_), M(M_), P(P_) {
+    __host__ __device__ V2Layout(int G_, int N_, int M_, int P_, int mode, int rb, int W_ = 0)
+        : G(G_), N(N_), M(M_), P(P_), W(W_) {
         rows = mode == CH_MODE_CTDE ? 12 : N;
+        slot = 3 * (size_t)P > 6 * (size_t)M * N ? 3 * (size_t)P : 6 * (size_t)M * N;
+        const size_t shared = 4 * (size_t)G * P > 6 * (size_t)G * M * N ? 4 * (size_t)G * P : 6 * (size_t)G * M * N;
         size_t o = 0;
         off[CX] = o;     o = al(o + 8 * (size_t)G * M * rb);         // cx cy cvx cvy aux auy spx spy
         off[DRONE] = o;  o = al(o + 12 * (size_t)G * N * rb);        // dx dy dz pa pb sa sb ca cb scat psp mrew
         off[DCOW] = o;   o = al(o + (size_t)G * N * M * rb);         // cow-drone distances
         off[ENVR] = o;   o = al(o + 4 * (size_t)G * rb);             // prev clock, herd centroid x y
-        off[PAIRS] = o;  o = al(o + (4 * (size_t)G * P > 6 * (size_t)G * M * N ? 4 * (size_t)G * P : 6 * (size_t)G * M * N) * rb);   // alpha pair table, then shepherd terms
+        off[PAIRS] = o;  o = al(o + (W ? (size_t)W * slot : shared) * rb);   // alpha pair table(s), then shepherd terms
         off[MET] = o;    o = al(o + (size_t)kMetricRows * G * 8);
         off[IMG] = o;                                                // (observations go straight to HBM)
         off[EI] = o;     o = al(o + ((size_t)kV2EnvInts * G + 2 * G + 2 + kV2Flags) * 4);   // + flock/reset lists
         off[LEVELS] = o; o = al(o + 8 * sizeof(Level));              // curriculum table
         off[PAIRL] = o;  o = al(o + 2 * (size_t)P);                  // unordered cow pairs (i | j << 8)
-        off[BYTES] = o;  o = al(o + (size_t)G * P + 3 * (size_t)G * N + (size_t)G * M + (size_t)G * M * N);
+        const size_t tabs = W ? (size_t)W : (size_t)G;               // pair flags and term flags: per slot / per env
+        // W > 0: no pair flags; per-cow "has a neighbour in sensing range" bytes and, per slot, the queue of
+        // the env's pairs inside the bump's support (u16 pair indices)
+        off[BYTES] = o;  o = al(o + (W ? al((size_t)G * M) + 2 * (size_t)W * P : (size_t)G * P) + 3 * (size_t)G * N +
+                                (size_t)G * M + tabs * M * N);
         off[NOFF] = o;
     }
     __host__ __device__ size_t bytes() const { return off[NOFF]; }
@@ -134,5 +148,7 @@ template <class R> hipError_t launch_reset(const StepParams<R>& p, int team, hip
 // step captured into a HIP graph needs no host-side setup)
 template <class R> hipError_t launch_step_v2(const StepParams<R>& p, int block, size_t lds, hipStream_t st,
                                              bool launch = true);
+// the v2 kernel runs with per-wave env tables (V2Layout W > 0) for herds above this size
+constexpr int kPwMinCattle = 17;
 
 }  // namespace ch

@@ -139,9 +139,11 @@ struct V2Smem {
     const uint16_t* pl;                              // [P] unordered cow pairs, copied from p.pairs
     uint8_t *pflag, *dflags, *herded, *md1, *md2;    // [G*P], [G*N], [G*M], [G*N], [G*N]
     uint8_t* tdf;                                    // [G*M*N] shepherd term in range | predator in range << 1
+    uint8_t* hasnb;                                  // PW: [G*M] cow has a neighbour within sensing range
+    uint16_t* queue;                                 // PW: [W][P] pairs of the slot's env inside the bump support
 
     __device__ V2Smem(unsigned char* base, const V2Layout& L) {
-        const int GM = L.G * L.M, GN = L.G * L.N, GP = L.G * L.P;
+        const int GM = L.G * L.M, GN = L.G * L.N, GP = (L.W ? L.W : L.G) * L.P;
         cx = (R*)(base + L.off[V2Layout::CX]); cy = cx + GM; cvx = cy + GM; cvy = cvx + GM; aux = cvy + GM; auy = aux + GM;
         spx = auy + GM; spy = spx + GM;
         dx = (R*)(base + L.off[V2Layout::DRONE]); dy = dx + GN; dz = dy + GN;
@@ -156,7 +158,12 @@ struct V2Smem {
         ei = (int*)(base + L.off[V2Layout::EI]);
         flags = ei + I_COUNT * L.G + 2 * L.G + 2;
         LT = (Level*)(base + L.off[V2Layout::LEVELS]);
-        pflag = base + L.off[V2Layout::BYTES]; dflags = pflag + GP; herded = dflags + GN; md1 = herded + GM;
+        pflag = base + L.off[V2Layout::BYTES];
+        hasnb = pflag;
+        const int GMa = (GM + 15) & ~15;
+        queue = reinterpret_cast<uint16_t*>(pflag + GMa);   // W > 0 only
+        dflags = L.W ? pflag + GMa + 2 * L.W * L.P : pflag + GP;
+        herded = dflags + GN; md1 = herded + GM;
         md2 = md1 + GN; tdf = md2 + GN;
     }
 };
@@ -286,10 +293,87 @@ __device__ __forceinline__ void alpha_row(V2Smem<R>& S, int M, int P, int u, int
     S.aux[u] = ux; S.auy[u] = uy;
 }
 
+// ---- per-wave env tables (V2Layout W > 0, large herds) ---------------------------------------------
+// Env g's alpha pair table in the calling wave's slot: gradient x, y and the bump b per pair
+// (flockUtils.py:237-258, 327-337).  The consensus term b (p_hi - p_lo) is not stored: alpha_row_pw
+// recomputes it from the velocities with the same rounding.
+//
+// Two passes.  The cheap pass (one 64-pair chunk per call) evaluates sigma_norm(|z|) / r_alpha for every
+// pair; the bump is exactly 0 above 1 (and for NaN), so such a pair's table entry is +0 -- what the full
+// evaluation stores -- and only pairs with z <= 1 are queued.  The expensive pass (cos of the bump,
+// sigma_1, the divisions) then runs on full waves of queued pairs.  In a spread herd most pairs are
+// outside the lattice range d_alpha = 1.2 m, so most lanes skip the expensive part.
+template <class R>
+__device__ __forceinline__ void alpha_cheap_pw(V2Smem<R>& S, int M, int P, int g, int c, R* tb, uint16_t* qu,
+                                               int& qn) {
+    const R ra = sigma_norm_n(R(1.2));
+    const int lane = threadIdx.x & 63;
+    const int r = c * 64 + lane;
+    bool full = false;
+    if (r < P) {
+        const uint32_t pr = S.pl[r];
+        const int bi = g * M + (pr & 0xff), bj = g * M + (pr >> 8);
+        const R zx = S.cx[bj] - S.cx[bi], zy = S.cy[bj] - S.cy[bi];
+        const R nrm = sqrt(zx * zx + zy * zy);
+        if (nrm <= R(999)) {   // within sensing range: both cows have a neighbour (the rows' nb > 0)
+            S.hasnb[bi] = 1;
+            S.hasnb[bj] = 1;
+            const R den = sqrt(R(1) + R(kEps) * (nrm * nrm));   // pair_terms_n's z, same operations
+            const R sn = divc(den - R(1), R(kEps));
+            full = divc(sn, ra) <= R(1);
+        }
+        if (!full) { tb[r] = R(0); tb[P + r] = R(0); tb[2 * P + r] = R(0); }
+    }
+    const unsigned long long m = __ballot(full);
+    if (full) qu[qn + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)r;
+    qn += __popcll(m);
+}
+
+template <class R>
+__device__ __forceinline__ void alpha_full_pw(V2Smem<R>& S, int M, int P, int g, int q0, int qn, R* tb,
+                                              const uint16_t* qu) {
+    const R ra = sigma_norm_n(R(1.2)), da = ra;
+    const int q = q0 + (threadIdx.x & 63);
+    if (q >= qn) return;
+    const int r = qu[q];
+    const uint32_t pr = S.pl[r];
+    const int bi = g * M + (pr & 0xff), bj = g * M + (pr >> 8);
+    const R zx = S.cx[bj] - S.cx[bi], zy = S.cy[bj] - S.cy[bi];
+    const R nrm = sqrt(zx * zx + zy * zy);
+    R gx = 0, gy = 0, cx = 0, cy = 0;
+    const R b = pair_terms_n(nrm, zx, zy, R(0), R(0), R(0), R(0), ra, da, gx, gy, cx, cy);
+    tb[r] = gx; tb[P + r] = gy; tb[2 * P + r] = b;
+}
+
+// alpha row of cow j of env g from the wave's slot, in neighbour order (as alpha_row).  The pair's
+// consensus term is b * (p_hi - p_lo), hi/lo the pair's cows, exactly as the shared table holds it; a
+// pair outside the bump support has b = +0 and adds +-0, which leaves the row sum unchanged.
+template <class R>
+__device__ __forceinline__ void alpha_row_pw(V2Smem<R>& S, int M, int P, int g, int j, const R* tb) {
+    const R C2A = R(2 * 1.7320508075688772);
+    const int u = g * M + j;
+    R gx = 0, gy = 0, cxx = 0, cyy = 0, ux = 0, uy = 0;
+    const R pjx = S.cvx[u], pjy = S.cvy[u];
+    CH_UNROLL for (int k = 0; k < M; ++k) {
+        if (k == j) continue;
+        const bool fwd = j < k;
+        const int idx = fwd ? tri(j, k, M) : tri(k, j, M);
+        const R tgx = tb[idx], tgy = tb[P + idx], b = tb[2 * P + idx];
+        const R pkx = S.cvx[g * M + k], pky = S.cvy[g * M + k];
+        const R dvx = fwd ? pkx - pjx : pjx - pkx, dvy = fwd ? pky - pjy : pjy - pky;
+        const R tcx = b * dvx, tcy = b * dvy;
+        gx += fwd ? tgx : -tgx; gy += fwd ? tgy : -tgy;
+        cxx += fwd ? tcx : -tcx; cyy += fwd ? tcy : -tcy;
+    }
+    if (S.hasnb[u]) { ux = C2A * gx + C2A * cxx; uy = C2A * gy + C2A * cyy; }
+    S.aux[u] = ux; S.auy[u] = uy;
+}
+
 // shepherd (delta, flockUtils.py:271-317) and predator (343-348) terms of drone k on cow u = g*M + j,
 // one (cow, drone) item per lane; stored in the term table for flock_combine.
 template <class R>
-__device__ __forceinline__ void delta_term(V2Smem<R>& S, int N, int M, int u, int g, int k, int T) {
+__device__ __forceinline__ void delta_term(V2Smem<R>& S, int N, int u, int g, int k, R* td, uint8_t* tdf, int i,
+                                           int T) {
     const R ra_b = sigma_norm_n(R(1.0)), da_b = ra_b;
     const R qix = S.cx[u], qiy = S.cy[u], pix = S.cvx[u], piy = S.cvy[u];
     const R yx = S.dx[g * N + k], yy = S.dy[g * N + k];
@@ -312,10 +396,9 @@ __device__ __forceinline__ void delta_term(V2Smem<R>& S, int N, int M, int u, in
         t[4] = R(-650000.0) * ex / d3;
         t[5] = R(-650000.0) * ey / d3;
     }
-    const int i = u * N + k;
 #pragma unroll
-    for (int c = 0; c < 6; ++c) S.td[c * T + i] = t[c];
-    S.tdf[i] = (uint8_t)(in | (pr << 1));
+    for (int c = 0; c < 6; ++c) td[c * T + i] = t[c];
+    tdf[i] = (uint8_t)(in | (pr << 1));
 }
 
 // gamma term (flockUtils.py:150-160, 340-341), the drone terms summed in drone order, and the velocity
@@ -323,7 +406,7 @@ __device__ __forceinline__ void delta_term(V2Smem<R>& S, int N, int M, int u, in
 // table, and adding +0 to a sum that starts at +0 leaves it unchanged, so only the count needs the flag.
 template <class R>
 __device__ __forceinline__ void flock_combine(const StepParams<R>& p, V2Smem<R>& S, int N, int M, int e0, int u, int n,
-                                              int T) {
+                                              const R* td, const uint8_t* tdf, int ib, int T) {
     const long long CS = (long long)p.E * M;
     const R C2B = R(2 * 4.47213595499958), C1G = R(5), C2G = R(0.2 * 2.23606797749979);
     const R qix = S.cx[u], qiy = S.cy[u], pix = S.cvx[u], piy = S.cvy[u];
@@ -331,10 +414,10 @@ __device__ __forceinline__ void flock_combine(const StepParams<R>& p, V2Smem<R>&
     int nb = 0;
     CH_UNROLL for (int k = 0; k < N; ++k) {
         if (k >= n) break;
-        const int i = u * N + k;
-        const int f = S.tdf[i];
-        if (f & 1) { ++nb; gx += S.td[i]; gy += S.td[T + i]; cxx += S.td[2 * T + i]; cyy += S.td[3 * T + i]; }
-        if (f & 2) { sx += S.td[4 * T + i]; sy += S.td[5 * T + i]; }
+        const int i = ib + k;
+        const int f = tdf[i];
+        if (f & 1) { ++nb; gx += td[i]; gy += td[T + i]; cxx += td[2 * T + i]; cyy += td[3 * T + i]; }
+        if (f & 2) { sx += td[4 * T + i]; sy += td[5 * T + i]; }
     }
     if (nb > 0) { ddx = C2B * gx + C2B * cxx; ddy = C2B * gy + C2B * cyy; }
     ddx += sx; ddy += sy;
@@ -350,13 +433,13 @@ __device__ __forceinline__ void flock_combine(const StepParams<R>& p, V2Smem<R>&
 
 // GT/NT/MT > 0 specialise the kernel for one geometry (envs per workgroup, drones, cattle): the LDS
 // carve and all index arithmetic then fold to immediates, which keeps the kernel within the SGPR file.
-template <class R, int MODE, int GT, int NT, int MT, bool PHYS = false>
+template <class R, int MODE, int GT, int NT, int MT, bool PHYS = false, bool PW = false>
 __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
     extern __shared__ __align__(16) unsigned char smem[];
     constexpr bool marl = MODE == 1;
     const int G = GT ? GT : p.G, N = NT ? NT : p.NC, M = MT ? MT : p.M, P = MT ? MT * (MT - 1) / 2 : p.P;
     const int rows = marl ? N : 12;
-    const V2Layout L(G, N, M, P, MODE, (int)sizeof(R));
+    const V2Layout L(G, N, M, P, MODE, (int)sizeof(R), PW ? (int)(blockDim.x >> 6) - 1 : 0);
     V2Smem<R> S(smem, L);
     const int BS = blockDim.x, tid = threadIdx.x;
     const int e0 = blockIdx.x * G;
@@ -427,6 +510,8 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
         for (int k = ct; k < (int)(sizeof(kLevels) / 4); k += CW)
             reinterpret_cast<uint32_t*>(S.LT)[k] = reinterpret_cast<const uint32_t*>(kLevels)[k];
         for (int k = ct; k < P; k += CW) const_cast<uint16_t*>(S.pl)[k] = p.pairs[k];
+        if constexpr (PW)
+            for (int k = ct; k < G * M; k += CW) S.hasnb[k] = 0;
         if (ct < 64) {   // the first cow wave: env scalars, one env per lane
         const int g = ct;
         bool flk = false;
@@ -637,7 +722,10 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
                 done = te2 || tr;
             } else {
                 // MARLCattleAviary reward / terminated / truncated in the order env.step
-                // (rllib_envs/BaseAviary.py:425-431) and the wrapper (marl_wrapper.py:104-113) call them
+                // (rllib_envs/BaseAviary.py:425-431) and the wrapper (marl_wrapper.py:104-113) call them.
+                // Up to 2N rewards and 3N terminated calls run in sequence (their side effects chain), so the
+                // per-agent inputs and the current curriculum level live in registers (geometry-specialised
+                // kernels: NT > 0, every agent loop unrolled) instead of being re-read from LDS per call.
                 int& level = f_level;
                 int& tally = f_tally;
                 int& has_prev = f_hp;
@@ -650,50 +738,91 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
                 // own dicts and the wrapper's recomputation, so the wrapper sees the time limit one step
                 // earlier (MARLCattleAviary.py:376)
                 const bool time_up_w = (double)(f_sc + 1) / p.ctrl_freq > p.episode_len;
+                constexpr int NR = NT ? NT : 1;
+                R r_pa[NR], r_pb[NR], r_sa[NR], r_sb[NR], r_ca[NR], r_cb[NR], r_sc[NR], r_dh[NR], r_rw[NR];
+                uint8_t r_df[NR], r_d1[NR];
+                if constexpr (NT > 0) {
+                    CH_UNROLL for (int i = 0; i < NT; ++i) {
+                        r_pa[i] = S.pa[b0 + i]; r_pb[i] = S.pb[b0 + i]; r_sa[i] = S.sa[b0 + i]; r_sb[i] = S.sb[b0 + i];
+                        r_ca[i] = S.ca[b0 + i]; r_cb[i] = S.cb[b0 + i]; r_sc[i] = S.scat[b0 + i];
+                        r_dh[i] = norm2(scx - S.dx[b0 + i], scy - S.dy[b0 + i]);   // drone to herd centroid (level 4/6 bonus)
+                        r_df[i] = S.dflags[b0 + i];
+                    }
+                }
+#define AG(arr, lds) [&](int i_) { if constexpr (NT > 0) return arr[i_]; else return lds; }
+                auto PA = AG(r_pa, S.pa[b0 + i_]);
+                auto PB = AG(r_pb, S.pb[b0 + i_]);
+                auto SA = AG(r_sa, S.sa[b0 + i_]);
+                auto SB = AG(r_sb, S.sb[b0 + i_]);
+                auto CA = AG(r_ca, S.ca[b0 + i_]);
+                auto CB = AG(r_cb, S.cb[b0 + i_]);
+                auto SC = AG(r_sc, S.scat[b0 + i_]);
+                auto DH = AG(r_dh, norm2(scx - S.dx[b0 + i_], scy - S.dy[b0 + i_]));
+                auto DF = AG(r_df, S.dflags[b0 + i_]);
+#undef AG
+                Level Lc = LT[level];   // the current level's constants (re-read when the level changes)
+                const R approach_div = max_step + R(1e-6);
+                const R eff100 = divc(eff, R(100));   // eff / 100, the same for every call of this step
+                auto succeed = [&]() {   // curriculum_success (curriculum_learning.py:200-219)
+                    tally += 1;
+                    if (tally >= Lc.required_tally) {
+                        tally = 0;
+                        level += 1;
+                        if (level >= 8) level = 7;
+                        Lc = LT[level];
+                    }
+                };
                 auto trunc_i = [&](int i, bool tu) -> bool {
-                    return (S.dflags[b0 + i] & 7) || cent > R(kMissionBoundary) || tu;
+                    return (DF(i) & 7) || cent > R(kMissionBoundary) || tu;
                 };
                 auto reward_i = [&](int i, bool tu) -> R {
-                    const Level& Lv = LT[level];
-                    R a = S.pa[b0 + i], b = S.pb[b0 + i];
+                    const R a = PA(i), b = PB(i);
                     R sa, sb, ca, cb;
-                    if (level == lvl0) { sa = S.sa[b0 + i]; sb = S.sb[b0 + i]; ca = S.ca[b0 + i]; cb = S.cb[b0 + i]; }
-                    else { sa = simple_spacing(a, Lv); sb = simple_spacing(b, Lv); ca = complex_spacing(a, Lv); cb = complex_spacing(b, Lv); }
+                    if (level == lvl0) { sa = SA(i); sb = SB(i); ca = CA(i); cb = CB(i); }
+                    else { sa = simple_spacing(a, Lc); sb = simple_spacing(b, Lc); ca = complex_spacing(a, Lc); cb = complex_spacing(b, Lc); }
                     R simple = (sa + sb) / R(2), cplx = (ca + cb) / R(2);
                     if (!p.compat) {
                         if (!(b < R(INFINITY))) { simple = sa; cplx = ca; }
                         if (!(a < R(INFINITY))) { simple = 0; cplx = 0; }
                     }
                     R r = 0;
-                    r += simple * R(Lv.w_simple);
-                    r += cplx * R(Lv.w_complex);
-                    r += R(0.1) * R(Lv.w_survival);
+                    r += simple * R(Lc.w_simple);
+                    r += cplx * R(Lc.w_complex);
+                    r += R(0.1) * R(Lc.w_survival);
                     R change = has_prev ? prev - cent : R(0.0);
                     prev = cent; has_prev = 1;
-                    r += clip((change / (max_step + R(1e-6))) * R(5), R(-1.0), R(1.0)) * R(Lv.w_approach);
-                    r += (eff / R(100)) * R(Lv.w_eff);
-                    r += S.scat[b0 + i] * R(Lv.w_cattle);
-                    if (term_call(LT, level, clock, inc, ms, cent, eff)) {
-                        r += marl_end_of_episode(LT, level, a, b, cent, eff, norm2(scx - S.dx[b0 + i], scy - S.dy[b0 + i]), n);
-                        curriculum_success(LT, level, tally);
+                    r += clip(divc(change, approach_div) * R(5), R(-1.0), R(1.0)) * R(Lc.w_approach);
+                    r += eff100 * R(Lc.w_eff);
+                    r += SC(i) * R(Lc.w_cattle);
+                    if (term_call_L(Lc, level, clock, inc, ms, cent, eff)) {
+                        r += marl_end_of_episode_L(Lc, level, a, b, cent, eff, DH(i), n);
+                        succeed();
                     } else if (trunc_i(i, tu)) {
                         r -= R(50);
                     }
                     return r;
                 };
                 // env.step's own dicts (rllib_envs/BaseAviary.py:425-431)
-                for (int i = 0; i < n; ++i) S.mrew[b0 + i] = reward_i(i, time_up);
-                for (int i = 0; i < n; ++i) S.md1[b0 + i] = term_call(LT, level, clock, inc, ms, cent, eff);
+                CH_UNROLL for (int i = 0; i < N; ++i) {
+                    if (i >= n) break;
+                    const R rr = reward_i(i, time_up);
+                    if constexpr (NT > 0) r_rw[i] = rr; else S.mrew[b0 + i] = rr;
+                }
+                CH_UNROLL for (int i = 0; i < N; ++i) {
+                    if (i >= n) break;
+                    const uint8_t d = term_call_L(Lc, level, clock, inc, ms, cent, eff);
+                    if constexpr (NT > 0) r_d1[i] = d; else S.md1[b0 + i] = d;
+                }
                 const int act0 = active;
                 if (p.marl_wrapper) {
                     // the wrapper recomputes everything per live agent (marl_wrapper.py:104-110)
                     done = 1;
-                    for (int i = 0; i < N; ++i) {
+                    CH_UNROLL for (int i = 0; i < N; ++i) {
                         R rr = R(NAN);
                         uint8_t tt = 0, trr = 0;
                         if (i < n && ((act0 >> i) & 1)) {
                             rr = reward_i(i, time_up_w);
-                            tt = term_call(LT, level, clock, inc, ms, cent, eff);
+                            tt = term_call_L(Lc, level, clock, inc, ms, cent, eff);
                             trr = trunc_i(i, time_up_w);
                         }
                         p.reward[(long long)e * N + i] = (float)rr;
@@ -704,14 +833,18 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
                         if (i < n && (((act0 >> i) & 1) || tt) && rr != rr) n_nan += 1;
                         if (i < n && ((act0 >> i) & 1) && tt) active &= ~(1 << i);   // finished agents drop out
                     }
-                    for (int i = 0; i < n; ++i)
-                        if ((active >> i) & 1) done = 0;   // __all__: every agent terminated (marl_wrapper.py:113-117)
+                    CH_UNROLL for (int i = 0; i < N; ++i)
+                        if (i < n && ((active >> i) & 1)) done = 0;   // __all__: every agent terminated (marl_wrapper.py:113-117)
                 } else {
                     done = 1;   // bare env.step dicts: __all__ = all(done.values())
-                    for (int i = 0; i < N; ++i) {
+                    CH_UNROLL for (int i = 0; i < N; ++i) {
                         R rr = R(NAN);
                         uint8_t tt = 0, trr = 0;
-                        if (i < n) { rr = S.mrew[b0 + i]; tt = S.md1[b0 + i]; trr = trunc_i(i, time_up); done &= tt; }
+                        if (i < n) {
+                            if constexpr (NT > 0) { rr = r_rw[i]; tt = r_d1[i]; } else { rr = S.mrew[b0 + i]; tt = S.md1[b0 + i]; }
+                            trr = trunc_i(i, time_up);
+                            done &= tt;
+                        }
                         p.reward[(long long)e * N + i] = (float)rr;
                         p.term[(long long)e * N + i] = tt;
                         p.trunc[(long long)e * N + i] = trr;
@@ -802,7 +935,51 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
         if (tid == 0) TS(7, (long long)clock64());
     } else {
         // ============ cow waves ================================================================
-        alpha_pairs(p, S, G, M, P);
+        const float rM = 1.0f / (float)M;
+        const int nf = ei[NF_AT];
+        const int* flist = ei + FL_LIST;
+        const int lane = tid & 63;
+        // PW: this wave's env slot and queue, the env (flock-list index) it holds, the next cheap-pass
+        // chunk, and the queue length / position of the expensive pass
+        R* tb = nullptr;
+        uint8_t* tf = nullptr;
+        uint16_t* qu = nullptr;
+        int f_cur = -1, ch = 0, qn = 0, qd = 0;
+        const int NCH = (P + 63) >> 6;
+        // one unit of PW alpha work (a cheap-pass chunk or an expensive-pass wave of queued pairs, plus the
+        // env's rows after its last unit); false when no flocking env is left.  The state is wave-uniform
+        // (grab is readfirstlane'd, the queue length a ballot count).
+        auto alpha_step = [&]() -> bool {
+            if (f_cur < 0) {
+                f_cur = grab(fl + C_PAIRS, 1);
+                ch = 0; qn = 0; qd = 0;
+            }
+            if (f_cur >= nf) return false;
+            CHUNK_T0;
+            const int g = flist[f_cur];
+            if (ch < NCH) {
+                alpha_cheap_pw(S, M, P, g, ch, tb, qu, qn);
+                if (++ch == NCH) wave_sync();   // the queue and the +0 entries
+            } else if (qd < qn) {
+                alpha_full_pw(S, M, P, g, qd, qn, tb, qu);
+                qd += 64;
+            }
+            if (ch == NCH && qd >= qn) {
+                wave_sync();   // every table entry of the env
+                for (int j = lane; j < M; j += 64) alpha_row_pw(S, M, P, g, j, tb);
+                wave_sync();   // the slot is free again
+                f_cur = -1;
+            }
+            CHUNK_T1(0);
+            return true;
+        };
+        if constexpr (PW) {
+            tb = S.tgx + (size_t)(tid / 64 - 1) * L.slot;
+            tf = S.tdf + (size_t)(tid / 64 - 1) * M * N;
+            qu = S.queue + (size_t)(tid / 64 - 1) * P;
+        } else {
+            alpha_pairs(p, S, G, M, P);
+        }
         if (ct == 0) TS(18, (long long)clock64());
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -813,25 +990,27 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
         // already holds them (first step into a buffer, after ch_set_state, ...; ch_api.cpp obs_zero_ptr)
         if (wobs && (p.obs_full || p.ctl[1]))
             for (int g = 0; g < Gv; ++g) obs_zero_env(obs_wg + g * RW, ei[I_N * G + g], rows, cat_off, m_obs, ct, CW);
-        lds_signal(fl + F_A);
-        const float rM = 1.0f / (float)M;
-        const int nf = ei[NF_AT];
-        const int* flist = ei + FL_LIST;
-        const int lane = tid & 63;
-        // alpha rows while the drone wave still integrates: once every pair is in the table, row chunks
-        // are taken until the drone positions arrive; the rest follows the drone hand-off below
-        for (int spins = 0; spins < (1 << 22); ++spins) {
-            if (lds_peek(fl + F_D) >= 1) break;
-            if (lds_peek(fl + F_A) < W1) { __builtin_amdgcn_s_sleep(1); continue; }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");   // the pair table
-            const int b = grab(fl + C_ROWS, 64), u = b + lane;
-            if (b >= nf * M) break;
-            CHUNK_T0;
-            if (u < nf * M) {
-                const int f = qdiv(u, M, rM), g = flist[f], j = u - f * M;
-                alpha_row(S, M, P, g * M + j, g, j);
+        if constexpr (PW) {
+            // whole envs' alpha tables and rows, one env per wave at a time, until the drone positions arrive
+            while (lds_peek(fl + F_D) < 1 && alpha_step()) {
             }
-            CHUNK_T1(2);
+        } else {
+            lds_signal(fl + F_A);
+            // alpha rows while the drone wave still integrates: once every pair is in the table, row chunks
+            // are taken until the drone positions arrive; the rest follows the drone hand-off below
+            for (int spins = 0; spins < (1 << 22); ++spins) {
+                if (lds_peek(fl + F_D) >= 1) break;
+                if (lds_peek(fl + F_A) < W1) { __builtin_amdgcn_s_sleep(1); continue; }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");   // the pair table
+                const int b = grab(fl + C_ROWS, 64), u = b + lane;
+                if (b >= nf * M) break;
+                CHUNK_T0;
+                if (u < nf * M) {
+                    const int f = qdiv(u, M, rM), g = flist[f], j = u - f * M;
+                    alpha_row(S, M, P, g * M + j, g, j);
+                }
+                CHUNK_T1(2);
+            }
         }
         if (ct == 0) TS(8, (long long)clock64());
         lds_wait(fl + F_D, 1, p.err);
@@ -874,6 +1053,31 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
             CHUNK_T1(1);
         }
         lds_signal(fl + F_H);
+        const float rN = 1.0f / (float)N;
+        if constexpr (PW) {
+            while (alpha_step()) {   // the rest of the alpha work (the current env first)
+            }
+            cow_sync(fl + F_W, W1, false, p.err);   // every alpha row (aux, auy) is written
+            if (ct == 0) TS(21, (long long)clock64());
+            // shepherd / predator terms and the velocity update, one flocking env per wave at a time in its
+            // slot: the env's (cow, drone) items, then each cow's terms in drone order
+            const int MN = M * N;
+            for (;;) {
+                const int f = grab(fl + C_DELTA, 1);
+                if (f >= nf) break;
+                CHUNK_T0;
+                const int g = flist[f], n = ei[I_N * G + g];
+                for (int q = lane; q < MN; q += 64) {
+                    const int j = qdiv(q, N, rN), k = q - j * N;
+                    if (k < n) delta_term(S, N, g * M + j, g, k, tb, tf, q, MN);
+                }
+                wave_sync();
+                for (int j = lane; j < M; j += 64) flock_combine(p, S, N, M, e0, g * M + j, n, tb, tf, j * N, MN);
+                wave_sync();   // the slot is free for the next env
+                CHUNK_T1(3);
+            }
+            if (ct == 0) TS(16, (long long)clock64());
+        } else {
         // the alpha rows only feed the velocity update: they wait until the drone wave has its hand-off
         lds_wait(fl + F_A, W1, p.err);   // every pair of the table
         if (ct == 0) TS(20, (long long)clock64());
@@ -890,7 +1094,7 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
         cow_sync(fl + F_W, W1, false, p.err);   // every alpha row read the pair table: its space now takes the drone terms
         if (ct == 0) TS(21, (long long)clock64());
         const int T = G * M * N, MN = M * N;
-        const float rMN = 1.0f / (float)MN, rN = 1.0f / (float)N;
+        const float rMN = 1.0f / (float)MN;
         // (cow, drone) items of flocking envs: shepherd and predator terms.  A chunk of 64 items holds
         // whole cows when N divides 64 (the cow's N items are consecutive): the wave that computed a cow's
         // terms then finishes that cow's velocity update itself (lane k = 0), with no workgroup sync.
@@ -906,11 +1110,11 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
                 const int rem = q - f * MN;
                 j = qdiv(rem, N, rN); k = rem - j * N;
                 g = flist[f]; n = ei[I_N * G + g];
-                if (k < n) delta_term(S, N, M, g * M + j, g, k, T);
+                if (k < n) delta_term(S, N, g * M + j, g, k, S.td, S.tdf, (g * M + j) * N + k, T);
             }
             if (fuse) {
                 wave_sync();   // the cow's terms, written by other lanes of this wave
-                if (valid && k == 0) flock_combine(p, S, N, M, e0, g * M + j, n, T);
+                if (valid && k == 0) flock_combine(p, S, N, M, e0, g * M + j, n, S.td, S.tdf, (g * M + j) * N, T);
             }
             CHUNK_T1(3);
         }
@@ -924,10 +1128,11 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
                 CHUNK_T0;
                 if (u < nf * M) {
                     const int f = qdiv(u, M, rM), g = flist[f], j = u - f * M;
-                    flock_combine(p, S, N, M, e0, g * M + j, ei[I_N * G + g], T);
+                    flock_combine(p, S, N, M, e0, g * M + j, ei[I_N * G + g], S.td, S.tdf, (g * M + j) * N, T);
                 }
                 CHUNK_T1(4);
             }
+        }
         }
         if (lane == 0) TS(40 + (tid >> 6), (long long)clock64());   // this cow wave's flock work done
         if (ct == 0) TS(31, (long long)nf);
@@ -1018,7 +1223,7 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
     if (tid == 0) { TS(14, (long long)clock64()); TS(1, (long long)wall_clock64()); }
 }
 
-template <class R, int MODE, int GT, int NT, int MT, bool PHYS = false>
+template <class R, int MODE, int GT, int NT, int MT, bool PHYS = false, bool PW = false>
 static hipError_t launch_v2_kernel(const StepParams<R>& p, int block, size_t lds, hipStream_t st, bool launch) {
     // opt-in to > 64 KiB of dynamic LDS, once per device (the attribute is per device context)
     static std::atomic<unsigned long long> attr_set{0};
@@ -1027,14 +1232,14 @@ static hipError_t launch_v2_kernel(const StepParams<R>& p, int block, size_t lds
     if (e != hipSuccess) return e;
     const unsigned long long bit = 1ull << (dev & 63);
     if (!(attr_set.load(std::memory_order_relaxed) & bit)) {
-        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_step2<R, MODE, GT, NT, MT, PHYS>),
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_step2<R, MODE, GT, NT, MT, PHYS, PW>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr_set.fetch_or(bit, std::memory_order_relaxed);
     }
     if (!launch) return hipSuccess;
     dim3 grid((p.E + p.G - 1) / p.G);
-    hipLaunchKernelGGL((k_step2<R, MODE, GT, NT, MT, PHYS>), grid, dim3(block), lds, st, p);
+    hipLaunchKernelGGL((k_step2<R, MODE, GT, NT, MT, PHYS, PW>), grid, dim3(block), lds, st, p);
     return hipGetLastError();
 }
 
@@ -1047,10 +1252,13 @@ hipError_t launch_step_v2(const StepParams<R>& p, int block, size_t lds, hipStre
         if (G == 16 && N == 4 && M == 16) return launch_v2_kernel<R, 0, 16, 4, 16, true>(p, block, lds, st, launch);   // configs[3]
         return launch_v2_kernel<R, 0, 0, 0, 0, true>(p, block, lds, st, launch);
     }
-    if (p.mode == 1) {
-        if (G == 4 && N == 4 && M == 32) return launch_v2_kernel<R, 1, 4, 4, 32>(p, block, lds, st, launch);     // configs[4]
-        return launch_v2_kernel<R, 1, 0, 0, 0>(p, block, lds, st, launch);
+    if (p.pw) {   // per-wave env tables (herds > 16 cows)
+        if (p.mode == 1 && G == 16 && N == 4 && M == 32)
+            return launch_v2_kernel<R, 1, 16, 4, 32, false, true>(p, block, lds, st, launch);   // configs[4]
+        if (p.mode == 1) return launch_v2_kernel<R, 1, 0, 0, 0, false, true>(p, block, lds, st, launch);
+        return launch_v2_kernel<R, 0, 0, 0, 0, false, true>(p, block, lds, st, launch);
     }
+    if (p.mode == 1) return launch_v2_kernel<R, 1, 0, 0, 0>(p, block, lds, st, launch);
     if (G == 8 && N == 4 && M == 16) return launch_v2_kernel<R, 0, 8, 4, 16>(p, block, lds, st, launch);          // configs[3]
     if (G == 16 && N == 4 && M == 16) return launch_v2_kernel<R, 0, 16, 4, 16>(p, block, lds, st, launch);         // configs[3], 512 threads
     if (G == 16 && N == 2 && M == 8) return launch_v2_kernel<R, 0, 16, 2, 8>(p, block, lds, st, launch);          // configs[2]

@@ -319,6 +319,10 @@ def test_full_size_properties():
                                              (0, 4, 16, 1000, (4, 128)), (0, 4, 16, 999, (2, 128)),
                                              (0, 4, 16, 1001, (8, 256)), (0, 4, 16, 1003, (16, 512)), (1, 5, 16, 333, (3, 128)),
                                              (0, 2, 8, 700, (1, 256)),
+                                             # per-wave env tables (> 16 cows): configs[4] at full size and
+                                             # other geometries, CTDE and MARL
+                                             (1, 4, 32, 4096, None), (1, 4, 32, 1000, (8, 512)), (1, 4, 32, 999, (4, 256)),
+                                             (0, 4, 32, 1001, (8, 256)), (1, 3, 24, 513, (16, 512)), (0, 2, 20, 300, (2, 128)),
                                              # physics variants (BaseAviary.py:420-450): DYN, GND, DRAG, DW, all
                                              (0, 4, 16, 4096, "dyn"), (0, 4, 16, 1000, "pyb_gnd"),
                                              (0, 4, 16, 1000, "pyb_drag"), (0, 6, 8, 1000, "pyb_dw"),

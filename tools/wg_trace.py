@@ -119,6 +119,11 @@ def trace(mode, E, n, m, prec, G=None, B=None, steps=4):
 
 
 def main():
+    if len(sys.argv) >= 5:   # one config: mode E n m [G B]
+        a = sys.argv[1:]
+        geom = (int(a[4]), int(a[5])) if len(a) >= 6 else (None, None)
+        trace(a[0], int(a[1]), int(a[2]), int(a[3]), "f64", *geom)
+        return
     precs = sys.argv[1:] or ["f64"]
     for prec in precs:
         trace("ctde", 4096, 4, 16, prec)
