@@ -100,7 +100,7 @@ struct V2Layout {
         const size_t shared = 4 * (size_t)G * P > 6 * (size_t)G * M * N ? 4 * (size_t)G * P : 6 * (size_t)G * M * N;
         size_t o = 0;
         off[CX] = o;     o = al(o + 8 * (size_t)G * M * rb);         // cx cy cvx cvy aux auy spx spy
-        off[DRONE] = o;  o = al(o + 12 * (size_t)G * N * rb);        // dx dy dz pa pb sa sb ca cb scat psp mrew
+        off[DRONE] = o;  o = al(o + 14 * (size_t)G * N * rb);        // dx dy dz pa pb sa sb ca cb scat psp mrew mq meor
         off[DCOW] = o;   o = al(o + (size_t)G * N * M * rb);         // cow-drone distances
         off[ENVR] = o;   o = al(o + 4 * (size_t)G * rb);             // prev clock, herd centroid x y
         off[PAIRS] = o;  o = al(o + (W ? (size_t)W * slot : shared) * rb);   // alpha pair table(s), then shepherd terms
@@ -112,7 +112,7 @@ struct V2Layout {
         const size_t tabs = W ? (size_t)W : (size_t)G;               // pair flags and term flags: per slot / per env
         // W > 0: no pair flags; per-cow "has a neighbour in sensing range" bytes and, per slot, the queue of
         // the env's pairs inside the bump's support (u16 pair indices)
-        off[BYTES] = o;  o = al(o + (W ? al((size_t)G * M) + 2 * (size_t)W * P : (size_t)G * P) + 3 * (size_t)G * N +
+        off[BYTES] = o;  o = al(o + (W ? 8 * (size_t)G * M + al((size_t)G * M) + 2 * (size_t)W * P : (size_t)G * P) + 3 * (size_t)G * N +
                                 (size_t)G * M + tabs * M * N);
         off[NOFF] = o;
     }

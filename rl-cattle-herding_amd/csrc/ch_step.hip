@@ -128,6 +128,7 @@ struct V2Smem {
     R *dx, *dy, *dz;                                 // [G*N] drone position after physics
     R *pa, *pb, *sa, *sb, *ca, *cb, *scat, *psp;     // [G*N] per-drone reward terms
     R* mrew;                                         // [G*N] MARL per-agent reward scratch
+    R *mq, *meor;                                    // [G*N] MARL: reward without the approach term, end-of-episode bonus
     R* dcow;                                         // [G*N*M] cow-drone distances, (g*N + k)*M + j
     R *prev, *clock, *hcx, *hcy;                     // [G] env reals; herd centroid (cow waves)
     R *tgx, *tgy, *tcx, *tcy;                        // [G*P] alpha pair table
@@ -140,6 +141,7 @@ struct V2Smem {
     uint8_t *pflag, *dflags, *herded, *md1, *md2;    // [G*P], [G*N], [G*M], [G*N], [G*N]
     uint8_t* tdf;                                    // [G*M*N] shepherd term in range | predator in range << 1
     uint8_t* hasnb;                                  // PW: [G*M] cow has a neighbour within sensing range
+    unsigned long long* nbm;                         // PW: [G*M] neighbours k whose pair is inside the bump support
     uint16_t* queue;                                 // PW: [W][P] pairs of the slot's env inside the bump support
 
     __device__ V2Smem(unsigned char* base, const V2Layout& L) {
@@ -148,7 +150,7 @@ struct V2Smem {
         spx = auy + GM; spy = spx + GM;
         dx = (R*)(base + L.off[V2Layout::DRONE]); dy = dx + GN; dz = dy + GN;
         pa = dz + GN; pb = pa + GN; sa = pb + GN; sb = sa + GN; ca = sb + GN; cb = ca + GN; scat = cb + GN;
-        psp = scat + GN; mrew = psp + GN;
+        psp = scat + GN; mrew = psp + GN; mq = mrew + GN; meor = mq + GN;
         dcow = (R*)(base + L.off[V2Layout::DCOW]);
         prev = (R*)(base + L.off[V2Layout::ENVR]); clock = prev + L.G; hcx = clock + L.G; hcy = hcx + L.G;
         pl = (const uint16_t*)(base + L.off[V2Layout::PAIRL]);
@@ -159,10 +161,11 @@ struct V2Smem {
         flags = ei + I_COUNT * L.G + 2 * L.G + 2;
         LT = (Level*)(base + L.off[V2Layout::LEVELS]);
         pflag = base + L.off[V2Layout::BYTES];
-        hasnb = pflag;
+        nbm = reinterpret_cast<unsigned long long*>(pflag);   // W > 0 only (BYTES is 16-byte aligned)
+        hasnb = pflag + 8 * GM;
         const int GMa = (GM + 15) & ~15;
-        queue = reinterpret_cast<uint16_t*>(pflag + GMa);   // W > 0 only
-        dflags = L.W ? pflag + GMa + 2 * L.W * L.P : pflag + GP;
+        queue = reinterpret_cast<uint16_t*>(hasnb + GMa);   // W > 0 only
+        dflags = L.W ? hasnb + GMa + 2 * L.W * L.P : pflag + GP;
         herded = dflags + GN; md1 = herded + GM;
         md2 = md1 + GN; tdf = md2 + GN;
     }
@@ -298,35 +301,41 @@ __device__ __forceinline__ void alpha_row(V2Smem<R>& S, int M, int P, int u, int
 // (flockUtils.py:237-258, 327-337).  The consensus term b (p_hi - p_lo) is not stored: alpha_row_pw
 // recomputes it from the velocities with the same rounding.
 //
-// Two passes.  The cheap pass (one 64-pair chunk per call) evaluates sigma_norm(|z|) / r_alpha for every
-// pair; the bump is exactly 0 above 1 (and for NaN), so such a pair's table entry is +0 -- what the full
-// evaluation stores -- and only pairs with z <= 1 are queued.  The expensive pass (cos of the bump,
-// sigma_1, the divisions) then runs on full waves of queued pairs.  In a spread herd most pairs are
-// outside the lattice range d_alpha = 1.2 m, so most lanes skip the expensive part.
+// Sparse in the bump's support.  The bump is exactly 0 for sigma_norm(|z|) / r_alpha > 1, i.e. beyond
+// the lattice range d_alpha = 1.2 m, and such a pair adds +-0 to both rows, which leaves a row sum that
+// starts at +0 unchanged.  A cheap pass over all pairs (no square root) queues the pairs with
+// |z|^2 <= 1.44 (1 + 1e-9) -- a superset of the support: any pair beyond it has z > 1 + 5e-10 exactly and
+// z > 1 as computed -- and marks them in both cows' neighbour masks; the full evaluation (square roots,
+// the bump's cos, sigma_1, divisions) runs on full waves of queued pairs only, and the rows visit only
+// masked neighbours, in ascending neighbour order like the dense loop.
+constexpr double kAlphaSupport2 = 1.44 * (1.0 + 1e-9);
 template <class R>
-__device__ __forceinline__ void alpha_cheap_pw(V2Smem<R>& S, int M, int P, int g, int c, R* tb, uint16_t* qu,
-                                               int& qn) {
-    const R ra = sigma_norm_n(R(1.2));
+__device__ __forceinline__ void alpha_cheap_pw(V2Smem<R>& S, int M, int P, int g, uint16_t* qu, int& qn) {
     const int lane = threadIdx.x & 63;
-    const int r = c * 64 + lane;
-    bool full = false;
-    if (r < P) {
-        const uint32_t pr = S.pl[r];
-        const int bi = g * M + (pr & 0xff), bj = g * M + (pr >> 8);
-        const R zx = S.cx[bj] - S.cx[bi], zy = S.cy[bj] - S.cy[bi];
-        const R nrm = sqrt(zx * zx + zy * zy);
-        if (nrm <= R(999)) {   // within sensing range: both cows have a neighbour (the rows' nb > 0)
-            S.hasnb[bi] = 1;
-            S.hasnb[bj] = 1;
-            const R den = sqrt(R(1) + R(kEps) * (nrm * nrm));   // pair_terms_n's z, same operations
-            const R sn = divc(den - R(1), R(kEps));
-            full = divc(sn, ra) <= R(1);
+    for (int r0 = 0; r0 < P; r0 += 64) {
+        const int r = r0 + lane;
+        bool cand = false;
+        if (r < P) {
+            const uint32_t pr = S.pl[r];
+            const int li = pr & 0xff, hi = pr >> 8;
+            const int bi = g * M + li, bj = g * M + hi;
+            const R zx = S.cx[bj] - S.cx[bi], zy = S.cy[bj] - S.cy[bi];
+            const R n2 = zx * zx + zy * zy;
+            // |z| <= 999 (sensing range) without the square root away from the boundary: sqrt is
+            // correctly rounded and monotonic, and sqrt(998001) = 999 exactly
+            bool sense = n2 <= R(998001.0);
+            if (!sense && n2 < R(998010.0)) sense = sqrt(n2) <= R(999);
+            if (sense) { S.hasnb[bi] = 1; S.hasnb[bj] = 1; }
+            cand = n2 <= R(kAlphaSupport2);
+            if (cand) {
+                atomicOr(&S.nbm[bi], 1ull << hi);
+                atomicOr(&S.nbm[bj], 1ull << li);
+            }
         }
-        if (!full) { tb[r] = R(0); tb[P + r] = R(0); tb[2 * P + r] = R(0); }
+        const unsigned long long m = __ballot(cand);
+        if (cand) qu[qn + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)r;
+        qn += __popcll(m);
     }
-    const unsigned long long m = __ballot(full);
-    if (full) qu[qn + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)r;
-    qn += __popcll(m);
 }
 
 template <class R>
@@ -345,17 +354,17 @@ __device__ __forceinline__ void alpha_full_pw(V2Smem<R>& S, int M, int P, int g,
     tb[r] = gx; tb[P + r] = gy; tb[2 * P + r] = b;
 }
 
-// alpha row of cow j of env g from the wave's slot, in neighbour order (as alpha_row).  The pair's
-// consensus term is b * (p_hi - p_lo), hi/lo the pair's cows, exactly as the shared table holds it; a
-// pair outside the bump support has b = +0 and adds +-0, which leaves the row sum unchanged.
+// alpha row of cow j of env g from the wave's slot, in neighbour order (as alpha_row), visiting the
+// masked neighbours only.  The pair's consensus term is b * (p_hi - p_lo), hi/lo the pair's cows,
+// exactly as the shared table holds it.
 template <class R>
 __device__ __forceinline__ void alpha_row_pw(V2Smem<R>& S, int M, int P, int g, int j, const R* tb) {
     const R C2A = R(2 * 1.7320508075688772);
     const int u = g * M + j;
     R gx = 0, gy = 0, cxx = 0, cyy = 0, ux = 0, uy = 0;
     const R pjx = S.cvx[u], pjy = S.cvy[u];
-    CH_UNROLL for (int k = 0; k < M; ++k) {
-        if (k == j) continue;
+    for (unsigned long long m = S.nbm[u]; m; m &= m - 1) {
+        const int k = __ffsll((long long)m) - 1;
         const bool fwd = j < k;
         const int idx = fwd ? tri(j, k, M) : tri(k, j, M);
         const R tgx = tb[idx], tgy = tb[P + idx], b = tb[2 * P + idx];
@@ -387,9 +396,17 @@ __device__ __forceinline__ void delta_term(V2Smem<R>& S, int N, int u, int g, in
         R mu = d / R(1.0) < R(1.0) ? d / R(1.0) : R(1.0);
         R akx = difx / d, aky = dify / d;
         R P00 = R(1) - akx * akx, P01 = R(0) - akx * aky, P10 = R(0) - aky * akx, P11 = R(1) - aky * aky;
-        R qkx = mu * qix + (R(1) - mu) * yx, qky = mu * qiy + (R(1) - mu) * yy;
         R pkx = mu * (P00 * pix + P01 * piy), pky = mu * (P10 * pix + P11 * piy);
-        pair_terms(qix, qiy, pix, piy, qkx, qky, pkx, pky, ra_b, da_b, t[0], t[1], t[2], t[3]);
+        if (mu == R(1) && isfinite(yx) && isfinite(yy) && isfinite(qix) && isfinite(qiy)) {
+            // a drone 1 m away or more: q_ik = 1 q_i + 0 y_k = q_i exactly, so pair_terms sees z = +0:
+            // |z| = 0, den = 1, sigma_norm = 0, bump(0) = 1, gradient ph * (0 / 1) = +-0 (+0 in the table),
+            // consensus 1 * (p_ik - p_i) -- the same values without the square roots and divisions
+            t[2] = pkx - pix;
+            t[3] = pky - piy;
+        } else {
+            R qkx = mu * qix + (R(1) - mu) * yx, qky = mu * qiy + (R(1) - mu) * yy;
+            pair_terms(qix, qiy, pix, piy, qkx, qky, pkx, pky, ra_b, da_b, t[0], t[1], t[2], t[3]);
+        }
     }
     if (pr) {
         R d3 = cube(dn);
@@ -511,7 +528,7 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
             reinterpret_cast<uint32_t*>(S.LT)[k] = reinterpret_cast<const uint32_t*>(kLevels)[k];
         for (int k = ct; k < P; k += CW) const_cast<uint16_t*>(S.pl)[k] = p.pairs[k];
         if constexpr (PW)
-            for (int k = ct; k < G * M; k += CW) S.hasnb[k] = 0;
+            for (int k = ct; k < G * M; k += CW) { S.hasnb[k] = 0; S.nbm[k] = 0; }
         if (ct < 64) {   // the first cow wave: env scalars, one env per lane
         const int g = ct;
         bool flk = false;
@@ -662,6 +679,43 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
                 if (d < best) best = d;
             }
             S.scat[tid] = cattle_spacing(best, R(p.cs_cc));
+            if constexpr (marl) {
+                // MARLCattleAviary._computeReward's per-agent part at the step's starting level
+                // (MARLCattleAviary.py:110-178), on every drone lane at once: the prefix
+                // P = simple w_s + complex w_c + 0.1 w_surv (psp), Q = P + eff/100 w_eff + cattle w_cat --
+                // the whole reward when the approach term is +-0, i.e. for every call but the first of a step
+                // (mq) -- and the end-of-episode bonus (meor, 183-241).  The env lane then only chains the
+                // calls' side effects (bookkeeping below); cent and eff are computed as the env lane does.
+                const int g = dg, n = n0, b0 = dg * N;
+                const int lv = ei[I_LEVEL * G + g];
+                const Level& Lv = LT[lv];
+                const R a = S.pa[tid], b = S.pb[tid], sa = S.sa[tid], sb = S.sb[tid], ca = S.ca[tid], cb = S.cb[tid];
+                R simple = (sa + sb) / R(2), cplx = (ca + cb) / R(2);
+                if (!p.compat) {
+                    if (!(b < R(INFINITY))) { simple = sa; cplx = ca; }
+                    if (!(a < R(INFINITY))) { simple = 0; cplx = 0; }
+                }
+                R P = 0;
+                P += simple * R(Lv.w_simple);
+                P += cplx * R(Lv.w_complex);
+                P += R(0.1) * R(Lv.w_survival);
+                R sdx = 0, sdy = 0;
+                CH_UNROLL for (int i = 0; i < N; ++i) {
+                    const bool li = i < n;
+                    sdx += li ? S.dx[b0 + i] : R(0); sdy += li ? S.dy[b0 + i] : R(0);
+                }
+                sdx = divc(sdx, R(n)); sdy = divc(sdy, R(n));
+                const R scx = S.hcx[g], scy = S.hcy[g];
+                const R ex = sdx - scx, ey = sdy - scy;
+                const R cent = sqrt(ex * ex + ey * ey + R(0) * R(0));
+                const R eff = R((double)ei[I_HERD * G + g] / M * 100);
+                R Q = P;
+                Q += divc(eff, R(100)) * R(Lv.w_eff);
+                Q += S.scat[tid] * R(Lv.w_cattle);
+                S.psp[tid] = P;
+                S.mq[tid] = Q;
+                S.meor[tid] = marl_end_of_episode_L(Lv, lv, a, b, cent, eff, norm2(scx - pos[0], scy - pos[1]), n);
+            }
         }
         wave_sync();
         if (tid == 0) TS(26, (long long)clock64());
@@ -710,6 +764,7 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
             }
             if (anynan) ms = R(NAN);
             const bool time_up = (double)f_sc / p.ctrl_freq > p.episode_len;
+            if (g == 0) TS(32, (long long)clock64());
             if constexpr (!marl) {
                 // CattleAviary: _computeReward (CattleAviary.py:213-332), then _computeTerminated twice and
                 // _computeTruncated.  The terminated calls read nothing the reward writes (the reward uses the
@@ -739,26 +794,26 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
                 // earlier (MARLCattleAviary.py:376)
                 const bool time_up_w = (double)(f_sc + 1) / p.ctrl_freq > p.episode_len;
                 constexpr int NR = NT ? NT : 1;
-                R r_pa[NR], r_pb[NR], r_sa[NR], r_sb[NR], r_ca[NR], r_cb[NR], r_sc[NR], r_dh[NR], r_rw[NR];
+                R r_pa[NR], r_pb[NR], r_sc[NR], r_dh[NR], r_rw[NR];
+                R r_pp[NR], r_qq[NR], r_eo[NR];
                 uint8_t r_df[NR], r_d1[NR];
                 if constexpr (NT > 0) {
                     CH_UNROLL for (int i = 0; i < NT; ++i) {
-                        r_pa[i] = S.pa[b0 + i]; r_pb[i] = S.pb[b0 + i]; r_sa[i] = S.sa[b0 + i]; r_sb[i] = S.sb[b0 + i];
-                        r_ca[i] = S.ca[b0 + i]; r_cb[i] = S.cb[b0 + i]; r_sc[i] = S.scat[b0 + i];
+                        r_pa[i] = S.pa[b0 + i]; r_pb[i] = S.pb[b0 + i]; r_sc[i] = S.scat[b0 + i];
                         r_dh[i] = norm2(scx - S.dx[b0 + i], scy - S.dy[b0 + i]);   // drone to herd centroid (level 4/6 bonus)
                         r_df[i] = S.dflags[b0 + i];
+                        r_pp[i] = S.psp[b0 + i]; r_qq[i] = S.mq[b0 + i]; r_eo[i] = S.meor[b0 + i];
                     }
                 }
 #define AG(arr, lds) [&](int i_) { if constexpr (NT > 0) return arr[i_]; else return lds; }
                 auto PA = AG(r_pa, S.pa[b0 + i_]);
                 auto PB = AG(r_pb, S.pb[b0 + i_]);
-                auto SA = AG(r_sa, S.sa[b0 + i_]);
-                auto SB = AG(r_sb, S.sb[b0 + i_]);
-                auto CA = AG(r_ca, S.ca[b0 + i_]);
-                auto CB = AG(r_cb, S.cb[b0 + i_]);
                 auto SC = AG(r_sc, S.scat[b0 + i_]);
                 auto DH = AG(r_dh, norm2(scx - S.dx[b0 + i_], scy - S.dy[b0 + i_]));
                 auto DF = AG(r_df, S.dflags[b0 + i_]);
+                auto PP = AG(r_pp, S.psp[b0 + i_]);
+                auto QQ = AG(r_qq, S.mq[b0 + i_]);
+                auto EO = AG(r_eo, S.meor[b0 + i_]);
 #undef AG
                 Level Lc = LT[level];   // the current level's constants (re-read when the level changes)
                 const R approach_div = max_step + R(1e-6);
@@ -777,80 +832,141 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
                 };
                 auto reward_i = [&](int i, bool tu) -> R {
                     const R a = PA(i), b = PB(i);
-                    R sa, sb, ca, cb;
-                    if (level == lvl0) { sa = SA(i); sb = SB(i); ca = CA(i); cb = CB(i); }
-                    else { sa = simple_spacing(a, Lc); sb = simple_spacing(b, Lc); ca = complex_spacing(a, Lc); cb = complex_spacing(b, Lc); }
-                    R simple = (sa + sb) / R(2), cplx = (ca + cb) / R(2);
-                    if (!p.compat) {
-                        if (!(b < R(INFINITY))) { simple = sa; cplx = ca; }
-                        if (!(a < R(INFINITY))) { simple = 0; cplx = 0; }
-                    }
-                    R r = 0;
-                    r += simple * R(Lc.w_simple);
-                    r += cplx * R(Lc.w_complex);
-                    r += R(0.1) * R(Lc.w_survival);
+                    const bool same = level == lvl0;   // the drone lanes' prefixes hold for this level
                     R change = has_prev ? prev - cent : R(0.0);
                     prev = cent; has_prev = 1;
-                    r += clip(divc(change, approach_div) * R(5), R(-1.0), R(1.0)) * R(Lc.w_approach);
-                    r += eff100 * R(Lc.w_eff);
-                    r += SC(i) * R(Lc.w_cattle);
+                    R r;
+                    if (same && change == R(0)) {
+                        // the approach term is +-0 and leaves P unchanged: the reward is Q
+                        r = QQ(i);
+                    } else {
+                        if (same) {
+                            r = PP(i);
+                        } else {
+                            const R sa = simple_spacing(a, Lc), sb = simple_spacing(b, Lc);
+                            const R ca = complex_spacing(a, Lc), cb = complex_spacing(b, Lc);
+                            R simple = (sa + sb) / R(2), cplx = (ca + cb) / R(2);
+                            if (!p.compat) {
+                                if (!(b < R(INFINITY))) { simple = sa; cplx = ca; }
+                                if (!(a < R(INFINITY))) { simple = 0; cplx = 0; }
+                            }
+                            r = 0;
+                            r += simple * R(Lc.w_simple);
+                            r += cplx * R(Lc.w_complex);
+                            r += R(0.1) * R(Lc.w_survival);
+                        }
+                        r += clip(divc(change, approach_div) * R(5), R(-1.0), R(1.0)) * R(Lc.w_approach);
+                        r += eff100 * R(Lc.w_eff);
+                        r += SC(i) * R(Lc.w_cattle);
+                    }
                     if (term_call_L(Lc, level, clock, inc, ms, cent, eff)) {
-                        r += marl_end_of_episode_L(Lc, level, a, b, cent, eff, DH(i), n);
+                        r += same ? EO(i) : marl_end_of_episode_L(Lc, level, a, b, cent, eff, DH(i), n);
                         succeed();
                     } else if (trunc_i(i, tu)) {
                         r -= R(50);
                     }
                     return r;
                 };
-                // env.step's own dicts (rllib_envs/BaseAviary.py:425-431)
-                CH_UNROLL for (int i = 0; i < N; ++i) {
-                    if (i >= n) break;
-                    const R rr = reward_i(i, time_up);
-                    if constexpr (NT > 0) r_rw[i] = rr; else S.mrew[b0 + i] = rr;
-                }
-                CH_UNROLL for (int i = 0; i < N; ++i) {
-                    if (i >= n) break;
-                    const uint8_t d = term_call_L(Lc, level, clock, inc, ms, cent, eff);
-                    if constexpr (NT > 0) r_d1[i] = d; else S.md1[b0 + i] = d;
-                }
+                // Fast path (wrapper semantics, the common step): every terminated call of the step -- n in
+                // env.step's rewards, n for its dict, then a reward and a terminated call per live agent in
+                // the wrapper -- sees the same inputs, so whether any returns True follows from the level and,
+                // at levels 0/1, the clock recurrence alone.  If none does, there is no end-of-episode bonus,
+                // no curriculum step and no agent drop-out; every wrapper reward is Q (its approach term is +-0
+                // after env.step's first call) minus the truncation penalty.  Otherwise the calls run in order.
                 const int act0 = active;
-                if (p.marl_wrapper) {
-                    // the wrapper recomputes everything per live agent (marl_wrapper.py:104-110)
-                    done = 1;
-                    CH_UNROLL for (int i = 0; i < N; ++i) {
-                        R rr = R(NAN);
-                        uint8_t tt = 0, trr = 0;
-                        if (i < n && ((act0 >> i) & 1)) {
-                            rr = reward_i(i, time_up_w);
-                            tt = term_call_L(Lc, level, clock, inc, ms, cent, eff);
-                            trr = trunc_i(i, time_up_w);
+                bool fast = p.marl_wrapper != 0;
+                if (fast) {
+                    int nact = 0;
+                    CH_UNROLL for (int i = 0; i < N; ++i) nact += (i < n && ((act0 >> i) & 1)) ? 1 : 0;
+                    const int K = 2 * n + 2 * nact;
+                    R ck = clock;
+                    if (level == 0 || level == 1) {
+                        const R up = R(Lc.desired) + R(Lc.desired) * R(Lc.tol), lo = R(Lc.desired) - R(Lc.desired) * R(Lc.tol);
+                        if (ms < up && ms > lo) {
+                            for (int k = 0; k < K && fast; ++k) {
+                                ck += inc;
+                                if (ck >= R(Lc.hold)) fast = false;
+                            }
+                        } else if (K > 0) {
+                            ck = 0;
                         }
-                        p.reward[(long long)e * N + i] = (float)rr;
-                        p.term[(long long)e * N + i] = tt;
-                        p.trunc[(long long)e * N + i] = trr;
-                        if (i < n && rr == rr) ret += (double)rr;
-                        n_term += tt; n_trunc += trr;
-                        if (i < n && (((act0 >> i) & 1) || tt) && rr != rr) n_nan += 1;
-                        if (i < n && ((act0 >> i) & 1) && tt) active &= ~(1 << i);   // finished agents drop out
+                    } else if (K > 0) {
+                        fast = !term_call_L(Lc, level, ck, inc, ms, cent, eff);
                     }
-                    CH_UNROLL for (int i = 0; i < N; ++i)
-                        if (i < n && ((active >> i) & 1)) done = 0;   // __all__: every agent terminated (marl_wrapper.py:113-117)
-                } else {
-                    done = 1;   // bare env.step dicts: __all__ = all(done.values())
-                    CH_UNROLL for (int i = 0; i < N; ++i) {
-                        R rr = R(NAN);
-                        uint8_t tt = 0, trr = 0;
-                        if (i < n) {
-                            if constexpr (NT > 0) { rr = r_rw[i]; tt = r_d1[i]; } else { rr = S.mrew[b0 + i]; tt = S.md1[b0 + i]; }
-                            trr = trunc_i(i, time_up);
-                            done &= tt;
+                    if (fast) {
+                        clock = ck;
+                        if (n > 0) { prev = cent; has_prev = 1; }
+                        done = 1;
+                        CH_UNROLL for (int i = 0; i < N; ++i) {
+                            R rr = R(NAN);
+                            uint8_t trr = 0;
+                            if (i < n && ((act0 >> i) & 1)) {
+                                rr = QQ(i);
+                                trr = trunc_i(i, time_up_w);
+                                if (trr) rr -= R(50);
+                                done = 0;
+                            }
+                            p.reward[(long long)e * N + i] = (float)rr;
+                            p.term[(long long)e * N + i] = 0;
+                            p.trunc[(long long)e * N + i] = trr;
+                            if (i < n && rr == rr) ret += (double)rr;
+                            n_trunc += trr;
+                            if (i < n && ((act0 >> i) & 1) && rr != rr) n_nan += 1;
                         }
-                        p.reward[(long long)e * N + i] = (float)rr;
-                        p.term[(long long)e * N + i] = tt;
-                        p.trunc[(long long)e * N + i] = trr;
-                        if (i < n && rr == rr) ret += (double)rr;
-                        n_term += tt; n_trunc += trr;
-                        if (i < n && (((act0 >> i) & 1) || tt) && rr != rr) n_nan += 1;
+                    }
+                }
+                if (!fast) {
+                    if (g == 0) TS(33, (long long)clock64());
+                    // env.step's own dicts (rllib_envs/BaseAviary.py:425-431)
+                    CH_UNROLL for (int i = 0; i < N; ++i) {
+                        if (i >= n) break;
+                        const R rr = reward_i(i, time_up);
+                        if constexpr (NT > 0) r_rw[i] = rr; else S.mrew[b0 + i] = rr;
+                    }
+                    CH_UNROLL for (int i = 0; i < N; ++i) {
+                        if (i >= n) break;
+                        const uint8_t d = term_call_L(Lc, level, clock, inc, ms, cent, eff);
+                        if constexpr (NT > 0) r_d1[i] = d; else S.md1[b0 + i] = d;
+                    }
+                    if (g == 0) TS(34, (long long)clock64());
+                    if (p.marl_wrapper) {
+                        // the wrapper recomputes everything per live agent (marl_wrapper.py:104-110)
+                        done = 1;
+                        CH_UNROLL for (int i = 0; i < N; ++i) {
+                            R rr = R(NAN);
+                            uint8_t tt = 0, trr = 0;
+                            if (i < n && ((act0 >> i) & 1)) {
+                                rr = reward_i(i, time_up_w);
+                                tt = term_call_L(Lc, level, clock, inc, ms, cent, eff);
+                                trr = trunc_i(i, time_up_w);
+                            }
+                            p.reward[(long long)e * N + i] = (float)rr;
+                            p.term[(long long)e * N + i] = tt;
+                            p.trunc[(long long)e * N + i] = trr;
+                            if (i < n && rr == rr) ret += (double)rr;
+                            n_term += tt; n_trunc += trr;
+                            if (i < n && (((act0 >> i) & 1) || tt) && rr != rr) n_nan += 1;
+                            if (i < n && ((act0 >> i) & 1) && tt) active &= ~(1 << i);   // finished agents drop out
+                        }
+                        CH_UNROLL for (int i = 0; i < N; ++i)
+                            if (i < n && ((active >> i) & 1)) done = 0;   // __all__: every agent terminated (marl_wrapper.py:113-117)
+                    } else {
+                        done = 1;   // bare env.step dicts: __all__ = all(done.values())
+                        CH_UNROLL for (int i = 0; i < N; ++i) {
+                            R rr = R(NAN);
+                            uint8_t tt = 0, trr = 0;
+                            if (i < n) {
+                                if constexpr (NT > 0) { rr = r_rw[i]; tt = r_d1[i]; } else { rr = S.mrew[b0 + i]; tt = S.md1[b0 + i]; }
+                                trr = trunc_i(i, time_up);
+                                done &= tt;
+                            }
+                            p.reward[(long long)e * N + i] = (float)rr;
+                            p.term[(long long)e * N + i] = tt;
+                            p.trunc[(long long)e * N + i] = trr;
+                            if (i < n && rr == rr) ret += (double)rr;
+                            n_term += tt; n_trunc += trr;
+                            if (i < n && (((act0 >> i) & 1) || tt) && rr != rr) n_nan += 1;
+                        }
                     }
                 }
             }
@@ -958,8 +1074,9 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
             CHUNK_T0;
             const int g = flist[f_cur];
             if (ch < NCH) {
-                alpha_cheap_pw(S, M, P, g, ch, tb, qu, qn);
-                if (++ch == NCH) wave_sync();   // the queue and the +0 entries
+                alpha_cheap_pw(S, M, P, g, qu, qn);
+                ch = NCH;
+                wave_sync();   // the queue
             } else if (qd < qn) {
                 alpha_full_pw(S, M, P, g, qd, qn, tb, qu);
                 qd += 64;

@@ -28,6 +28,8 @@ def trace(mode, E, n, m, prec, G=None, B=None, steps=4):
     for _ in range(250):   # steady state: resets have desynchronised the flocking parity
         b.step(random_actions=True, autoreset=True, terminal_obs=False)
     L.ch__set_tstamp(b.handle, ctypes.c_void_p(ts.data_ptr()))
+    if os.environ.get("CH_PHASE_MASK"):
+        L.ch__set_phase_mask(b.handle, ctypes.c_int32(int(os.environ["CH_PHASE_MASK"])))
     print(f"== {prec} {mode} E={E} N={n} M={m} G={g.value} block={blk.value} lds={lds.value} grid={grid}")
     for s in range(steps):
         ts.zero_()
@@ -58,6 +60,7 @@ def trace(mode, E, n, m, prec, G=None, B=None, steps=4):
                   f"D {r2(9):.0f} H(drone) {r2(6):.0f} delta {r2(16):.0f} Q {r2(17):.0f} flock {r2(10):.0f} "
                   f"| cow waves done (mean per wave) {' '.join(f'{(t[sel, 40 + w] - t[sel, 2]).mean():.0f}' for w in range(1, blk.value // 64))} "
                   f"| drone book {r2(7):.0f} B1 {r2(13):.0f} end {r2(14):.0f}")
+        print(f"   bookkeeping: scalars+centroid {rel(32):.0f} marl-prep {rel(33):.0f} env.step dicts {rel(34):.0f}")
         print(f"   drone wave after H: dtaskB {rel(26):.0f} pre-fence {rel(27):.0f} published {rel(15):.0f} "
               f"reward {rel(19):.0f} metrics stored {rel(28):.0f} book {rel(7):.0f}")
         simd = (t[:, 22:26] >> 4) & 3
