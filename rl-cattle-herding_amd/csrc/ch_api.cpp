@@ -348,14 +348,15 @@ int ch_create(const ch_config* c, int64_t n_envs, int32_t device, ch_handle** ou
         h->G = G;
         h->lds = V2Layout(G, h->NC, h->M, h->P, c->mode, (int)h->rsize).bytes();
         h->block = 256;
-        // measured (tools/ab/g16.py): at 4 drones x 16 cattle one 512-thread workgroup of 16 envs per
-        // CU (a full 64-drone wave + 7 cow waves sharing the work counters) beats two 256-thread
-        // workgroups of 8 envs (23.7 vs 25.1 us/step at 4096 envs)
+        // measured (tools/geom_sweep.py, profiles/r02/geom_*.log): at 4 drones x 16 cattle one workgroup
+        // of 16 envs per CU (a full 64-drone wave + cow waves sharing the work counters) beats two of 8
+        // envs, and 11 cow waves (768 threads, 3 waves per SIMD) edge out 7 (24.1 vs 24.8 us at 4096 envs);
+        // the physics variants keep 512 (their register use allows 2 waves per SIMD)
         if (c->mode == CH_MODE_CTDE && h->NC == 4 && h->M == 16 && E >= 16 * (int64_t)cus &&
             V2Layout(16, 4, 16, h->P, c->mode, (int)h->rsize).bytes() <= budget) {
             h->G = 16;
             h->lds = V2Layout(16, 4, 16, h->P, c->mode, (int)h->rsize).bytes();
-            h->block = 512;
+            h->block = c->physics == CH_PHYS_PYB ? CH_V2_MAX_BLOCK : CH_V2_MAX_BLOCK_PW;
         }
         // measured (tools/ab/marl.py, MI355X, 4096 envs): the dataflow kernel wins for every CTDE size
         // (2x8 19.4 vs 41.1 us, 8x16 39.7 vs 55.8, 12x16 59.9 vs 67.1) and for MARL with up to 16
@@ -583,7 +584,9 @@ int ch__set_tstamp(ch_handle* h, long long* dev) {
 
 /* Internal diagnostics: override the v2 geometry (envs per workgroup, block size) for sweeps. */
 int ch__set_geometry(ch_handle* h, int32_t G, int32_t block) {
-    if (!h || G < 1 || G > 64 || G * h->NC > 64 || block < 128 || block > CH_V2_MAX_BLOCK || block % 64) return CH_ERR_INVALID;
+    if (!h || G < 1 || G > 64 || G * h->NC > 64 || block < 128 || block % 64 ||
+        block > ((h->pw || h->cfg.physics != CH_PHYS_PYB) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK))
+        return CH_ERR_INVALID;
     if (G * h->M > 3 * (block - 64)) return CH_ERR_UNSUPPORTED;   // the cow waves prefetch <= 3 spawn slots per lane
     const size_t lds = V2Layout(G, h->NC, h->M, h->P, h->cfg.mode, (int)h->rsize, h->pw ? block / 64 - 1 : 0).bytes();
     if (lds > 160 * 1024) return CH_ERR_UNSUPPORTED;

@@ -78,10 +78,13 @@ struct Level {
 
 // LDS carve of one v2 step workgroup (ch_step.hip); identical on host (size) and device (offsets).
 #ifndef CH_V2_MAX_BLOCK
-#define CH_V2_MAX_BLOCK 512   // v2 workgroup size bound (__launch_bounds__)
+#define CH_V2_MAX_BLOCK 768   // v2 workgroup size bound: 12 waves, 3 per SIMD (shared-table kernels)
+#endif
+#ifndef CH_V2_MAX_BLOCK_PW
+#define CH_V2_MAX_BLOCK_PW 512   // per-wave-table and physics-variant kernels: 8 waves (their register use allows 2 per SIMD)
 #endif
 constexpr int kV2EnvInts = 13;
-constexpr int kV2Flags = 16;         // LDS hand-off counters between the drone wave and the cow waves + work counters
+constexpr int kV2Flags = 20;         // LDS hand-off counters between the drone wave and the cow waves + work counters
 // W = 0: one alpha pair table for the whole workgroup (4 reals per pair, G*P pairs), reused for the
 // shepherd terms.  W > 0 ("per-wave env tables", large herds): each of the W cow waves owns a slot for
 // ONE env at a time -- 3 reals per pair (gradient x, y and the bump; the consensus term is recomputed
@@ -110,9 +113,9 @@ struct V2Layout {
         off[LEVELS] = o; o = al(o + 8 * sizeof(Level));              // curriculum table
         off[PAIRL] = o;  o = al(o + 2 * (size_t)P);                  // unordered cow pairs (i | j << 8)
         const size_t tabs = W ? (size_t)W : (size_t)G;               // pair flags and term flags: per slot / per env
-        // W > 0: no pair flags; per-cow "has a neighbour in sensing range" bytes and, per slot, the queue of
-        // the env's pairs inside the bump's support (u16 pair indices)
-        off[BYTES] = o;  o = al(o + (W ? 8 * (size_t)G * M + al((size_t)G * M) + 2 * (size_t)W * P : (size_t)G * P) + 3 * (size_t)G * N +
+        // per-cow neighbour masks (u64) and "has a neighbour in sensing range" bytes, then the queue of pairs
+        // inside the bump's support (u16; one per slot for W > 0, one for the workgroup otherwise)
+        off[BYTES] = o;  o = al(o + 8 * (size_t)G * M + al((size_t)G * M) + 2 * (size_t)tabs * P + 3 * (size_t)G * N +
                                 (size_t)G * M + tabs * M * N);
         off[NOFF] = o;
     }

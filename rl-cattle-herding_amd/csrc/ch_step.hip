@@ -36,7 +36,8 @@ enum { I_N = 0, I_SC, I_SCA, I_HASPREV, I_LEVEL, I_TALLY, I_SPAWN, I_ACTIVE, I_E
        I_HERD, I_COUNT };
 static_assert(I_COUNT == kV2EnvInts, "LDS env-int rows");
 enum { F_D = 0, F_T, F_H, F_A, F_E, F_R, F_X0, F_X1, F_X2,     // hand-off counters
-       C_PAIRS, C_ROWS, C_COWS, C_FLOCK, C_DELTA, F_W, F_Q };    // work counters (grab), cow-wave syncs
+       C_PAIRS, C_ROWS, C_COWS, C_FLOCK, C_DELTA, F_W, F_Q,      // work counters (grab), cow-wave syncs
+       Q_LEN, C_QUEUE, F_C };                                     // shared alpha queue: length, grab, cheap pass done
 // after the per-env rows: flocking-env list [G], reset-env list [G], their counts, then the counters
 #define FL_LIST (I_COUNT * G)
 #define RS_LIST (I_COUNT * G + G)
@@ -138,7 +139,7 @@ struct V2Smem {
     int* flags;
     Level* LT;                                       // curriculum table (curriculum_learning.py:10-194)
     const uint16_t* pl;                              // [P] unordered cow pairs, copied from p.pairs
-    uint8_t *pflag, *dflags, *herded, *md1, *md2;    // [G*P], [G*N], [G*M], [G*N], [G*N]
+    uint8_t *dflags, *herded, *md1, *md2;            // [G*N], [G*M], [G*N], [G*N]
     uint8_t* tdf;                                    // [G*M*N] shepherd term in range | predator in range << 1
     uint8_t* hasnb;                                  // PW: [G*M] cow has a neighbour within sensing range
     unsigned long long* nbm;                         // PW: [G*M] neighbours k whose pair is inside the bump support
@@ -160,12 +161,12 @@ struct V2Smem {
         ei = (int*)(base + L.off[V2Layout::EI]);
         flags = ei + I_COUNT * L.G + 2 * L.G + 2;
         LT = (Level*)(base + L.off[V2Layout::LEVELS]);
-        pflag = base + L.off[V2Layout::BYTES];
-        nbm = reinterpret_cast<unsigned long long*>(pflag);   // W > 0 only (BYTES is 16-byte aligned)
-        hasnb = pflag + 8 * GM;
+        unsigned char* bytes = base + L.off[V2Layout::BYTES];
+        nbm = reinterpret_cast<unsigned long long*>(bytes);   // BYTES is 16-byte aligned
+        hasnb = bytes + 8 * GM;
         const int GMa = (GM + 15) & ~15;
-        queue = reinterpret_cast<uint16_t*>(hasnb + GMa);   // W > 0 only
-        dflags = L.W ? hasnb + GMa + 2 * L.W * L.P : pflag + GP;
+        queue = reinterpret_cast<uint16_t*>(hasnb + GMa);
+        dflags = hasnb + GMa + 2 * GP;
         herded = dflags + GN; md1 = herded + GM;
         md2 = md1 + GN; tdf = md2 + GN;
     }
@@ -241,58 +242,95 @@ __device__ __forceinline__ int nearest_two(const R* dx, const R* dy, int b0, int
     return (i1 + 1) | ((i2 + 1) << 8);
 }
 
-// flock alpha term, pair form, for every flocking env (flockUtils.py:237-258, 327-337; MathUtils 11-58).
-// l = lane rank among the A lanes that share the table.
+// flock alpha term, pair form, for every flocking env (flockUtils.py:237-258, 327-337; MathUtils 11-58):
+// one table of the workgroup's unordered cow pairs, evaluated in the bump's support only.  The bump is
+// exactly 0 for sigma_norm(|z|) / r_alpha > 1 (beyond the lattice range d_alpha = 1.2 m); such a pair adds
+// +-0 to both rows, which leaves a row sum that starts at +0 unchanged.  A cheap pass over every pair (no
+// square root) marks the pairs with |z|^2 <= 1.44 (1 + 1e-9) -- a superset of the support, see
+// kAlphaSupport2 -- in both cows' neighbour masks and appends them to a queue; the full evaluation runs on
+// full waves of queued pairs; the rows visit the masked neighbours in ascending order like the dense loop.
+constexpr double kAlphaSupport2 = 1.44 * (1.0 + 1e-9);
+
+// |z| <= 999 (the sensing range) from |z|^2 without the square root away from the boundary: sqrt is
+// correctly rounded and monotonic, and sqrt(998001) = 999 exactly
+template <class R> __device__ __forceinline__ bool in_sensing(R n2) {
+    bool s = n2 <= R(998001.0);
+    if (!s && n2 < R(998010.0)) s = sqrt(n2) <= R(999);
+    return s;
+}
+
 template <class R>
-__device__ __forceinline__ void alpha_pairs(const StepParams<R>& p, V2Smem<R>& S, int G, int M, int P) {
-    const int nf = S.ei[NF_AT];
-    const int* flist = S.ei + FL_LIST;
-    const R ra = sigma_norm_n(R(1.2)), da = ra;
-    const int tot = nf * P;
+__device__ __forceinline__ void alpha_cheap(V2Smem<R>& S, int* fl, int M, int P, int nf, const int* flist) {
     const float rP = 1.0f / (float)P;
-    auto one = [&](int q) {
-        const int f = qdiv(q, P, rP), r = q - f * P, g = flist[f];
-        const uint32_t pr = S.pl[r];
-        const int bi = g * M + (pr & 0xff), bj = g * M + (pr >> 8);
-        const R zx = S.cx[bj] - S.cx[bi], zy = S.cy[bj] - S.cy[bi];
-        const R nrm = sqrt(zx * zx + zy * zy);
-        const int idx = g * P + r;
-        const bool in = nrm <= R(999);
-        S.pflag[idx] = in;
-        R gx = 0, gy = 0, cx = 0, cy = 0;
-        if (in) pair_terms_n(nrm, zx, zy, S.cvx[bi], S.cvy[bi], S.cvx[bj], S.cvy[bj], ra, da, gx, gy, cx, cy);
-        S.tgx[idx] = gx; S.tgy[idx] = gy; S.tcx[idx] = cx; S.tcy[idx] = cy;
-    };
     const int lane = threadIdx.x & 63;
-    for (;;) {   // 128 pairs per grab, two independent pairs per lane (instruction-level parallelism)
-        const int b = grab(S.flags + C_PAIRS, 128);
-        if (b >= tot) break;
-        CHUNK_T0;
-        if (b + lane < tot) one(b + lane);
-        if (b + 64 + lane < tot) one(b + 64 + lane);
-        CHUNK_T1(0);
+    for (;;) {
+        const int b = grab(fl + C_PAIRS, 64);
+        if (b >= nf * P) break;
+        const int q = b + lane;
+        bool cand = false;
+        int gi = 0;
+        if (q < nf * P) {
+            const int f = qdiv(q, P, rP), r = q - f * P, g = flist[f];
+            const uint32_t pr = S.pl[r];
+            const int li = pr & 0xff, hi = pr >> 8;
+            const int bi = g * M + li, bj = g * M + hi;
+            const R zx = S.cx[bj] - S.cx[bi], zy = S.cy[bj] - S.cy[bi];
+            const R n2 = zx * zx + zy * zy;
+            if (in_sensing(n2)) { S.hasnb[bi] = 1; S.hasnb[bj] = 1; }
+            cand = n2 <= R(kAlphaSupport2);
+            if (cand) {
+                atomicOr(&S.nbm[bi], 1ull << hi);
+                atomicOr(&S.nbm[bj], 1ull << li);
+            }
+            gi = g * P + r;
+        }
+        const unsigned long long m = __ballot(cand);
+        int base = 0;
+        if (lane == 0 && m) base = atomicAdd(fl + Q_LEN, (int)__popcll(m));
+        base = __builtin_amdgcn_readfirstlane(base);
+        if (cand) S.queue[base + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)gi;
     }
 }
 
-// alpha row of cow u = g*M + j in neighbour order, scaled by c2_alpha (flockUtils.py:237-258)
+template <class R>
+__device__ __forceinline__ void alpha_full(V2Smem<R>& S, int* fl, int M, int P) {
+    const R ra = sigma_norm_n(R(1.2)), da = ra;
+    const int qn = lds_peek(fl + Q_LEN);   // final: every cow wave's cheap pass is done (F_C)
+    const float rP = 1.0f / (float)P;
+    const int lane = threadIdx.x & 63;
+    for (;;) {
+        const int b = grab(fl + C_QUEUE, 64);
+        if (b >= qn) break;
+        if (b + lane < qn) {
+            const int gi = S.queue[b + lane];
+            const int g = qdiv(gi, P, rP), r = gi - g * P;
+            const uint32_t pr = S.pl[r];
+            const int bi = g * M + (pr & 0xff), bj = g * M + (pr >> 8);
+            const R zx = S.cx[bj] - S.cx[bi], zy = S.cy[bj] - S.cy[bi];
+            const R nrm = sqrt(zx * zx + zy * zy);
+            R gx = 0, gy = 0, cx = 0, cy = 0;
+            pair_terms_n(nrm, zx, zy, S.cvx[bi], S.cvy[bi], S.cvx[bj], S.cvy[bj], ra, da, gx, gy, cx, cy);
+            S.tgx[gi] = gx; S.tgy[gi] = gy; S.tcx[gi] = cx; S.tcy[gi] = cy;
+        }
+    }
+}
+
+// alpha row of cow u = g*M + j in neighbour order over its masked neighbours, scaled by c2_alpha
+// (flockUtils.py:237-258); the two directed contributions of a pair are exact negations
 template <class R>
 __device__ __forceinline__ void alpha_row(V2Smem<R>& S, int M, int P, int u, int g, int j) {
     const R C2A = R(2 * 1.7320508075688772);
     R gx = 0, gy = 0, cxx = 0, cyy = 0, ux = 0, uy = 0;
-    int nb = 0;
     const int pb = g * P;
-    CH_UNROLL for (int k = 0; k < M; ++k) {
-        if (k == j) continue;
+    for (unsigned long long m = S.nbm[u]; m; m &= m - 1) {
+        const int k = __ffsll((long long)m) - 1;
         const bool fwd = j < k;
         const int idx = pb + (fwd ? tri(j, k, M) : tri(k, j, M));
-        // out-of-range pairs hold +0 terms and adding (+/-)0 to a sum that starts at +0 changes
-        // nothing, so every entry is summed without waiting on its flag (no load -> branch chain)
-        nb += S.pflag[idx];
         const R tgx = S.tgx[idx], tgy = S.tgy[idx], tcx = S.tcx[idx], tcy = S.tcy[idx];
         gx += fwd ? tgx : -tgx; gy += fwd ? tgy : -tgy;
         cxx += fwd ? tcx : -tcx; cyy += fwd ? tcy : -tcy;
     }
-    if (nb > 0) { ux = C2A * gx + C2A * cxx; uy = C2A * gy + C2A * cyy; }
+    if (S.hasnb[u]) { ux = C2A * gx + C2A * cxx; uy = C2A * gy + C2A * cyy; }
     S.aux[u] = ux; S.auy[u] = uy;
 }
 
@@ -308,7 +346,6 @@ __device__ __forceinline__ void alpha_row(V2Smem<R>& S, int M, int P, int u, int
 // z > 1 as computed -- and marks them in both cows' neighbour masks; the full evaluation (square roots,
 // the bump's cos, sigma_1, divisions) runs on full waves of queued pairs only, and the rows visit only
 // masked neighbours, in ascending neighbour order like the dense loop.
-constexpr double kAlphaSupport2 = 1.44 * (1.0 + 1e-9);
 template <class R>
 __device__ __forceinline__ void alpha_cheap_pw(V2Smem<R>& S, int M, int P, int g, uint16_t* qu, int& qn) {
     const int lane = threadIdx.x & 63;
@@ -321,11 +358,7 @@ __device__ __forceinline__ void alpha_cheap_pw(V2Smem<R>& S, int M, int P, int g
             const int bi = g * M + li, bj = g * M + hi;
             const R zx = S.cx[bj] - S.cx[bi], zy = S.cy[bj] - S.cy[bi];
             const R n2 = zx * zx + zy * zy;
-            // |z| <= 999 (sensing range) without the square root away from the boundary: sqrt is
-            // correctly rounded and monotonic, and sqrt(998001) = 999 exactly
-            bool sense = n2 <= R(998001.0);
-            if (!sense && n2 < R(998010.0)) sense = sqrt(n2) <= R(999);
-            if (sense) { S.hasnb[bi] = 1; S.hasnb[bj] = 1; }
+            if (in_sensing(n2)) { S.hasnb[bi] = 1; S.hasnb[bj] = 1; }
             cand = n2 <= R(kAlphaSupport2);
             if (cand) {
                 atomicOr(&S.nbm[bi], 1ull << hi);
@@ -451,7 +484,7 @@ __device__ __forceinline__ void flock_combine(const StepParams<R>& p, V2Smem<R>&
 // GT/NT/MT > 0 specialise the kernel for one geometry (envs per workgroup, drones, cattle): the LDS
 // carve and all index arithmetic then fold to immediates, which keeps the kernel within the SGPR file.
 template <class R, int MODE, int GT, int NT, int MT, bool PHYS = false, bool PW = false>
-__global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
+__global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
     extern __shared__ __align__(16) unsigned char smem[];
     constexpr bool marl = MODE == 1;
     const int G = GT ? GT : p.G, N = NT ? NT : p.NC, M = MT ? MT : p.M, P = MT ? MT * (MT - 1) / 2 : p.P;
@@ -527,8 +560,7 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
         for (int k = ct; k < (int)(sizeof(kLevels) / 4); k += CW)
             reinterpret_cast<uint32_t*>(S.LT)[k] = reinterpret_cast<const uint32_t*>(kLevels)[k];
         for (int k = ct; k < P; k += CW) const_cast<uint16_t*>(S.pl)[k] = p.pairs[k];
-        if constexpr (PW)
-            for (int k = ct; k < G * M; k += CW) { S.hasnb[k] = 0; S.nbm[k] = 0; }
+        for (int k = ct; k < G * M; k += CW) { S.hasnb[k] = 0; S.nbm[k] = 0; }
         if (ct < 64) {   // the first cow wave: env scalars, one env per lane
         const int g = ct;
         bool flk = false;
@@ -1095,7 +1127,10 @@ __global__ __launch_bounds__(CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
             tf = S.tdf + (size_t)(tid / 64 - 1) * M * N;
             qu = S.queue + (size_t)(tid / 64 - 1) * P;
         } else {
-            alpha_pairs(p, S, G, M, P);
+            alpha_cheap(S, fl, M, P, nf, flist);
+            lds_signal(fl + F_C);
+            lds_wait(fl + F_C, W1, p.err);   // the queue is complete
+            alpha_full(S, fl, M, P);
         }
         if (ct == 0) TS(18, (long long)clock64());
 #pragma unroll

@@ -42,8 +42,8 @@ def main():
             L.ch__set_kernel(b.handle, ctypes.c_int32(1))
             row.append(f"v1={time_launches(b):.1f}")
             L.ch__set_kernel(b.handle, ctypes.c_int32(2))
-            for G in (1, 2, 3, 4, 8, 16, 32):
-                for B in (128, 192, 256, 320, 384, 512):
+            for G in ([int(x) for x in os.environ["CH_SWEEP_G"].split(",")] if os.environ.get("CH_SWEEP_G") else (1, 2, 3, 4, 8, 16, 32)):
+                for B in (128, 192, 256, 320, 384, 512, 576, 640, 704, 768):
                     if L.ch__set_geometry(b.handle, ctypes.c_int32(G), ctypes.c_int32(B)) != 0:
                         continue
                     row.append(f"G{G}/B{B}={time_launches(b):.1f}")
