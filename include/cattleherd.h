@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CH_ABI_VERSION 2
+#define CH_ABI_VERSION 3
 
 enum {
     CH_OK = 0,
@@ -88,9 +88,9 @@ typedef struct ch_config {
                                  (config/cattle_positions.yaml, 100 x 16; extended for > 16 cows) */
     int32_t spawn_scenarios;
     int32_t spawn_cows;
-    int32_t physics;          /* CH_PHYS_* (CattleAviary ctor `physics`, CattleAviary.py:21); the variants
-                                 run on the team-per-env step kernel */
-    int32_t _pad;
+    int32_t physics;          /* CH_PHYS_* (CattleAviary ctor `physics`, CattleAviary.py:21) */
+    int32_t eval_metrics;     /* 1 (default) = keep update_evaluation_metrics' per-drone episode distance on
+                                 the device every step (BaseAviary.py:1406-1435), read with ch_get_eval */
 } ch_config;
 
 typedef struct ch_handle ch_handle;
@@ -166,6 +166,12 @@ int ch_metrics_device(ch_handle* h, double* dev_out, int32_t reset_after, void* 
  * ch_get_state report it too.  (The reference's analogue: an exception out of env.step,
  * marl_wrapper.py:87-95.) */
 int ch_sync(ch_handle* h, void* stream);
+
+/* update_evaluation_metrics' per-drone episode distance (sb3_envs/BaseAviary.py:1415-1426, the
+ * `episode_drone_distances` the evaluator logs; both components of the reference's 2-vector are equal):
+ * host double[E][N], zero for drones beyond NUM_DRONES; reset with the episode.  Needs
+ * cfg->eval_metrics (CH_ERR_UNSUPPORTED otherwise).  Synchronises `stream`. */
+int ch_get_eval(ch_handle* h, double* host_out, void* stream);
 
 /* Number of built-in spawn scenarios / cows, and a copy of the table (host double[S][C][2]):
  * config/cattle_positions.yaml, 100 scenarios x 16 cows (BaseAviary.py:88-94). */

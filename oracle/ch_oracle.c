@@ -841,6 +841,7 @@ void och_reset(const och_config* c, och_state* s) {
         for (int k = 0; k < 3; ++k) { s->dv[i][k] = 0; s->dw[i][k] = 0; }
         s->active[i] = (uint8_t)(i < n);
         for (int k = 0; k < 4; ++k) s->last_rpm[i][k] = 0;   /* _housekeeping (565, 581-582) */
+        s->eval_dist[i] = 0;   /* episode_drone_distances = self.pos rows, zeroed by _housekeeping (567, 683-688) */
         for (int k = 0; k < 3; ++k) s->rpy_rates[i][k] = 0;
         if (!c->compat) for (int k = 0; k < 3; ++k) { s->pid_last_rpy[i][k] = 0; s->pid_int_pos[i][k] = 0; s->pid_int_rpy[i][k] = 0; }
     }
@@ -874,7 +875,8 @@ int och_step(const och_config* c, och_state* s, const float* actions, float* obs
     const double dt_ctrl = 1.0 / c->ctrl_freq, dt = 1.0 / c->pyb_freq;
     const int substeps = c->pyb_freq / c->ctrl_freq;
     s->step_counter_A += 1;
-    double rpm[OCH_NMAX][4];
+    double rpm[OCH_NMAX][4], p0[OCH_NMAX][2];
+    for (int k = 0; k < n; ++k) { p0[k][0] = s->dp[k][0]; p0[k][1] = s->dp[k][1]; }
     const double sl = speed_limit();
     for (int k = 0; k < n; ++k) {
         /* _preprocessAction VEL branch: BaseRLAviary.py:185-222 */
@@ -910,6 +912,13 @@ int och_step(const och_config* c, och_state* s, const float* actions, float* obs
         if (ph != PH_DYN)   /* no p.stepSimulation under DYN: the cattle bodies do not move (447-448) */
             for (int j = 0; j < c->m; ++j) { s->cp[j][0] += s->cv[j][0] * dt; s->cp[j][1] += s->cv[j][1] * dt; }
         for (int k = 0; k < n; ++k) memcpy(s->last_rpm[k], rpm[k], sizeof(rpm[k]));   /* 450 */
+    }
+    /* update_evaluation_metrics (BaseAviary.py:1415-1426): |last_drones_pos - pos| * 1.7, last = the
+     * previous read-back, (0, 0) on an episode's first step (reset() zeroes it, BaseAviary.py:317) */
+    for (int k = 0; k < n; ++k) {
+        const double lx = s->step_counter == 0 ? 0.0 : p0[k][0], ly = s->step_counter == 0 ? 0.0 : p0[k][1];
+        const double ex = lx - s->dp[k][0], ey = ly - s->dp[k][1];
+        s->eval_dist[k] += sqrt(ex * ex + ey * ey) * 1.7;
     }
     if (s->step_counter_A % 2 == 0) {
         double cp[2 * OCH_MMAX], cv[2 * OCH_MMAX], nv[2 * OCH_MMAX], dxy[2 * OCH_NMAX];

@@ -48,6 +48,7 @@ typedef struct och_state {
     int64_t env_id;                     /* global env index (Philox key part) */
     double last_rpm[OCH_NMAX][4];       /* last_clipped_action (BaseAviary.py:450, 565): drag input */
     double rpy_rates[OCH_NMAX][3];      /* DYN body rates (BaseAviary.py:581-582, 1075) */
+    double eval_dist[OCH_NMAX];         /* update_evaluation_metrics' episode distance (BaseAviary.py:1415-1426) */
 } och_state;
 
 #ifdef __cplusplus

@@ -48,7 +48,8 @@ class State(ctypes.Structure):
                 ("clock", ctypes.c_double), ("level", ctypes.c_int32), ("tally", ctypes.c_int32),
                 ("spawn_index", ctypes.c_int32), ("active", ctypes.c_uint8 * NMAX),
                 ("episode", ctypes.c_int64), ("env_id", ctypes.c_int64),
-                ("last_rpm", (ctypes.c_double * 4) * NMAX), ("rpy_rates", (ctypes.c_double * 3) * NMAX)]
+                ("last_rpm", (ctypes.c_double * 4) * NMAX), ("rpy_rates", (ctypes.c_double * 3) * NMAX),
+                ("eval_dist", ctypes.c_double * NMAX)]
 
 
 _lib = None
@@ -242,7 +243,8 @@ class Env:
                 "step_counter_A": st.step_counter_A, "prev_cent": st.prev_cent if st.has_prev else np.nan,
                 "has_prev": st.has_prev, "clock": st.clock, "level": st.level, "tally": st.tally,
                 "spawn_index": st.spawn_index, "active": np.array(list(st.active), np.uint8),
-                "episode": st.episode, "last_rpm": a(st.last_rpm, 4), "rpy_rates": a(st.rpy_rates, 3)}
+                "episode": st.episode, "last_rpm": a(st.last_rpm, 4), "rpy_rates": a(st.rpy_rates, 3),
+                "eval_dist": np.array(list(st.eval_dist), np.float64)}
 
 
 def batch_rollout(mode, n, m, spawn_table, E, T, threads=0, seed=0x5EED, compat=True):

@@ -15,14 +15,14 @@ CH_PREC_F64, CH_PREC_F32 = 0, 1
 CH_STEP_AUTORESET, CH_STEP_RANDOM_ACTIONS = 0x1, 0x2
 METRIC_NAMES = ("steps", "episodes", "return_sum", "length_sum", "terminated", "truncated", "nan_rewards",
                 "effectiveness_sum")
-ABI_VERSION = 2
+ABI_VERSION = 3
 # Physics enum (utils/enums.py:13-21, include/cattleherd.h CH_PHYS_*)
 PHYSICS = {"pyb": 0, "dyn": 1, "pyb_gnd": 2, "pyb_drag": 3, "pyb_dw": 4, "pyb_gnd_drag_dw": 5}
 
 # every symbol include/cattleherd.h declares
 EXPORTS = ("ch_default_config", "ch_create", "ch_destroy", "ch_last_error", "ch_shape", "ch_reset", "ch_step",
            "ch_state_size", "ch_get_state", "ch_set_state", "ch_metrics", "ch_metrics_device", "ch_sync",
-           "ch_builtin_spawn_table",
+           "ch_get_eval", "ch_builtin_spawn_table",
            "ch_spawn_table", "ch_mlp_forward", "ch_policy_forward")
 CH_ACT_NONE, CH_ACT_TANH, CH_ACT_RELU = 0, 1, 2
 
@@ -35,7 +35,7 @@ class ChConfig(ctypes.Structure):
                 ("gyro", ctypes.c_int32), ("marl_wrapper", ctypes.c_int32), ("damping", ctypes.c_double), ("seed", ctypes.c_uint64),
                 ("env_id_offset", ctypes.c_int64), ("spawn_table", ctypes.POINTER(ctypes.c_double)),
                 ("spawn_scenarios", ctypes.c_int32), ("spawn_cows", ctypes.c_int32), ("physics", ctypes.c_int32),
-                ("_pad", ctypes.c_int32)]
+                ("eval_metrics", ctypes.c_int32)]
 
 
 class ChStepIO(ctypes.Structure):
@@ -85,6 +85,7 @@ def lib():
     L.ch_metrics.argtypes = [vp, vp, i32, vp]
     L.ch_metrics_device.argtypes = [vp, vp, i32, vp]
     L.ch_sync.argtypes = [vp, vp]
+    L.ch_get_eval.argtypes = [vp, vp, vp]
     L.ch_builtin_spawn_table.argtypes = [vp, P(i32), P(i32)]
     L.ch_spawn_table.argtypes = [i32, vp, P(i32), P(i32)]
     L.ch_mlp_forward.argtypes = [P(ChMlp), vp, i64, vp, vp]

@@ -25,7 +25,7 @@ class HerdBatch:
     def __init__(self, n_envs, num_drones, num_cattle, mode="ctde", device=None, compat=True, precision="f64",
                  min_drones=None, max_drones=None, curriculum_level=None, seed=0x5EED, env_id_offset=0,
                  damping=0.04, torque_world=True, gyro=True, ctrl_freq=60, pyb_freq=240, spawn_table=None,
-                 marl_wrapper=True, physics="pyb"):
+                 marl_wrapper=True, physics="pyb", eval_metrics=True):
         import torch
         if not torch.cuda.is_available():
             raise RuntimeError("HerdBatch needs a ROCm GPU (torch.cuda.is_available() is False); there is no CPU "
@@ -51,6 +51,7 @@ class HerdBatch:
         if hasattr(physics, "value"):
             physics = physics.value
         cfg.physics = L.PHYSICS[physics.lower()] if isinstance(physics, str) else int(physics)
+        cfg.eval_metrics = int(bool(eval_metrics))
         self._table = None
         if spawn_table is not None:
             self._table = np.ascontiguousarray(spawn_table, np.float64)
@@ -176,6 +177,15 @@ class HerdBatch:
         L.check(L.lib().ch_get_state(self.handle, d.ctypes.data, i.ctypes.data, self._stream()), self.handle)
         return d, i
 
+    def env_ints(self):
+        """The per-env integer scalars only (ENV_INTS rows, numpy int32 [E] each): one small copy instead
+        of the whole state (NUM_DRONES, step counters, curriculum level, ...)."""
+        nd, ni = self.state_size()
+        i = np.zeros(ni, np.int32)
+        L.check(L.lib().ch_get_state(self.handle, None, i.ctypes.data, self._stream()), self.handle)
+        iv = i.reshape(len(ENV_INTS), self.n_envs)
+        return {name: iv[k].copy() for k, name in enumerate(ENV_INTS)}
+
     def set_state_raw(self, d, i):
         d = np.ascontiguousarray(d, np.float64)
         i = np.ascontiguousarray(i, np.int32)
@@ -249,6 +259,13 @@ class HerdBatch:
             out = self.torch.empty(len(L.METRIC_NAMES), dtype=self.torch.float64, device=self.device)
         L.check(L.lib().ch_metrics_device(self.handle, ctypes.c_void_p(out.data_ptr()), int(bool(reset)),
                                           self._stream()), self.handle)
+        return out
+
+    def eval_distances(self):
+        """update_evaluation_metrics' per-drone episode distance (BaseAviary.py:1415-1426), numpy
+        float64 [E, num_drones]; the reference's 2-vector holds this value in both components."""
+        out = np.zeros((self.n_envs, self.num_drones), np.float64)
+        L.check(L.lib().ch_get_eval(self.handle, out.ctypes.data, self._stream()), self.handle)
         return out
 
     def sync(self):

@@ -1,11 +1,25 @@
-"""Host-side evaluation logger for single-env evaluation runs (reference: utils/evaluation.py:5-94,
-BaseAviary.update_evaluation_metrics / evaluation_episode_trigger, sb3_envs/BaseAviary.py:1406-1450).
+"""Evaluation logging of the reference (utils/evaluation.py:5-94 ``evaluator``; BaseAviary
+``update_evaluation_metrics`` / ``evaluation_episode_trigger``, sb3_envs/BaseAviary.py:1406-1450) over
+the device batch.
 
-Records per-step drone/cattle poses and velocities, effectiveness and episode time, and writes the
-reference's ``evaluation_data.pkl`` schema.  Two deliberate differences, both documented in
-DESIGN.md: per-step rows are copies (the reference appends aliases of arrays it keeps mutating), and
-recording only happens while ``is_evaluating`` is set by the caller (the reference appends on every
-training step without bound).
+``Evaluator`` keeps the reference's attributes and methods, so ``save_evaluation_data`` writes the same
+``evaluation_data.pkl`` schema.  ``EvalTracker`` is the env-side half of BaseAviary: the per-episode list
+``episode_drone_distances`` and the two call sites.  The per-drone distance itself is accumulated on the
+device by the step kernel every step (ch_config.eval_metrics, ``HerdBatch.eval_distances``), so only
+logging needs host data.
+
+The reference's data flow is reproduced as it is, because it is what its pickle holds:
+* the distance "2-vector" of a drone starts at (0, 0) -- ``_housekeeping`` zeroes ``self.pos`` before it
+  copies it (BaseAviary.py:567, 683-688) -- and both components receive the same additions;
+* every logged distance row is the env's list object itself, mutated in place afterwards, so all rows of
+  an episode show its final distances (and an episode's first row is the previous episode's list, see
+  below);
+* ``evaluation_episode_trigger`` fires from ``_computeTruncated`` at the time limit, which ``step`` runs
+  twice -- inside ``_computeReward`` and after it (CattleAviary.py:314-315, BaseAviary.py:458-460) -- both
+  before ``update_evaluation_metrics`` (462): two episode entries per time-out, the second empty, and the
+  time-out step itself logged into the next episode's rows.
+One deliberate difference: rows are appended only while ``is_evaluating`` is set (the reference appends
+on every training step, without bound); distances are accumulated on every step regardless.
 """
 import os
 import pickle
@@ -31,71 +45,105 @@ def herding_effectiveness(cattle_xy, drone_xy):
 
 
 class Evaluator:
+    """utils/evaluation.py:5-94 (``evaluator``): episode-level and per-step lists."""
+
     def __init__(self):
-        self.active = True
-        for k in ("total_drone_distances", "total_time_taken", "total_effectiveness", "total_number_of_drones",
-                  "drone_distances_per_step", "effectiveness_per_step", "time_per_step", "drone_poses_per_step",
-                  "cattle_poses_per_step", "drone_vel_per_step", "cattle_vel_per_step"):
-            setattr(self, k, [])
+        self.total_drone_distances = []
+        self.total_time_taken = []
+        self.total_effectiveness = []
+        self.total_number_of_drones = []
+        self.drone_distances_per_step = []
+        self.effectiveness_per_step = []
+        self.time_per_step = []
+        self.drone_poses_per_step = []
+        self.cattle_poses_per_step = []
+        self.drone_vel_per_step = []
+        self.cattle_vel_per_step = []
         self._clear_current()
-        self._last_pos = None
-        self._dist = None
-        self._prev_cattle_vel = None
 
     def _clear_current(self):
-        self.curr = {k: [] for k in ("drone_poses", "cattle_poses", "drone_vel", "cattle_vel", "drone_distances",
-                                     "effectiveness", "time")}
+        self.curr_drone_poses, self.curr_cattle_poses, self.curr_drone_vel, self.curr_cattle_vel = [], [], [], []
+        self.curr_drone_distances, self.curr_effectiveness, self.curr_time = [], [], []
 
-    def start_episode(self, s, n):
-        # _housekeeping initialises the distance accumulators to the start positions and reset()
-        # zeroes last_drones_pos (BaseAviary.py:317, 683-688)
-        self._dist = [np.array(s["drone_pos"][0, i, :2], np.float64) for i in range(n)]
-        self._last_pos = [np.zeros(2) for _ in range(n)]
-        self._prev_cattle_vel = np.array(s["cow_vel"][0], np.float64)
+    def append_timestep_data(self, drone_distances, timestep_time, effectiveness, drone_poses, cattle_poses, drone_vel,
+                             cattle_vel):
+        self.curr_drone_distances.append(drone_distances)
+        self.curr_time.append(timestep_time)
+        self.curr_effectiveness.append(effectiveness)
+        self.curr_drone_poses.append(drone_poses)
+        self.curr_cattle_poses.append(cattle_poses)
+        self.curr_drone_vel.append(drone_vel)
+        self.curr_cattle_vel.append(cattle_vel)
 
-    def record_step(self, s, n, m, ctrl_freq, counter_inc=4):
-        if self._dist is None:
-            self.start_episode(s, n)
-        dp = np.array(s["drone_pos"][0, :n, :2], np.float64)
-        for i in range(n):
-            self._dist[i] = self._dist[i] + np.linalg.norm(self._last_pos[i] - dp[i]) * 1.7
-            self._last_pos[i] = dp[i].copy()
-        cp = np.array(s["cow_pos"][0, :m], np.float64)
-        # update_evaluation_metrics runs before the step counter advances (BaseAviary.py:462-464)
-        t = (int(s["step_counter"][0]) - counter_inc) / ctrl_freq
-        row = {"drone_poses": dp, "cattle_poses": cp, "drone_vel": np.array(s["drone_vel"][0, :n, :2]),
-               "cattle_vel": self._prev_cattle_vel[:m].copy(), "drone_distances": [d.copy() for d in self._dist],
-               "effectiveness": herding_effectiveness(cp, dp), "time": t}
-        self._prev_cattle_vel = np.array(s["cow_vel"][0], np.float64)
-        for k, v in row.items():
-            self.curr[k].append(v)
+    def append_episode_data(self, drone_distances, num_drones, time, effectiveness):
+        self.total_drone_distances.append(drone_distances)
+        self.total_number_of_drones.append(num_drones)
+        self.total_time_taken.append(time)
+        self.total_effectiveness.append(effectiveness)
+        self.drone_poses_per_step.append(self.curr_drone_poses)
+        self.cattle_poses_per_step.append(self.curr_cattle_poses)
+        self.drone_vel_per_step.append(self.curr_drone_vel)
+        self.cattle_vel_per_step.append(self.curr_cattle_vel)
+        self.drone_distances_per_step.append(self.curr_drone_distances)
+        self.time_per_step.append(self.curr_time)
+        self.effectiveness_per_step.append(self.curr_effectiveness)
+        self._clear_current()
 
-    def end_episode(self, n, ep_time):
-        """evaluation_episode_trigger fires once per _computeTruncated call — twice per step
-        (CattleAviary.py:315 and BaseAviary.py:460) — hence an empty second episode, as in the
-        reference's own evaluation_data.pkl."""
-        for _ in range(2):
-            eff = self.curr["effectiveness"][-1] if self.curr["effectiveness"] else 0
-            self.total_drone_distances.append([d.copy() for d in (self._dist or [])])
-            self.total_number_of_drones.append(n)
-            self.total_time_taken.append(ep_time)
-            self.total_effectiveness.append(eff)
-            self.drone_poses_per_step.append(self.curr["drone_poses"])
-            self.cattle_poses_per_step.append(self.curr["cattle_poses"])
-            self.drone_vel_per_step.append(self.curr["drone_vel"])
-            self.cattle_vel_per_step.append(self.curr["cattle_vel"])
-            self.drone_distances_per_step.append(self.curr["drone_distances"])
-            self.time_per_step.append(self.curr["time"])
-            self.effectiveness_per_step.append(self.curr["effectiveness"])
-            self._clear_current()
-
-    def save_evaluation_data(self, save_path="evaluation_data.pkl"):
-        data = {"distances": self.total_drone_distances, "num_drones": self.total_number_of_drones,
+    def evaluation_data(self):
+        """The dict save_evaluation_data pickles (evaluation.py:73-90)."""
+        return {"distances": self.total_drone_distances, "num_drones": self.total_number_of_drones,
                 "time_taken": self.total_time_taken, "effectiveness": self.total_effectiveness,
                 "distances_per_step": self.drone_distances_per_step, "time_per_step": self.time_per_step,
                 "effectiveness_per_step": self.effectiveness_per_step,
                 "drone_poses_per_step": self.drone_poses_per_step, "cattle_poses_per_step": self.cattle_poses_per_step,
                 "drone_vel_per_step": self.drone_vel_per_step, "cattle_vel_per_step": self.cattle_vel_per_step}
+
+    def save_evaluation_data(self, save_path="evaluation_data.pkl"):
         with open(save_path, "wb") as f:
-            pickle.dump(data, f)
+            pickle.dump(self.evaluation_data(), f)
         print(f"Evaluation data saved to {os.path.abspath(save_path)}")
+
+
+class EvalTracker:
+    """BaseAviary's side of the logging for env ``e`` of a batch: ``episode_drone_distances`` (one list per
+    episode, its arrays updated in place from the device accumulator) and the two call sites."""
+
+    def __init__(self, evaluator, env_index=0):
+        self.evaluator = evaluator
+        self.e = env_index
+        self.episode_drone_distances = []
+        self._prev_cattle_vel = None
+
+    def on_reset(self, state, n):
+        """_housekeeping (BaseAviary.py:683-688): a new list, every entry (0, 0)."""
+        self.episode_drone_distances = [np.zeros(2) for _ in range(n)]
+        self._prev_cattle_vel = np.array(state["cow_vel"][self.e], np.float64)
+
+    def set_step_start(self, state):
+        """The cattle velocities at the start of a step: what the read-back of that step returns (the
+        flock update of the step only reaches Bullet afterwards, BaseAviary.py:452-455, 1398-1400)."""
+        self._prev_cattle_vel = np.array(state["cow_vel"][self.e], np.float64)
+
+    def _sync_distances(self, dist_row):
+        for i, d in enumerate(self.episode_drone_distances):
+            d[:] = dist_row[i]   # in place: rows logged earlier in the episode see it (the reference's aliasing)
+
+    def _poses(self, state, n, m):
+        e = self.e
+        return (np.array(state["drone_pos"][e, :n, :2], np.float64), np.array(state["cow_pos"][e, :m], np.float64))
+
+    def after_step(self, state, dist_row, n, m, step_counter_before, ctrl_freq, episode_len_sec):
+        """One env.step's logging, in the reference's order: the time-out triggers of the two
+        _computeTruncated calls (CattleAviary.py:545-548), then update_evaluation_metrics (BaseAviary.py:462)."""
+        self._sync_distances(dist_row)
+        drone_poses, cattle_poses = self._poses(state, n, m)
+        ep_time = step_counter_before / ctrl_freq
+        eff = herding_effectiveness(cattle_poses, drone_poses)
+        if ep_time > episode_len_sec:
+            for _ in range(2):   # evaluation_episode_trigger (BaseAviary.py:1439-1450)
+                self.evaluator.append_episode_data(self.episode_drone_distances, n, ep_time, eff)
+        drone_vel = np.array(state["drone_vel"][self.e, :n, :2], np.float64)
+        cattle_vel = self._prev_cattle_vel[:m].copy() if self._prev_cattle_vel is not None else np.zeros((m, 2))
+        self.evaluator.append_timestep_data(self.episode_drone_distances, ep_time, eff, drone_poses, cattle_poses,
+                                            drone_vel, cattle_vel)
+        self.set_step_start(state)

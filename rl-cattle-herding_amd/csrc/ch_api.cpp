@@ -53,6 +53,7 @@ struct ch_handle {
     size_t lds = 0;
     uint16_t* pairs = nullptr;
     int* errw = nullptr;        // device error word (CH_DEVERR_* bits), sticky
+    double* evald = nullptr;    // [E][NC] evaluation distances (cfg.eval_metrics)
     double* mdev = nullptr;     // device [CH_METRIC_COUNT + 1]: reduced metrics + error word
     double* mhost = nullptr;    // pinned host copy of mdev
     std::string err;
@@ -163,6 +164,7 @@ static StepParams<R> params(ch_handle* h) {
     p.tstamp = h->tstamp;
     p.physics = c.physics; p.gnd_h_clip = gnd_eff_h_clip(); p.phys = (R*)h->phys;
     p.err = h->errw;
+    p.evald = h->evald;
     return p;
 }
 
@@ -213,6 +215,7 @@ int ch_default_config(ch_config* c, int32_t mode, int32_t num_drones, int32_t nu
     c->env_id_offset = 0;
     c->spawn_table = nullptr;
     c->physics = CH_PHYS_PYB;
+    c->eval_metrics = 1;
     return CH_OK;
 }
 
@@ -220,7 +223,7 @@ const char* ch_last_error(const ch_handle* h) { return h ? h->err.c_str() : g_cr
 
 static void free_all(ch_handle* h) {
     void* ptrs[] = {h->drone, h->rpy, h->cattle, h->phys, h->envr, h->envi, h->metrics, h->spawn, h->pairs,
-                    h->errw, h->mdev, h->ctl};
+                    h->errw, h->mdev, h->ctl, h->evald};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (h->mhost) (void)hipHostFree(h->mhost);
@@ -315,6 +318,10 @@ int ch_create(const ch_config* c, int64_t n_envs, int32_t device, ch_handle** ou
         const int ctl0[4] = {1, 1, 0, 0};   // no Euler cache yet; obs bytes unknown
         CTRY(hipMalloc(&h->ctl, sizeof(ctl0)));
         CTRY(hipMemcpy(h->ctl, ctl0, sizeof(ctl0), hipMemcpyHostToDevice));
+    }
+    if (c->eval_metrics) {
+        CTRY(hipMalloc(&h->evald, sizeof(double) * E * h->NC));
+        CTRY(hipMemset(h->evald, 0, sizeof(double) * E * h->NC));
     }
     CTRY(hipMalloc(&h->errw, sizeof(int)));
     CTRY(hipMemset(h->errw, 0, sizeof(int)));
@@ -689,6 +696,15 @@ int ch_metrics_device(ch_handle* h, double* dev_out, int32_t reset_after, void* 
     if (!h || !dev_out) return fail(h, CH_ERR_INVALID, "ch_metrics_device: NULL argument");
     HIP_TRY(h, hipSetDevice(h->device));
     HIP_TRY(h, launch_metrics_reduce(h->metrics, h->E, dev_out, nullptr, nullptr, reset_after, (hipStream_t)stream));
+    return CH_OK;
+}
+
+int ch_get_eval(ch_handle* h, double* host_out, void* stream) {
+    if (!h || !host_out) return fail(h, CH_ERR_INVALID, "ch_get_eval: NULL argument");
+    if (!h->evald) return fail(h, CH_ERR_UNSUPPORTED, "ch_get_eval: the handle was created with eval_metrics = 0");
+    HIP_TRY(h, hipSetDevice(h->device));
+    HIP_TRY(h, hipStreamSynchronize((hipStream_t)stream));
+    HIP_TRY(h, hipMemcpy(host_out, h->evald, sizeof(double) * h->E * h->NC, hipMemcpyDeviceToHost));
     return CH_OK;
 }
 

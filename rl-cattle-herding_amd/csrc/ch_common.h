@@ -95,6 +95,7 @@ __device__ __forceinline__ void reset_drone(const StepParams<R>& p, long long di
         z = R(kTargetAlt);
     }
     R* D = p.drone;
+    if (p.evald) p.evald[di] = 0;   // episode_drone_distances: (0, 0) -- _housekeeping zeroes self.pos (BaseAviary.py:567, 683-688)
     D[0 * DS + di] = x; D[1 * DS + di] = y; D[2 * DS + di] = z;
     D[3 * DS + di] = 0; D[4 * DS + di] = 0; D[5 * DS + di] = 0; D[6 * DS + di] = 1;
 #pragma unroll
@@ -128,6 +129,17 @@ __device__ __forceinline__ void reset_cow(const StepParams<R>& p, long long ci, 
     reset_cow_at(p, ci, env_id, j, R(tab[0]), R(tab[1]), episode, x, y, vx, vy);
 }
 
+
+// update_evaluation_metrics' per-drone distance (BaseAviary.py:1415-1426; rllib twin): |last - current| * 1.7
+// added to the episode's accumulator, last = the previous step's read-back position, or (0, 0) on an
+// episode's first step (reset() zeroes last_drones_pos, BaseAviary.py:317).  Both components of the
+// reference's 2-vector accumulator start at 0 and receive the same additions, so one number is kept.
+template <class R>
+__device__ __forceinline__ double eval_distance_step(double acc, bool first, R x0, R y0, R x1, R y1) {
+    const R lx = first ? R(0) : x0, ly = first ? R(0) : y0;
+    const R ex = lx - x1, ey = ly - y1;
+    return acc + (double)(sqrt(ex * ex + ey * ey) * R(1.7));
+}
 
 // end-of-episode bonus of MARLCattleAviary._endOfEpisodeReward (MARLCattleAviary.py:183-241)
 template <class R>

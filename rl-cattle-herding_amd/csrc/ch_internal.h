@@ -60,6 +60,7 @@ struct StepParams {
     R* phys;                  // [kPhysComps][E][NC]
     int* err;                 // device error word of the handle (CH_DEVERR_* bits), read by ch_sync & co.
     int pw;                   // v2: per-wave env tables (V2Layout W = block / 64 - 1)
+    double* evald;            // optional [E][NC]: update_evaluation_metrics' per-drone episode distance
 };
 
 // device error word bits (ch_api.cpp reports them as CH_ERR_DEVICE)

@@ -164,6 +164,7 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
         if (valid && t < n) {
             const long long di = (long long)e * p.NC + t;
             R pos[3] = {ld(p.drone, 0, DS, di), ld(p.drone, 1, DS, di), ld(p.drone, 2, DS, di)};
+            const R px0 = pos[0], py0 = pos[1];
             R q[4] = {ld(p.drone, 3, DS, di), ld(p.drone, 4, DS, di), ld(p.drone, 5, DS, di), ld(p.drone, 6, DS, di)};
             R v[3] = {ld(p.drone, 7, DS, di), ld(p.drone, 8, DS, di), ld(p.drone, 9, DS, di)};
             R w[3] = {ld(p.drone, 10, DS, di), ld(p.drone, 11, DS, di), ld(p.drone, 12, DS, di)};
@@ -207,6 +208,7 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
                 }
             }
             R* D = p.drone;
+            if (p.evald) p.evald[di] = eval_distance_step(p.evald[di], sc == 0, px0, py0, pos[0], pos[1]);
             D[0 * DS + di] = pos[0]; D[1 * DS + di] = pos[1]; D[2 * DS + di] = pos[2];
             D[3 * DS + di] = q[0]; D[4 * DS + di] = q[1]; D[5 * DS + di] = q[2]; D[6 * DS + di] = q[3];
             D[7 * DS + di] = v[0]; D[8 * DS + di] = v[1]; D[9 * DS + di] = v[2];

@@ -515,6 +515,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
     R pos[3], q[4], v[3], w[3], pid[9], rpy_in[3] = {0, 0, 0};
     R ph_lr[4] = {0, 0, 0, 0}, ph_rr[3] = {0, 0, 0};   // PHYS: last_clipped_action, DYN rpy_rates
     int stepi = 0, n0 = 0, act0 = 0;
+    double ev_acc = 0;   // update_evaluation_metrics' distance of this drone (optional)
     R spx_r[3] = {0, 0, 0}, spy_r[3] = {0, 0, 0};   // cow waves: prefetched spawn positions
     bool rpy_valid = false;
     if (tid < 64) {
@@ -537,6 +538,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
 #pragma unroll
             for (int c = 0; c < 3; ++c) rpy_in[c] = p.rpy[c * DS + di];
             stepi = p.envi[9 * E + e0 + dg];   // ch_step calls on this env so far: the Philox action counter
+            if (p.evald) ev_acc = p.evald[di];
             if constexpr (PHYS) {
 #pragma unroll
                 for (int c = 0; c < 4; ++c) ph_lr[c] = p.phys[c * DS + di];
@@ -612,7 +614,9 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         const int n = dlane ? n0 : 0;
         const bool live = dlane && dk < n;
         R rpy_out[3] = {0, 0, 0};
+        R px0 = 0, py0 = 0;
         if (live) {
+            px0 = pos[0]; py0 = pos[1];
             const int e = e0 + dg;
             float a[4];
             if (p.flags & CH_STEP_RANDOM_ACTIONS) {
@@ -666,6 +670,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         if (live && wobs) obs_own(obs_wg + dg * RW, dk, pos[2], rpy_out, v, w);
         if (tid == 0) TS(4, (long long)clock64());
         lds_wait(fl + F_E, W1, p.err);   // env scalars and the curriculum table (staged by the cow waves)
+        if (p.evald && live) p.evald[di] = eval_distance_step(ev_acc, ei[I_SC * G + dg] == 0, px0, py0, pos[0], pos[1]);
 
         // per-drone reward terms (CattleAviary.py:230-246, 572-679) and neighbour obs (BaseRLAviary.py:303-317)
         if (live && task) {

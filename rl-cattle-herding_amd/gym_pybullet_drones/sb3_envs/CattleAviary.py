@@ -10,7 +10,7 @@ Gymnasium / SB3 ``DummyVecEnv`` / ``evaluate_policy`` use; for throughput use th
 """
 import numpy as np
 
-from cattleherd.evaluation import Evaluator
+from cattleherd.evaluation import EvalTracker, Evaluator
 from cattleherd.env import HerdBatch
 from cattleherd.spaces import (ActionType, DroneModel, ObservationType, Physics, check_supported,
                                ctde_action_space, ctde_observation_space)
@@ -50,7 +50,6 @@ class CattleAviary(_EnvBase):
         self.NUM_CATTLE = num_cattle
         self.DRONE_TARGET_ALTITUDE = 0.45
         self.GUI, self.RECORD = bool(gui), bool(record)
-        self.is_evaluating = False
         self.batch = HerdBatch(1, num_drones, num_cattle, mode="ctde", device=device, compat=compat,
                                precision=precision, min_drones=self.MIN_NUM_DRONES, max_drones=self.MAX_NUM_DRONES,
                                curriculum_level=curriculum_level, seed=seed, env_id_offset=env_id,
@@ -60,28 +59,45 @@ class CattleAviary(_EnvBase):
         self.action_space = ctde_action_space(num_drones)
         self.observation_space = ctde_observation_space()
         self.eval_system = Evaluator()
+        self._tracker = EvalTracker(self.eval_system)
+        self._is_evaluating = False
         self._needs_reset = True
 
+    @property
+    def is_evaluating(self):
+        return self._is_evaluating
+
+    @is_evaluating.setter
+    def is_evaluating(self, on):
+        """Logging starts with the next step; the cattle velocities it logs are this step's read-back."""
+        self._is_evaluating = bool(on)
+        if self._is_evaluating and not self._needs_reset:
+            self._tracker.set_step_start(self.batch.get_state())
+
     # ------------------------------------------------------------------------------------------
-    def _sync_counts(self):
-        s = self.batch.get_state()
-        self.NUM_DRONES = int(s["n"][0])
-        self.step_counter = int(s["step_counter"][0])
-        self.step_counter_A = int(s["step_counter_A"][0])
-        return s
+    def _sync_counts(self, ints=None):
+        ints = self.batch.env_ints() if ints is None else ints
+        self.NUM_DRONES = int(ints["n"][0])
+        self.step_counter = int(ints["step_counter"][0])
+        self.step_counter_A = int(ints["step_counter_A"][0])
+        return ints
 
     def reset(self, seed: int = None, options: dict = None):
         """BaseAviary.reset (sb3_envs/BaseAviary.py:280-331); ``seed`` is ignored like the reference's."""
         obs = self.batch.reset()
-        s = self._sync_counts()
-        self.eval_system.start_episode(s, self.NUM_DRONES)
+        s = self.batch.get_state()
+        self._sync_counts(s)
+        self._tracker.on_reset(s, self.NUM_DRONES)
         self._needs_reset = False
         return obs[0].cpu().numpy(), {"answer": 42}
 
     def step(self, action):
-        """BaseAviary.step (sb3_envs/BaseAviary.py:335-465) for this env; no auto-reset (Gymnasium)."""
+        """BaseAviary.step (sb3_envs/BaseAviary.py:335-465) for this env; no auto-reset (Gymnasium).
+        While ``is_evaluating``: the reference's logging (update_evaluation_metrics, and the time-out
+        evaluation_episode_trigger of _computeTruncated), see cattleherd.evaluation."""
         if self._needs_reset:
             self.reset()
+        sc_before, n = self.step_counter, self.NUM_DRONES
         a = np.zeros((1, self._num_drones_ctor, 4), np.float32)
         act = np.asarray(action, np.float32).reshape(-1, 4)
         k = min(len(act), self._num_drones_ctor)
@@ -91,11 +107,13 @@ class CattleAviary(_EnvBase):
         obs_np = obs[0].cpu().numpy()
         reward = float(rew[0, 0].item())
         terminated, truncated = bool(te[0, 0].item()), bool(tr[0, 0].item())
-        s = self._sync_counts()
-        if self.is_evaluating:
-            self.eval_system.record_step(s, self.NUM_DRONES, self.NUM_CATTLE, self.CTRL_FREQ, self.PYB_STEPS_PER_CTRL)
-        if truncated and self.is_evaluating and s["step_counter"][0] / self.CTRL_FREQ > self.EPISODE_LEN_SEC:
-            self.eval_system.end_episode(self.NUM_DRONES, s["step_counter"][0] / self.CTRL_FREQ)
+        if self._is_evaluating:
+            s = self.batch.get_state()
+            self._tracker.after_step(s, self.batch.eval_distances()[0], n, self.NUM_CATTLE, sc_before, self.CTRL_FREQ,
+                                     self.EPISODE_LEN_SEC)
+            self._sync_counts(s)
+        else:
+            self._sync_counts()
         return obs_np, reward, terminated, truncated, {"answer": 42}
 
     def evaluation_save(self, save_path="evaluation_data.pkl"):

@@ -76,6 +76,16 @@ class FakeBatch:
         for e, env in enumerate(self.envs):
             env.set_state({k: np.asarray(v)[e] for k, v in s.items()})
 
+    def env_ints(self):
+        s = stack([env.get_state() for env in self.envs])
+        return {k: np.asarray(s[k], np.int64) for k in ("n", "step_counter", "step_counter_A")}
+
+    def eval_distances(self):
+        return np.stack([env.get_state()["eval_dist"][:self.num_drones] for env in self.envs])
+
+    def invalidate_obs(self):
+        pass
+
     def metrics(self, reset=False):
         return np.zeros(8)
 

@@ -441,6 +441,55 @@ def gen_ctde_rollout(rng, n, m, steps, level=7, tag=None, hover=False):
     print(name, steps, "steps; resets at", rec["reset_at"][:6], "nan rewards", int(np.isnan(out["reward"]).sum()))
 
 
+def gen_eval(rng, n=3, m=4, level=2, steps=1300):
+    """The evaluation logger with ``is_evaluating = True``: BaseAviary.update_evaluation_metrics
+    (sb3_envs/BaseAviary.py:1406-1435) every step, evaluation_episode_trigger (1439-1450) from
+    _computeTruncated at the time limit (CattleAviary.py:545-548, twice per step), reset between
+    episodes, and the evaluator's lists exactly as save_evaluation_data (utils/evaluation.py:73-94)
+    would pickle them -- aliasing included: the distance rows reference the env's list of arrays,
+    which update_evaluation_metrics mutates in place.  Level 2 (40 s, terminates only on approach)
+    with hover actions runs two full episodes into the time limit."""
+    env = make_ctde(n, m, level=level)
+    env.is_evaluating = True
+    with quiet():
+        env.reset()
+    rec = {"state": [], "action": [], "reset_at": [], "reset_state": []}
+    for t in range(steps):
+        a = (rng.uniform(-1, 1, (n, 4)) * 0.15).astype(np.float32)
+        rec["state"].append(capture(env))
+        with quiet():
+            _, _, te, tr, _ = env.step(a)
+        rec["action"].append(a)
+        if te or tr:
+            with quiet():
+                env.reset()
+            rec["reset_at"].append(t)
+            rec["reset_state"].append(capture(env))
+    ev = env.eval_system
+    out = {"action": np.array(rec["action"]), "reset_at": np.array(rec["reset_at"], np.int64),
+           "level": np.int64(level)}
+    out.update({"state_" + k: v for k, v in stack_states(rec["state"]).items()})
+    out.update({"reset_" + k: v for k, v in stack_states(rec["reset_state"]).items()})
+    # episode level
+    out["ev_distances"] = np.array([np.array([np.asarray(d, np.float64) for d in ep]) for ep in ev.total_drone_distances])
+    out["ev_num_drones"] = np.array(ev.total_number_of_drones, np.int64)
+    out["ev_time_taken"] = np.array(ev.total_time_taken, np.float64)
+    out["ev_effectiveness"] = np.array(ev.total_effectiveness, np.float64)
+    # step level, concatenated over episodes with their lengths
+    lens = [len(x) for x in ev.time_per_step]
+    out["ev_steps_per_episode"] = np.array(lens, np.int64)
+    cat = lambda lists: [row for ep in lists for row in ep]  # noqa: E731
+    out["ev_time_per_step"] = np.array(cat(ev.time_per_step), np.float64)
+    out["ev_effectiveness_per_step"] = np.array(cat(ev.effectiveness_per_step), np.float64)
+    out["ev_distances_per_step"] = np.array([np.array([np.asarray(d, np.float64) for d in row])
+                                             for row in cat(ev.drone_distances_per_step)])
+    for key, src in (("drone_poses", ev.drone_poses_per_step), ("cattle_poses", ev.cattle_poses_per_step),
+                     ("drone_vel", ev.drone_vel_per_step), ("cattle_vel", ev.cattle_vel_per_step)):
+        out[f"ev_{key}_per_step"] = np.array(cat(src), np.float64)
+    np.savez_compressed(os.path.join(HERE, "eval_ctde.npz"), **out)
+    print("eval_ctde", steps, "steps; resets at", rec["reset_at"], "episodes", len(lens), "lengths", lens)
+
+
 PHYSICS_IDS = {"pyb": 0, "dyn": 1, "pyb_gnd": 2, "pyb_drag": 3, "pyb_dw": 4, "pyb_gnd_drag_dw": 5}
 
 
@@ -587,6 +636,11 @@ def main():
 if __name__ == "__main__":
     if "--physics" in sys.argv:   # the physics-variant fixtures only (own seeds)
         gen_physics()
+    elif "--eval" in sys.argv:   # eval_ctde.npz only, own seed
+        np.random.seed(12345)
+        import random
+        random.seed(12345)
+        gen_eval(np.random.default_rng(20261017))
     elif "--task-marl" in sys.argv:   # task_marl.npz only, own seed (regenerated for the step_counter order)
         np.random.seed(12345)
         gen_task_marl(np.random.default_rng(20261016))

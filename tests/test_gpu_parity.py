@@ -236,6 +236,8 @@ def test_random_rollout_with_autoreset_vs_oracle(physics, mode, n, m):
     for k in ("drone_pos", "drone_quat", "drone_vel") + (("last_rpm", "rpy_rates") if ph else ()):
         assert close(st[k][:, :n], want[k][:, :n], 1e-9, 1e-9)[0], k
     assert close(st["cow_pos"], want["cow_pos"][:, :m], 1e-12, 1e-13)[0]
+    # update_evaluation_metrics' per-drone distance, accumulated on the device every step (BaseAviary.py:1415-1426)
+    assert close(b.eval_distances(), np.stack([env.get_state()["eval_dist"][:n] for env in envs]), 1e-9, 1e-12)[0]
     b.close()
 
 
@@ -357,6 +359,7 @@ def test_step_kernels_v1_v2_bit_identical(mode, n, m, E, geom):
     for k in s1:
         assert np.array_equal(np.nan_to_num(s1[k]), np.nan_to_num(s2[k])), k
     assert np.array_equal(hs[0].metrics(), hs[1].metrics(), equal_nan=True)
+    assert np.array_equal(hs[0].eval_distances(), hs[1].eval_distances())
     for h in hs:
         h.close()
 
