@@ -116,6 +116,14 @@ int ch_shape(const ch_handle* h, int64_t* n_envs, int32_t* obs_rows, int32_t* ob
  * observation into obs (device, [E][R][86]); other envs' obs rows are left untouched. */
 int ch_reset(ch_handle* h, const uint8_t* mask_dev, float* obs_dev, void* stream);
 
+/* ch_reset with the reset's random draws supplied by the caller instead of the device's Philox stream:
+ * num_drones host int32[E] (NUM_DRONES of each reset env, BaseAviary.py:307) and/or cow_vel host
+ * double[E][M][2] (the cattle spawn velocities 0.2 (cos a, sin a), BaseAviary.py:631-632); either may be
+ * NULL.  With cattleherd/seeded.py replaying the reference's own seeded `random` / NumPy draws this
+ * reproduces the reference's reset state bit for bit.  Synchronises `stream`. */
+int ch_reset_with(ch_handle* h, const uint8_t* mask_dev, const int32_t* num_drones, const double* cow_vel,
+                  float* obs_dev, void* stream);
+
 typedef struct ch_step_io {
     const float* actions;      /* device [E][N][4]; ignored with CH_STEP_RANDOM_ACTIONS */
     float* actions_out;        /* optional: where device-drawn random actions are stored */

@@ -20,7 +20,8 @@ ABI_VERSION = 3
 PHYSICS = {"pyb": 0, "dyn": 1, "pyb_gnd": 2, "pyb_drag": 3, "pyb_dw": 4, "pyb_gnd_drag_dw": 5}
 
 # every symbol include/cattleherd.h declares
-EXPORTS = ("ch_default_config", "ch_create", "ch_destroy", "ch_last_error", "ch_shape", "ch_reset", "ch_step",
+EXPORTS = ("ch_default_config", "ch_create", "ch_destroy", "ch_last_error", "ch_shape", "ch_reset", "ch_reset_with",
+           "ch_step",
            "ch_state_size", "ch_get_state", "ch_set_state", "ch_metrics", "ch_metrics_device", "ch_sync",
            "ch_get_eval", "ch_builtin_spawn_table",
            "ch_spawn_table", "ch_mlp_forward", "ch_policy_forward")
@@ -78,6 +79,7 @@ def lib():
     L.ch_last_error.restype = ctypes.c_char_p
     L.ch_shape.argtypes = [vp, P(i64), P(i32), P(i32), P(i32)]
     L.ch_reset.argtypes = [vp, vp, vp, vp]
+    L.ch_reset_with.argtypes = [vp, vp, vp, vp, vp, vp]
     L.ch_step.argtypes = [vp, P(ChStepIO), vp]
     L.ch_state_size.argtypes = [vp, P(i64), P(i64)]
     L.ch_get_state.argtypes = [vp, vp, vp, vp]

@@ -98,13 +98,26 @@ class HerdBatch:
             return ctypes.c_void_p(self._raw_stream(self._dev_index))
         return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
 
-    def reset(self, mask=None):
-        """BaseAviary.reset for the envs selected by ``mask`` (bool/uint8 [E] device tensor; None = all)."""
+    def reset(self, mask=None, num_drones=None, cow_vel=None):
+        """BaseAviary.reset for the envs selected by ``mask`` (bool/uint8 [E] device tensor; None = all).
+
+        ``num_drones`` (int [E]) and ``cow_vel`` (float64 [E, num_cattle, 2]) replace the device's Philox
+        draws of those resets -- e.g. cattleherd.seeded.ReferenceResetRNG's replay of the reference's own
+        seeded draws (ch_reset_with)."""
         m = None
         if mask is not None:
             mask = mask.to(device=self.device, dtype=self.torch.uint8).contiguous()
             m = ctypes.c_void_p(mask.data_ptr())
-        L.check(L.lib().ch_reset(self.handle, m, ctypes.c_void_p(self.obs.data_ptr()), self._stream()), self.handle)
+        obs = ctypes.c_void_p(self.obs.data_ptr())
+        if num_drones is None and cow_vel is None:
+            L.check(L.lib().ch_reset(self.handle, m, obs, self._stream()), self.handle)
+            return self.obs
+        nd = None if num_drones is None else np.ascontiguousarray(np.broadcast_to(num_drones, (self.n_envs,)), np.int32)
+        cv = None
+        if cow_vel is not None:
+            cv = np.ascontiguousarray(np.broadcast_to(cow_vel, (self.n_envs, self.num_cattle, 2)), np.float64)
+        L.check(L.lib().ch_reset_with(self.handle, m, None if nd is None else nd.ctypes.data,
+                                      None if cv is None else cv.ctypes.data, obs, self._stream()), self.handle)
         return self.obs
 
     def step(self, actions=None, autoreset=True, random_actions=False, terminal_obs=True, step_io=None):

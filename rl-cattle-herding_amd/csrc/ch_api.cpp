@@ -54,6 +54,8 @@ struct ch_handle {
     uint16_t* pairs = nullptr;
     int* errw = nullptr;        // device error word (CH_DEVERR_* bits), sticky
     double* evald = nullptr;    // [E][NC] evaluation distances (cfg.eval_metrics)
+    int* rdn = nullptr;         // ch_reset_with: device copies of the injected draws
+    double* rdv = nullptr;
     double* mdev = nullptr;     // device [CH_METRIC_COUNT + 1]: reduced metrics + error word
     double* mhost = nullptr;    // pinned host copy of mdev
     std::string err;
@@ -223,7 +225,7 @@ const char* ch_last_error(const ch_handle* h) { return h ? h->err.c_str() : g_cr
 
 static void free_all(ch_handle* h) {
     void* ptrs[] = {h->drone, h->rpy, h->cattle, h->phys, h->envr, h->envi, h->metrics, h->spawn, h->pairs,
-                    h->errw, h->mdev, h->ctl, h->evald};
+                    h->errw, h->mdev, h->ctl, h->evald, h->rdn, h->rdv};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (h->mhost) (void)hipHostFree(h->mhost);
@@ -461,6 +463,45 @@ int ch_reset(ch_handle* h, const uint8_t* mask_dev, float* obs_dev, void* stream
     if (e != hipSuccess) return fail(h, CH_ERR_DEVICE, std::string("ch_reset launch: ") + hipGetErrorString(e));
     if (!mask_dev) h->obs_zero_ptr = obs_dev;                    // every block written in full
     else if (h->obs_zero_ptr != obs_dev) h->obs_zero_ptr = nullptr;   // some blocks of obs_dev unknown
+    return CH_OK;
+}
+
+int ch_reset_with(ch_handle* h, const uint8_t* mask_dev, const int32_t* num_drones, const double* cow_vel,
+                  float* obs_dev, void* stream) {
+    if (!h) return fail(nullptr, CH_ERR_INVALID, "ch_reset_with: NULL handle");
+    if (!obs_dev) return fail(h, CH_ERR_INVALID, "ch_reset_with: obs is NULL");
+    if (num_drones)
+        for (int64_t e = 0; e < h->E; ++e)
+            if (num_drones[e] < 1 || num_drones[e] > h->NC)
+                return fail(h, CH_ERR_INVALID,
+                            "ch_reset_with: NUM_DRONES " + std::to_string(num_drones[e]) + " outside [1, num_drones] "
+                            "(the reference indexes controllers sized by num_drones, BaseRLAviary.py:80)");
+    HIP_TRY(h, hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    if (num_drones) {
+        if (!h->rdn) HIP_TRY(h, hipMalloc(&h->rdn, sizeof(int) * h->E));
+        HIP_TRY(h, hipMemcpyAsync(h->rdn, num_drones, sizeof(int) * h->E, hipMemcpyHostToDevice, st));
+    }
+    if (cow_vel) {
+        if (!h->rdv) HIP_TRY(h, hipMalloc(&h->rdv, sizeof(double) * h->E * h->M * 2));
+        HIP_TRY(h, hipMemcpyAsync(h->rdv, cow_vel, sizeof(double) * h->E * h->M * 2, hipMemcpyHostToDevice, st));
+    }
+    hipError_t e;
+    if (h->rsize == sizeof(double)) {
+        StepParams<double> p = params<double>(h);
+        p.reset_mask = mask_dev; p.obs = obs_dev;
+        p.reset_n = num_drones ? h->rdn : nullptr; p.reset_vel = cow_vel ? h->rdv : nullptr;
+        e = launch_reset(p, h->team, st);
+    } else {
+        StepParams<float> p = params<float>(h);
+        p.reset_mask = mask_dev; p.obs = obs_dev;
+        p.reset_n = num_drones ? h->rdn : nullptr; p.reset_vel = cow_vel ? h->rdv : nullptr;
+        e = launch_reset(p, h->team, st);
+    }
+    if (e != hipSuccess) return fail(h, CH_ERR_DEVICE, std::string("ch_reset_with launch: ") + hipGetErrorString(e));
+    HIP_TRY(h, hipStreamSynchronize(st));   // the host arrays may be reused as soon as this returns
+    if (!mask_dev) h->obs_zero_ptr = obs_dev;
+    else if (h->obs_zero_ptr != obs_dev) h->obs_zero_ptr = nullptr;
     return CH_OK;
 }
 

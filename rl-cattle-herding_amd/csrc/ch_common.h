@@ -69,7 +69,7 @@ __device__ __forceinline__ int reset_draw_n(const StepParams<R>& p, int episode,
 template <class R>
 __device__ __forceinline__ void reset_scalars(const StepParams<R>& p, int e, int& n, int& sc, int& scA, int& spawn,
                                               int& episode, int& active, int& has_prev, R& prev, R& clock) {
-    const int nn = reset_draw_n(p, episode, p.env_off + e);
+    const int nn = p.reset_n ? p.reset_n[e] : reset_draw_n(p, episode, p.env_off + e);
     n = nn;
     sc = 0; scA = 0;
     spawn += 1;
@@ -112,11 +112,15 @@ __device__ __forceinline__ void reset_cow_at(const StepParams<R>& p, long long c
                                              uint32_t episode, R& x, R& y, R& vx, R& vy) {
     const long long CS = (long long)p.E * p.M;
     x = x0; y = y0;
-    double u = philox_uniform53(p.k0, p.k1, episode, 1 + j, (uint32_t)env_id);
-    double ang = kPi * (2 * u - 1);
-    double sa, ca;
-    sincos(ang, &sa, &ca);
-    vx = R(kMaxVelCattle * ca); vy = R(kMaxVelCattle * sa);
+    if (p.reset_vel) {   // the host's replay of the reference's own draws (ch_reset_with, cattleherd/seeded.py)
+        vx = R(p.reset_vel[2 * ci]); vy = R(p.reset_vel[2 * ci + 1]);
+    } else {
+        double u = philox_uniform53(p.k0, p.k1, episode, 1 + j, (uint32_t)env_id);
+        double ang = kPi * (2 * u - 1);
+        double sa, ca;
+        sincos(ang, &sa, &ca);
+        vx = R(kMaxVelCattle * ca); vy = R(kMaxVelCattle * sa);
+    }
     p.cattle[0 * CS + ci] = x; p.cattle[1 * CS + ci] = y; p.cattle[2 * CS + ci] = vx; p.cattle[3 * CS + ci] = vy;
 }
 

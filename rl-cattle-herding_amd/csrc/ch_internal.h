@@ -61,6 +61,8 @@ struct StepParams {
     int* err;                 // device error word of the handle (CH_DEVERR_* bits), read by ch_sync & co.
     int pw;                   // v2: per-wave env tables (V2Layout W = block / 64 - 1)
     double* evald;            // optional [E][NC]: update_evaluation_metrics' per-drone episode distance
+    const int* reset_n;       // optional (ch_reset_with): NUM_DRONES of each reset env instead of the Philox draw
+    const double* reset_vel;  // optional (ch_reset_with): [E][M][2] cattle spawn velocities instead of Philox
 };
 
 // device error word bits (ch_api.cpp reports them as CH_ERR_DEVICE)

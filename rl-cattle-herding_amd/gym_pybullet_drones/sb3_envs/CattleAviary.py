@@ -11,6 +11,7 @@ Gymnasium / SB3 ``DummyVecEnv`` / ``evaluate_policy`` use; for throughput use th
 import numpy as np
 
 from cattleherd.evaluation import EvalTracker, Evaluator
+from cattleherd.seeded import ReferenceResetRNG
 from cattleherd.env import HerdBatch
 from cattleherd.spaces import (ActionType, DroneModel, ObservationType, Physics, check_supported,
                                ctde_action_space, ctde_observation_space)
@@ -34,7 +35,8 @@ class CattleAviary(_EnvBase):
                  physics: Physics = Physics.PYB, pyb_freq: int = 240, ctrl_freq: int = 60, gui=False, record=False,
                  obs: ObservationType = ObservationType.COKIN, act: ActionType = ActionType.VEL, *,
                  curriculum_level: int = 7, device=None, compat: bool = True, precision: str = "f64",
-                 min_drones=None, max_drones=None, seed: int = 0x5EED, env_id: int = 0):
+                 min_drones=None, max_drones=None, seed: int = 0x5EED, env_id: int = 0,
+                 reference_rng_seed=None):
         check_supported(drone_model, physics, obs, act)
         if pyb_freq % ctrl_freq != 0:
             raise ValueError("[ERROR] in BaseAviary.__init__(), pyb_freq is not divisible by env_freq.")
@@ -55,6 +57,9 @@ class CattleAviary(_EnvBase):
                                curriculum_level=curriculum_level, seed=seed, env_id_offset=env_id,
                                ctrl_freq=ctrl_freq, pyb_freq=pyb_freq, physics=physics)
         self._num_drones_ctor = num_drones
+        # seed-exact resets: the draws a reference env makes after `random.seed(s); np.random.seed(s)`
+        # (cattleherd/seeded.py; the curriculum's own [min, max] drone range, as the reference draws it)
+        self._ref_rng = None if reference_rng_seed is None else ReferenceResetRNG(reference_rng_seed, lo, hi, num_cattle)
         self.NUM_DRONES = num_drones
         self.action_space = ctde_action_space(num_drones)
         self.observation_space = ctde_observation_space()
@@ -84,7 +89,14 @@ class CattleAviary(_EnvBase):
 
     def reset(self, seed: int = None, options: dict = None):
         """BaseAviary.reset (sb3_envs/BaseAviary.py:280-331); ``seed`` is ignored like the reference's."""
-        obs = self.batch.reset()
+        if self._ref_rng is not None:
+            scA = getattr(self, "step_counter_A", 0)   # steps of the episode that ends (its flocking draws)
+            n, vel = self._ref_rng.reset(scA)
+            if n > self._num_drones_ctor:   # the reference indexes controllers sized by num_drones (BaseRLAviary.py:80)
+                raise IndexError(f"NUM_DRONES draw {n} exceeds num_drones={self._num_drones_ctor}")
+            obs = self.batch.reset(num_drones=[n], cow_vel=vel[None])
+        else:
+            obs = self.batch.reset()
         s = self.batch.get_state()
         self._sync_counts(s)
         self._tracker.on_reset(s, self.NUM_DRONES)

@@ -490,6 +490,46 @@ def gen_eval(rng, n=3, m=4, level=2, steps=1300):
     print("eval_ctde", steps, "steps; resets at", rec["reset_at"], "episodes", len(lens), "lengths", lens)
 
 
+def gen_reset_seeded(seeds=(7, 20251031), schedule=(0, 3, 10, 1, 7, 0, 4)):
+    """The reference's own random draws for resets under seeded global RNGs: ``random.seed(s);
+    np.random.seed(s)`` then ``CattleAviary(num_drones=12, num_cattle=16)`` at curriculum level 7 (the CTDE
+    driver's setup), reset, ``schedule[k]`` steps, reset, ...  Draw sites: NUM_DRONES =
+    random.randint(min, max) (sb3_envs/BaseAviary.py:242 at construction, 307 per reset), per cow a yaw and
+    a velocity angle np.pi * (2 np.random.rand() - 1) (617, 631), and per flocking step the drift noise
+    np.random.normal(0, 0.02, (M, 2)) (1373; once an initial np.random.uniform(-0.1, 0.1, (M, 2)), 1366).
+    The actions come from a separate generator, so only the env consumes the global streams."""
+    import random
+    out = {"seeds": np.array(seeds, np.int64), "schedule": np.array(schedule, np.int64)}
+    for si, seed in enumerate(seeds):
+        random.seed(seed)
+        np.random.seed(seed)
+        orig = CA_mod.CurriculumLearning
+        CA_mod.CurriculumLearning = lambda _lvl: CurriculumLearning(7)
+        try:
+            with quiet():
+                env = CA_mod.CattleAviary(num_drones=12, num_cattle=16)
+        finally:
+            CA_mod.CurriculumLearning = orig
+        arng = np.random.default_rng(1000 + si)
+        rec = {"n": [], "cow_pos": [], "cow_vel": [], "drone_pos": [], "spawn_index": [], "scA_before": []}
+        out[f"s{si}_ctor_n"] = np.int64(env.NUM_DRONES)
+        for k, steps in enumerate(schedule):
+            rec["scA_before"].append(env.step_counter_A)
+            with quiet():
+                env.reset()
+            c = capture(env)
+            rec["n"].append(c["n"]); rec["cow_pos"].append(c["cow_pos"][:16]); rec["cow_vel"].append(c["cow_vel"][:16])
+            rec["drone_pos"].append(c["drone_pos"]); rec["spawn_index"].append(c["spawn_index"])
+            for _ in range(steps):
+                a = arng.uniform(-1, 1, (12, 4)).astype(np.float32)
+                with quiet():
+                    env.step(a)
+        for key, v in rec.items():
+            out[f"s{si}_{key}"] = np.array(v)
+    np.savez_compressed(os.path.join(HERE, "reset_seeded.npz"), **out)
+    print("reset_seeded", {k: out[k].tolist() for k in out if k.endswith("_n")})
+
+
 PHYSICS_IDS = {"pyb": 0, "dyn": 1, "pyb_gnd": 2, "pyb_drag": 3, "pyb_dw": 4, "pyb_gnd_drag_dw": 5}
 
 
@@ -636,6 +676,8 @@ def main():
 if __name__ == "__main__":
     if "--physics" in sys.argv:   # the physics-variant fixtures only (own seeds)
         gen_physics()
+    elif "--reset-seeded" in sys.argv:   # reset_seeded.npz only (seeds its own global RNGs)
+        gen_reset_seeded()
     elif "--eval" in sys.argv:   # eval_ctde.npz only, own seed
         np.random.seed(12345)
         import random
