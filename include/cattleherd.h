@@ -53,7 +53,9 @@ enum {
     CH_PHYS_PYB_GND = 2,      /* + _groundEffect (943-980) */
     CH_PHYS_PYB_DRAG = 3,     /* + _drag (982-1011) */
     CH_PHYS_PYB_DW = 4,       /* + _downwash (1013-1041) */
-    CH_PHYS_PYB_GND_DRAG_DW = 5
+    CH_PHYS_PYB_GND_DRAG_DW = 5,
+    CH_PHYS_DYN_RK4 = 6       /* option, not in the reference: DYN's equations of motion integrated by classic
+                                 RK4 per substep (q renormalised); cattle stay put as under DYN */
 };
 
 /* Flags for ch_step_io.flags */

@@ -170,7 +170,7 @@ static const double DRAG_XY = 9.1785e-7, DRAG_Z = 10.311e-7;
 static const double DW_C1 = 2267.18, DW_C2 = .16, DW_C3 = -.11;
 static const double THRUST2WEIGHT = 2.25;
 
-enum { PH_PYB = 0, PH_DYN = 1, PH_GND = 2, PH_DRAG = 3, PH_DW = 4, PH_ALL = 5 };
+enum { PH_PYB = 0, PH_DYN = 1, PH_GND = 2, PH_DRAG = 3, PH_DW = 4, PH_ALL = 5, PH_DYN_RK4 = 6 };
 static int ph_gnd(int ph) { return ph == PH_GND || ph == PH_ALL; }
 static int ph_drag(int ph) { return ph == PH_DRAG || ph == PH_ALL; }
 static int ph_dw(int ph) { return ph == PH_DW || ph == PH_ALL; }
@@ -274,6 +274,66 @@ static void dyn_substep(double* p, double* q, double* v, double* w, double* rr, 
     }
     for (int i = 0; i < 3; ++i) w[i] = R[3 * i + 0] * rr[0] + R[3 * i + 1] * rr[1] + R[3 * i + 2] * rr[2];
 }
+/* RK4 option (north_star; not a reference path): the equations of motion of _dynamics
+ * (BaseAviary.py:1043-1102) as an ODE in y = (p, v, q, w_b) -- p' = v, v' = (R(q) T e_z - m g e_z) / m,
+ * w_b' = J^-1 (tau - w_b x J w_b), q' = 1/2 L(w_b) q with _integrateQ's L (1104-1118) -- integrated by the
+ * classic four-stage Runge-Kutta over one substep at constant rpm; q renormalised after the step and the
+ * world angular velocity reported as R(q_new) w_b (DYN reports R(q_old) w_b). */
+static void dyn_deriv(const double* q, const double* v, const double* rr, const double* rpm, double* dp, double* dv,
+                      double* dq, double* drr) {
+    double R[9]; och_matrix_from_quat(q, R);
+    double f[4], z[4];
+    for (int i = 0; i < 4; ++i) { f[i] = rpm[i] * rpm[i] * KF; z[i] = rpm[i] * rpm[i] * KM; }
+    const double T = f[0] + f[1] + f[2] + f[3];
+    const double fw[3] = {R[2] * T, R[5] * T, R[8] * T - G * MASS};
+    const double zt = -z[0] + z[1] - z[2] + z[3];
+    const double ls = ARM / sqrt(2.0);
+    const double xt = (f[0] + f[1] - f[2] - f[3]) * ls, yt = (-f[0] + f[1] + f[2] - f[3]) * ls;
+    const double Jr[3] = {JX * rr[0], JY * rr[1], JZ * rr[2]};
+    double c[3]; cross3(rr, Jr, c);
+    const double tq[3] = {xt - c[0], yt - c[1], zt - c[2]};
+    const double jinv[3] = {1.0 / JX, 1.0 / JY, 1.0 / JZ};
+    for (int i = 0; i < 3; ++i) { dp[i] = v[i]; dv[i] = fw[i] / MASS; drr[i] = jinv[i] * tq[i]; }
+    const double P = rr[0], Q = rr[1], Rz = rr[2];
+    const double L[4][4] = {{0, Rz, -Q, P}, {-Rz, 0, P, Q}, {Q, -P, 0, Rz}, {-P, -Q, -Rz, 0}};
+    for (int i = 0; i < 4; ++i) dq[i] = 0.5 * (L[i][0] * q[0] + L[i][1] * q[1] + L[i][2] * q[2] + L[i][3] * q[3]);
+}
+static void rk4_substep(double* p, double* q, double* v, double* w, double* rr, const double* rpm, double dt) {
+    double kp[4][3], kv[4][3], kq[4][4], kr[4][3];
+    double yp[3], yv[3], yq[4], yr[3];
+    const double a[4] = {0.0, 0.5 * dt, 0.5 * dt, dt};
+    for (int s = 0; s < 4; ++s) {
+        for (int i = 0; i < 3; ++i) {
+            yp[i] = s ? p[i] + a[s] * kp[s - 1][i] : p[i];
+            yv[i] = s ? v[i] + a[s] * kv[s - 1][i] : v[i];
+            yr[i] = s ? rr[i] + a[s] * kr[s - 1][i] : rr[i];
+        }
+        for (int i = 0; i < 4; ++i) yq[i] = s ? q[i] + a[s] * kq[s - 1][i] : q[i];
+        (void)yp;
+        dyn_deriv(yq, yv, yr, rpm, kp[s], kv[s], kq[s], kr[s]);
+    }
+    const double h6 = dt / 6.0;
+    for (int i = 0; i < 3; ++i) {
+        p[i] = p[i] + h6 * (((kp[0][i] + 2.0 * kp[1][i]) + 2.0 * kp[2][i]) + kp[3][i]);
+        v[i] = v[i] + h6 * (((kv[0][i] + 2.0 * kv[1][i]) + 2.0 * kv[2][i]) + kv[3][i]);
+        rr[i] = rr[i] + h6 * (((kr[0][i] + 2.0 * kr[1][i]) + 2.0 * kr[2][i]) + kr[3][i]);
+    }
+    for (int i = 0; i < 4; ++i) q[i] = q[i] + h6 * (((kq[0][i] + 2.0 * kq[1][i]) + 2.0 * kq[2][i]) + kq[3][i]);
+    const double qn = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    for (int i = 0; i < 4; ++i) q[i] = q[i] / qn;
+    double R[9]; och_matrix_from_quat(q, R);
+    for (int i = 0; i < 3; ++i) w[i] = R[3 * i + 0] * rr[0] + R[3 * i + 1] * rr[1] + R[3 * i + 2] * rr[2];
+}
+
+/* One drone, `steps` substeps of DYN (rk4 = 0, explicit Euler as the reference) or the RK4 option at
+ * constant rpm: the order-of-convergence probe (tests/test_oracle_golden.py). y = p[3] v[3] q[4] rr[3] w[3]. */
+void och_dyn_integrate(double* y, const double* rpm, double dt, int64_t steps, int rk4) {
+    for (int64_t s = 0; s < steps; ++s) {
+        if (rk4) rk4_substep(y, y + 6, y + 3, y + 13, y + 10, rpm, dt);
+        else dyn_substep(y, y + 6, y + 3, y + 13, y + 10, rpm, dt);
+    }
+}
+
 static void drone_substep(const och_config* c, double* p, double* q, double* v, double* w, const double* rpm, double dt,
                           const phys_ctx* x) {
     double R[9]; och_matrix_from_quat(q, R);
@@ -904,12 +964,14 @@ int och_step(const och_config* c, och_state* s, const float* actions, float* obs
         for (int k = 0; k < n; ++k) {
             if (ph == PH_DYN) {
                 dyn_substep(s->dp[k], s->dq[k], s->dv[k], s->dw[k], s->rpy_rates[k], rpm[k], dt);
+            } else if (ph == PH_DYN_RK4) {
+                rk4_substep(s->dp[k], s->dq[k], s->dv[k], s->dw[k], s->rpy_rates[k], rpm[k], dt);
             } else {
                 phys_ctx x = {ph, s->last_rpm[k], (const double (*)[3])pos0, n, k, h_clip};
                 drone_substep(c, s->dp[k], s->dq[k], s->dv[k], s->dw[k], rpm[k], dt, ph == PH_PYB ? NULL : &x);
             }
         }
-        if (ph != PH_DYN)   /* no p.stepSimulation under DYN: the cattle bodies do not move (447-448) */
+        if (ph != PH_DYN && ph != PH_DYN_RK4)   /* no p.stepSimulation under DYN: the cattle bodies do not move (447-448) */
             for (int j = 0; j < c->m; ++j) { s->cp[j][0] += s->cv[j][0] * dt; s->cp[j][1] += s->cv[j][1] * dt; }
         for (int k = 0; k < n; ++k) memcpy(s->last_rpm[k], rpm[k], sizeof(rpm[k]));   /* 450 */
     }

@@ -66,6 +66,7 @@ double och_simple_spacing(double r, int level);
 double och_complex_spacing(double r, int level);
 double och_cattle_spacing(double r);
 double och_gnd_eff_h_clip(void);   /* BaseAviary.py:173 */
+void och_dyn_integrate(double* y, const double* rpm, double dt, int64_t steps, int rk4);   /* DYN / RK4 probe */
 
 /* whole env */
 int  och_obs_rows(const och_config* c);

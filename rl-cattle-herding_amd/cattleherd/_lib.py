@@ -17,7 +17,7 @@ METRIC_NAMES = ("steps", "episodes", "return_sum", "length_sum", "terminated", "
                 "effectiveness_sum")
 ABI_VERSION = 3
 # Physics enum (utils/enums.py:13-21, include/cattleherd.h CH_PHYS_*)
-PHYSICS = {"pyb": 0, "dyn": 1, "pyb_gnd": 2, "pyb_drag": 3, "pyb_dw": 4, "pyb_gnd_drag_dw": 5}
+PHYSICS = {"pyb": 0, "dyn": 1, "pyb_gnd": 2, "pyb_drag": 3, "pyb_dw": 4, "pyb_gnd_drag_dw": 5, "dyn_rk4": 6}
 
 # every symbol include/cattleherd.h declares
 EXPORTS = ("ch_default_config", "ch_create", "ch_destroy", "ch_last_error", "ch_shape", "ch_reset", "ch_reset_with",

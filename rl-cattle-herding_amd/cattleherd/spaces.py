@@ -38,10 +38,11 @@ except Exception:  # noqa: BLE001
         def __repr__(self):
             return f"Box({self.shape}, {self.dtype})"
 
-# enums: same member names and values as the reference's utils/enums.py
+# enums: same member names and values as the reference's utils/enums.py, plus DYN_RK4 (the RK4 integrator
+# option of include/cattleherd.h CH_PHYS_DYN_RK4, not a reference member)
 DroneModel = Enum("DroneModel", [("CF2X", "cf2x"), ("CF2P", "cf2p"), ("RACE", "racer")])
 Physics = Enum("Physics", [("PYB", "pyb"), ("DYN", "dyn"), ("PYB_GND", "pyb_gnd"), ("PYB_DRAG", "pyb_drag"),
-                           ("PYB_DW", "pyb_dw"), ("PYB_GND_DRAG_DW", "pyb_gnd_drag_dw")])
+                           ("PYB_DW", "pyb_dw"), ("PYB_GND_DRAG_DW", "pyb_gnd_drag_dw"), ("DYN_RK4", "dyn_rk4")])
 ImageType = Enum("ImageType", [("RGB", 0), ("DEP", 1), ("SEG", 2), ("BW", 3)])
 ActionType = Enum("ActionType", [("RPM", "rpm"), ("PID", "pid"), ("VEL", "vel"), ("ONE_D_RPM", "one_d_rpm"),
                                  ("ONE_D_PID", "one_d_pid")])
@@ -75,7 +76,7 @@ def check_supported(drone_model, physics, obs, act):
         return getattr(x, "value", x)
     if val(drone_model) not in ("cf2x", "cf2p"):
         raise ValueError("[ERROR] in BaseRLAviary.__init()__, no controller is available for the specified drone_model")
-    if val(physics) not in ("pyb", "dyn", "pyb_gnd", "pyb_drag", "pyb_dw", "pyb_gnd_drag_dw"):
+    if val(physics) not in ("pyb", "dyn", "pyb_gnd", "pyb_drag", "pyb_dw", "pyb_gnd_drag_dw", "dyn_rk4"):
         raise ValueError(f"physics={val(physics)!r} is not a Physics member (utils/enums.py:13-21)")
     if val(obs) != "cokin":
         raise ValueError("[ERROR] in BaseRLAviary._observationSpace()")

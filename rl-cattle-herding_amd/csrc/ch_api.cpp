@@ -246,7 +246,7 @@ int ch_create(const ch_config* c, int64_t n_envs, int32_t device, ch_handle** ou
     *out = nullptr;
     if (c->abi_version != CH_ABI_VERSION) return fail(nullptr, CH_ERR_INVALID, "ch_create: abi_version mismatch");
     if (c->mode != CH_MODE_CTDE && c->mode != CH_MODE_MARL) return fail(nullptr, CH_ERR_INVALID, "ch_create: bad mode");
-    if (c->physics < CH_PHYS_PYB || c->physics > CH_PHYS_PYB_GND_DRAG_DW)
+    if (c->physics < CH_PHYS_PYB || c->physics > CH_PHYS_DYN_RK4)
         return fail(nullptr, CH_ERR_INVALID, "ch_create: physics must be one of CH_PHYS_* (utils/enums.py:13-21)");
     if (n_envs <= 0 || n_envs > (1ll << 28)) return fail(nullptr, CH_ERR_INVALID, "ch_create: n_envs out of range");
     if (c->num_drones < 1 || c->num_drones > kNMax)

@@ -439,6 +439,68 @@ __device__ __forceinline__ void dyn_substep(R p[3], R q[4], R v[3], R w[3], R rr
     for (int i = 0; i < 3; ++i) w[i] = M[3 * i + 0] * rr[0] + M[3 * i + 1] * rr[1] + M[3 * i + 2] * rr[2];
 }
 
+// RK4 option (CH_PHYS_DYN_RK4; north_star, not a reference path): the DYN equations of motion
+// (_dynamics, BaseAviary.py:1043-1102; _integrateQ's L, 1104-1118) as an ODE in (p, v, q, w_b), classic
+// four-stage Runge-Kutta over one substep at constant rpm, q renormalised, world rates R(q_new) w_b.
+// Same operations in the same order as the oracle's rk4_substep (ch_oracle.c).
+template <class R>
+__device__ __forceinline__ void dyn_deriv(const R q[4], const R v[3], const R rr[3], const R rpm[4], R dp[3], R dv[3],
+                                          R dq[4], R drr[3]) {
+    R M[9];
+    quat_to_mat(q, M);
+    R f[4], z[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { f[i] = rpm[i] * rpm[i] * R(kKF); z[i] = rpm[i] * rpm[i] * R(kKM); }
+    const R T = f[0] + f[1] + f[2] + f[3];
+    const R fw[3] = {M[2] * T, M[5] * T, M[8] * T - R(kG * kMass)};
+    const R zt = -z[0] + z[1] - z[2] + z[3];
+    const R ls = R(kArm) / sqrt(R(2));
+    const R xt = (f[0] + f[1] - f[2] - f[3]) * ls, yt = (-f[0] + f[1] + f[2] - f[3]) * ls;
+    const R J[3] = {R(kJx), R(kJy), R(kJz)};
+    const R Jr[3] = {J[0] * rr[0], J[1] * rr[1], J[2] * rr[2]};
+    const R c[3] = {rr[1] * Jr[2] - rr[2] * Jr[1], rr[2] * Jr[0] - rr[0] * Jr[2], rr[0] * Jr[1] - rr[1] * Jr[0]};
+    const R tq[3] = {xt - c[0], yt - c[1], zt - c[2]};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { dp[i] = v[i]; dv[i] = fw[i] / R(kMass); drr[i] = (R(1) / J[i]) * tq[i]; }
+    const R P = rr[0], Q = rr[1], Z = rr[2];
+    const R L[4][4] = {{0, Z, -Q, P}, {-Z, 0, P, Q}, {Q, -P, 0, Z}, {-P, -Q, -Z, 0}};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dq[i] = R(0.5) * (L[i][0] * q[0] + L[i][1] * q[1] + L[i][2] * q[2] + L[i][3] * q[3]);
+}
+template <class R>
+__device__ __forceinline__ void rk4_substep(R p[3], R q[4], R v[3], R w[3], R rr[3], const R rpm[4], R dt) {
+    R kp[4][3], kv[4][3], kq[4][4], kr[4][3];
+    const R a[4] = {R(0), R(0.5) * dt, R(0.5) * dt, dt};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        R yv[3], yq[4], yr[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            yv[i] = s ? v[i] + a[s] * kv[s - 1][i] : v[i];
+            yr[i] = s ? rr[i] + a[s] * kr[s - 1][i] : rr[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) yq[i] = s ? q[i] + a[s] * kq[s - 1][i] : q[i];
+        dyn_deriv(yq, yv, yr, rpm, kp[s], kv[s], kq[s], kr[s]);
+    }
+    const R h6 = dt / R(6.0);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        p[i] = p[i] + h6 * (((kp[0][i] + R(2) * kp[1][i]) + R(2) * kp[2][i]) + kp[3][i]);
+        v[i] = v[i] + h6 * (((kv[0][i] + R(2) * kv[1][i]) + R(2) * kv[2][i]) + kv[3][i]);
+        rr[i] = rr[i] + h6 * (((kr[0][i] + R(2) * kr[1][i]) + R(2) * kr[2][i]) + kr[3][i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = q[i] + h6 * (((kq[0][i] + R(2) * kq[1][i]) + R(2) * kq[2][i]) + kq[3][i]);
+    const R qn = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = q[i] / qn;
+    R M[9];
+    quat_to_mat(q, M);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) w[i] = M[3 * i + 0] * rr[0] + M[3 * i + 1] * rr[1] + M[3 * i + 2] * rr[2];
+}
+
 // Physics variants (BaseAviary.py:420-450) for the drone on this lane, all substeps of one control
 // step.  `base` is the lane of the env's drone 0, `nsh` a wave-uniform bound (>= n) on its drones and
 // n its live drones; lr / rr carry last_clipped_action and the DYN body rates in and out.  The
@@ -455,6 +517,8 @@ __device__ __forceinline__ void variant_substeps(const StepParams<R>& p, int bas
     for (int s = 0; s < p.substeps; ++s) {
         if (ph == CH_PHYS_DYN) {
             dyn_substep(pos, q, v, w, rr, rpm, R(p.dt));
+        } else if (ph == CH_PHYS_DYN_RK4) {
+            rk4_substep(pos, q, v, w, rr, rpm, R(p.dt));
         } else {
             // extra() runs before drone_substep moves the body: pos/q/v are the substep-start state
             auto extra = [&](const R* M, R* F, R* Tw) {

@@ -229,7 +229,7 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
             cvx = ld(p.cattle, 2, CS, ci); cvy = ld(p.cattle, 3, CS, ci);
             const R dt = R(p.dt);
             // no p.stepSimulation under Physics.DYN: the cattle bodies keep their positions (BaseAviary.py:447-448)
-            if (!PHYS || p.physics != CH_PHYS_DYN)
+            if (!PHYS || (p.physics != CH_PHYS_DYN && p.physics != CH_PHYS_DYN_RK4))
                 for (int s = 0; s < p.substeps; ++s) { x += cvx * dt; y += cvy * dt; }
             p.cattle[0 * CS + ci] = x; p.cattle[1 * CS + ci] = y;
             S.cx[t] = x; S.cy[t] = y; S.cvx[t] = cvx; S.cvy[t] = cvy;

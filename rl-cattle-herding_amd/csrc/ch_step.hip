@@ -554,7 +554,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             const R vx = p.cattle[2 * CS + ci], vy = p.cattle[3 * CS + ci];
             const R dt = R(p.dt);
             // frictionless cube (trace-pinned); no p.stepSimulation under Physics.DYN (BaseAviary.py:447-448)
-            if (!PHYS || p.physics != CH_PHYS_DYN)
+            if (!PHYS || (p.physics != CH_PHYS_DYN && p.physics != CH_PHYS_DYN_RK4))
                 for (int s = 0; s < p.substeps; ++s) { x += vx * dt; y += vy * dt; }
             CH_ST(&p.cattle[0 * CS + ci], x); CH_ST(&p.cattle[1 * CS + ci], y);
             S.cx[u] = x; S.cy[u] = y; S.cvx[u] = vx; S.cvy[u] = vy;

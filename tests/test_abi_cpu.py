@@ -81,9 +81,10 @@ def test_physics_field_default_and_range():
     assert L.ch_default_config(ctypes.byref(c), 0, 4, 16) == 0
     assert c.physics == _lib.PHYSICS["pyb"] == 0
     assert _lib.ChConfig.physics.offset == _lib.ChConfig.spawn_cows.offset + 4
+    assert _lib.ChConfig.eval_metrics.offset == _lib.ChConfig.physics.offset + 4 and c.eval_metrics == 1
     assert ctypes.sizeof(_lib.ChConfig) % 8 == 0
     h = ctypes.c_void_p()
-    for bad in (-1, 6):
+    for bad in (-1, 7):
         c.physics = bad
         assert L.ch_create(ctypes.byref(c), 8, 0, ctypes.byref(h)) == _lib.CH_ERR_INVALID
         assert b"physics" in L.ch_last_error(None)

@@ -183,7 +183,8 @@ def _oracle_view(g, e, nmax):
 
 
 @pytest.mark.parametrize("physics,mode,n,m", [("pyb", 0, 4, 16), ("pyb", 1, 4, 16), ("pyb", 0, 2, 8),
-                                               ("dyn", 0, 4, 16), ("pyb_gnd_drag_dw", 0, 4, 16),
+                                               ("dyn", 0, 4, 16), ("dyn_rk4", 0, 4, 16), ("dyn_rk4", 0, 2, 8),
+                                               ("pyb_gnd_drag_dw", 0, 4, 16),
                                                ("pyb_gnd_drag_dw", 1, 3, 8)])
 def test_random_rollout_with_autoreset_vs_oracle(physics, mode, n, m):
     """240 lockstep steps of device Philox actions with in-kernel auto-reset: before every step the
@@ -329,7 +330,7 @@ def test_full_size_properties():
                                              (0, 4, 16, 4096, "dyn"), (0, 4, 16, 1000, "pyb_gnd"),
                                              (0, 4, 16, 1000, "pyb_drag"), (0, 6, 8, 1000, "pyb_dw"),
                                              (0, 4, 16, 4096, "pyb_gnd_drag_dw"), (1, 4, 16, 333, "pyb_gnd_drag_dw"),
-                                             (1, 3, 8, 257, "dyn")])
+                                             (1, 3, 8, 257, "dyn"), (0, 4, 16, 1000, "dyn_rk4"), (1, 4, 32, 300, "dyn_rk4")])
 def test_step_kernels_v1_v2_bit_identical(mode, n, m, E, geom):
     """The role-split v2 step kernel (ch_step.hip, the default) and the team-per-env v1 kernel
     (ch_kernels.hip) compute the same arithmetic in the same order: 150 random-action steps with
