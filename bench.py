@@ -126,11 +126,38 @@ def policy_rollout(b, n, steps, warmup):
     d0 = actor.dims
     flops = 2.0 * E * (n * 86 * d0[1] + sum(d0[i] * d0[i + 1] for i in range(1, len(d0) - 1)))
     tf = flops / (fwd_us * 1e-6) / 1e12
-    return {"env_steps_per_s": E * steps / dt, "ms_per_step": dt / steps * 1000.0,
-            "policy": "SB3 MlpPolicy actor 1032-128-128-48 tanh (model-v16-6), deterministic, f32",
-            "forward_us": fwd_us,
-            "roofline": {"bound": "mfma", "achieved": tf, "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": tf / MFMA_F32_PEAK_TFLOPS, "flops_per_forward": flops}}
+    out = {"env_steps_per_s": E * steps / dt, "ms_per_step": dt / steps * 1000.0,
+           "policy": "SB3 MlpPolicy actor 1032-128-128-48 tanh (model-v16-6), deterministic, f32",
+           "forward_us": fwd_us,
+           "roofline": {"bound": "mfma", "achieved": tf, "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": tf / MFMA_F32_PEAK_TFLOPS, "flops_per_forward": flops}}
+    out["ppo_rollout"] = ppo_rollout(b, d)
+    return out
+
+
+def ppo_rollout(b, d, T=32):
+    """SB3 collect_rollouts on the device (cattleherd.rollout): per step actor + critic forward,
+    Gaussian sample / log-prob / buffer store, env step with auto-reset and terminal obs, V(terminal obs)
+    bootstrap; then GAE.  env-steps/s of one whole T-step collection (after one untimed collection)."""
+    import torch
+    from cattleherd.policy import DevicePolicy
+    from cattleherd.rollout import DeviceRolloutBuffer
+    sd = {k.replace("__", "."): torch.tensor(d[k]) for k in d.files if "__" in k}
+    actor = DevicePolicy.sb3_actor(sd, clip=False)
+    critic = DevicePolicy.sb3_critic(sd)
+    log_std = torch.full((actor.dims[-1],), -1.0, device=b.device)   # log_std_init (CTDECattleHerder.py:122)
+    rb = DeviceRolloutBuffer(b, T, act_dim=actor.dims[-1])
+    b.reset()
+    rb.collect(actor, critic, log_std, seed=1)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rb.collect(actor, critic, log_std, seed=2)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    out = {"env_steps_per_s": b.n_envs * T / dt, "ms_per_step": dt / T * 1000.0, "n_steps": T,
+           "buffer_GB": sum(t.numel() * 4 for t in (rb.obs, rb.actions)) / 1e9}
+    del rb
+    return out
 
 
 def cpu_baseline(mode, n, m, seconds=12.0):

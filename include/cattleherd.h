@@ -221,6 +221,46 @@ int ch_mlp_forward(const ch_mlp* net, const float* x, int64_t rows, float* y, vo
  * in the observation and are not multiplied. */
 int ch_policy_forward(ch_handle* h, const ch_mlp* net, const float* obs, float* y, void* stream);
 
+/* ---- On-device PPO rollout buffer ---------------------------------------------
+ * Replaces: stable_baselines3 OnPolicyAlgorithm.collect_rollouts' RolloutBuffer and
+ * RolloutBuffer.compute_returns_and_advantage for the CTDE driver's PPO (CTDECattleHerder.py:107-150:
+ * n_steps, gamma 0.99, gae_lambda 0.95, DiagGaussian actions with log_std).  CTDE handles only (one row
+ * per env).  All buffers are caller-owned device float32 arrays, rows = n_envs:
+ *   obs [T][rows][12*86], actions [T][rows][act_dim] (unclipped samples), rewards, episode_starts, values,
+ *   log_probs, advantages, returns [T][rows]; last_episode_starts [rows] (SB3's _last_episode_starts,
+ *   1 after a reset). */
+typedef struct ch_rollout {
+    int32_t n_steps;           /* T */
+    int32_t act_dim;           /* policy action width (the reference's 12 x 4 = 48) */
+    float* obs;
+    float* actions;
+    float* rewards;
+    float* episode_starts;
+    float* values;
+    float* log_probs;
+    float* advantages;
+    float* returns;
+    float* last_episode_starts;
+} ch_rollout;
+
+/* Step t, before env.step: copy obs [rows][12*86] into the buffer, sample actions = mean + exp(log_std) eps
+ * (eps ~ N(0,1) from Philox keyed by seed, counter (t, action, env)), store them with their summed Normal
+ * log-probability, value [rows] and the episode starts; write the actions clipped to [-1, 1] into
+ * env_actions [rows][num_drones][4] (the first num_drones*4 of act_dim, as the env reads a (12, 4) action). */
+int ch_rollout_store(ch_handle* h, const ch_rollout* rb, int32_t t, const float* obs, const float* mean,
+                     const float* value, const float* log_std, uint64_t seed, float* env_actions, void* stream);
+
+/* Step t, after env.step: rewards[t] = reward, plus gamma * terminal_value where the env was truncated and
+ * not terminated (SB3's TimeLimit.truncated bootstrap; terminal_value may be NULL); the next step's
+ * episode starts = terminated | truncated. */
+int ch_rollout_post(ch_handle* h, const ch_rollout* rb, int32_t t, const float* reward, const uint8_t* terminated,
+                    const uint8_t* truncated, const float* terminal_value, float gamma, void* stream);
+
+/* compute_returns_and_advantage: GAE(gamma, gae_lambda) backwards over the T steps in float32 with
+ * last_value [rows] = V(obs after the last step). */
+int ch_rollout_gae(ch_handle* h, const ch_rollout* rb, const float* last_value, float gamma, float gae_lambda,
+                   void* stream);
+
 #ifdef __cplusplus
 }
 #endif

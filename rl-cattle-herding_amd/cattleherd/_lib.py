@@ -23,7 +23,7 @@ PHYSICS = {"pyb": 0, "dyn": 1, "pyb_gnd": 2, "pyb_drag": 3, "pyb_dw": 4, "pyb_gn
 EXPORTS = ("ch_default_config", "ch_create", "ch_destroy", "ch_last_error", "ch_shape", "ch_reset", "ch_reset_with",
            "ch_step",
            "ch_state_size", "ch_get_state", "ch_set_state", "ch_metrics", "ch_metrics_device", "ch_sync",
-           "ch_get_eval", "ch_builtin_spawn_table",
+           "ch_get_eval", "ch_builtin_spawn_table", "ch_rollout_store", "ch_rollout_post", "ch_rollout_gae",
            "ch_spawn_table", "ch_mlp_forward", "ch_policy_forward")
 CH_ACT_NONE, CH_ACT_TANH, CH_ACT_RELU = 0, 1, 2
 

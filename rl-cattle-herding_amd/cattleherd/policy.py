@@ -66,13 +66,14 @@ class DevicePolicy:
 
     # ---- constructors for the reference's models ------------------------------------------------
     @classmethod
-    def sb3_actor(cls, state_dict, device=None):
-        """Deterministic SB3 ActorCriticPolicy action: policy_net (tanh) -> action_net, clipped to [-1, 1]."""
+    def sb3_actor(cls, state_dict, device=None, clip=True):
+        """Deterministic SB3 ActorCriticPolicy action: policy_net (tanh) -> action_net, clipped to [-1, 1]
+        (``clip=False``: the Gaussian mean, for stochastic rollouts, cattleherd.rollout)."""
         sd = state_dict
         layers = [(sd["mlp_extractor.policy_net.0.weight"], sd["mlp_extractor.policy_net.0.bias"]),
                   (sd["mlp_extractor.policy_net.2.weight"], sd["mlp_extractor.policy_net.2.bias"]),
                   (sd["action_net.weight"], sd["action_net.bias"])]
-        return cls(layers, "tanh", (-1.0, 1.0), device)
+        return cls(layers, "tanh", (-1.0, 1.0) if clip else None, device)
 
     @classmethod
     def sb3_critic(cls, state_dict, device=None):

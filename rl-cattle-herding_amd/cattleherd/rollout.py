@@ -1,0 +1,88 @@
+"""On-device PPO rollout collection for the CTDE driver.
+
+The reference trains with stable_baselines3 PPO (simulator/CTDECattleHerder.py:107-150: n_steps 2048,
+gamma 0.99, gae_lambda 0.95, MlpPolicy with log_std_init -1).  Each of its rollout steps copies the
+(n_envs, 12, 86) observations to the host, runs the policy, steps the SubprocVecEnv and appends to a numpy
+RolloutBuffer.  ``DeviceRolloutBuffer.collect`` keeps all of it on the GPU: actor and critic forwards
+(``ch_policy_forward``, f32 MFMA), the Gaussian sample / log-probability / buffer store
+(``ch_rollout_store``), the env step (``ch_step``), the truncation bootstrap with V(terminal_observation)
+and the episode starts (``ch_rollout_post``), and finally GAE (``ch_rollout_gae``).  The tensors then feed
+a torch PPO update directly.
+
+Semantics restated from SB3 2.7 (OnPolicyAlgorithm.collect_rollouts, RolloutBuffer,
+DiagGaussianDistribution); SB3 is not installed here, so the restatement is "parity unpinned" to its
+source.  The noise comes from Philox (seeded), not torch's generator.
+"""
+import ctypes
+
+from . import _lib as L
+
+
+class ChRollout(ctypes.Structure):
+    _fields_ = [("n_steps", ctypes.c_int32), ("act_dim", ctypes.c_int32)] + \
+        [(k, ctypes.c_void_p) for k in ("obs", "actions", "rewards", "episode_starts", "values", "log_probs",
+                                        "advantages", "returns", "last_episode_starts")]
+
+
+def _bind():
+    lib = L.lib()
+    vp, i32, u64, f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint64, ctypes.c_float
+    P = ctypes.POINTER(ChRollout)
+    lib.ch_rollout_store.argtypes = [vp, P, i32, vp, vp, vp, vp, u64, vp, vp]
+    lib.ch_rollout_post.argtypes = [vp, P, i32, vp, vp, vp, vp, f32, vp]
+    lib.ch_rollout_gae.argtypes = [vp, P, vp, f32, f32, vp]
+    for f in (lib.ch_rollout_store, lib.ch_rollout_post, lib.ch_rollout_gae):
+        f.restype = ctypes.c_int
+    return lib
+
+
+class DeviceRolloutBuffer:
+    def __init__(self, batch, n_steps, act_dim=None, gamma=0.99, gae_lambda=0.95):
+        if batch.mode != L.CH_MODE_CTDE:
+            raise ValueError("the SB3 rollout buffer is for CTDE batches")
+        torch = batch.torch
+        self.batch, self.T, self.gamma, self.gae_lambda = batch, int(n_steps), float(gamma), float(gae_lambda)
+        E, od = batch.n_envs, batch.obs_rows * 86
+        self.act_dim = int(act_dim or batch.num_drones * 4)
+        z = dict(dtype=torch.float32, device=batch.device)
+        self.obs = torch.zeros((self.T, E, od), **z)
+        self.actions = torch.zeros((self.T, E, self.act_dim), **z)
+        for k in ("rewards", "episode_starts", "values", "log_probs", "advantages", "returns"):
+            setattr(self, k, torch.zeros((self.T, E), **z))
+        self.last_episode_starts = torch.ones(E, **z)          # SB3: _last_episode_starts = ones after reset
+        self.env_actions = torch.zeros((E, batch.num_drones, 4), **z)
+        self.value = torch.zeros((E, 1), **z)
+        self.mean = torch.zeros((E, self.act_dim), **z)
+        self.terminal_value = torch.zeros((E, 1), **z)
+        rb = ChRollout()
+        rb.n_steps, rb.act_dim = self.T, self.act_dim
+        for k in ("obs", "actions", "rewards", "episode_starts", "values", "log_probs", "advantages", "returns",
+                  "last_episode_starts"):
+            setattr(rb, k, getattr(self, k).data_ptr())
+        self._rb = rb
+        self._lib = _bind()
+
+    def collect(self, actor, critic, log_std, seed=0, bootstrap_truncated=True):
+        """SB3 collect_rollouts for n_steps steps of every env, on the device.  ``actor``: DevicePolicy of
+        the action mean (no clip: SB3's action_net output), ``critic``: DevicePolicy of V, ``log_std``:
+        float32 [act_dim] device tensor."""
+        b, lib, rb = self.batch, self._lib, ctypes.byref(self._rb)
+        torch = b.torch
+        log_std = log_std.to(device=b.device, dtype=torch.float32).contiguous()
+        for t in range(self.T):
+            actor.forward_batch(b, self.mean)
+            critic.forward_batch(b, self.value)
+            L.check(lib.ch_rollout_store(b.handle, rb, t, b.obs.data_ptr(), self.mean.data_ptr(), self.value.data_ptr(),
+                                         log_std.data_ptr(), int(seed), self.env_actions.data_ptr(), b._stream()),
+                    b.handle)
+            b.step(self.env_actions, autoreset=True, terminal_obs=True)
+            tv = None
+            if bootstrap_truncated:
+                critic.forward(b.terminal_obs.view(b.n_envs, -1), self.terminal_value)
+                tv = self.terminal_value.data_ptr()
+            L.check(lib.ch_rollout_post(b.handle, rb, t, b.reward.data_ptr(), b.terminated.data_ptr(),
+                                        b.truncated.data_ptr(), tv, self.gamma, b._stream()), b.handle)
+        critic.forward_batch(b, self.value)
+        L.check(lib.ch_rollout_gae(b.handle, rb, self.value.data_ptr(), self.gamma, self.gae_lambda, b._stream()),
+                b.handle)
+        return self

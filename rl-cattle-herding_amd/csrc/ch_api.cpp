@@ -721,6 +721,69 @@ int ch_policy_forward(ch_handle* h, const ch_mlp* net, const float* obs, float* 
     return CH_OK;
 }
 
+static int rollout_args(ch_handle* h, const ch_rollout* rb, RolloutArgs& a, const char* who) {
+    if (!h) return fail(nullptr, CH_ERR_INVALID, std::string(who) + ": NULL handle");
+    if (!rb) return fail(h, CH_ERR_INVALID, std::string(who) + ": NULL rollout buffer");
+    if (h->cfg.mode != CH_MODE_CTDE)
+        return fail(h, CH_ERR_UNSUPPORTED, std::string(who) + ": the SB3 rollout buffer is for CTDE handles");
+    if (rb->n_steps < 1 || rb->act_dim < 1 || rb->act_dim > 256)
+        return fail(h, CH_ERR_INVALID, std::string(who) + ": n_steps >= 1 and 1 <= act_dim <= 256 required");
+    std::memset(&a, 0, sizeof(a));
+    a.T = rb->n_steps; a.rows = h->E; a.obs_dim = h->rows * 86; a.act_dim = rb->act_dim;
+    a.env_act_dim = std::min(rb->act_dim, h->NC * 4);
+    a.obs = rb->obs; a.actions = rb->actions; a.rewards = rb->rewards; a.episode_starts = rb->episode_starts;
+    a.values = rb->values; a.log_probs = rb->log_probs; a.advantages = rb->advantages; a.returns = rb->returns;
+    a.last_episode_starts = rb->last_episode_starts;
+    return CH_OK;
+}
+
+int ch_rollout_store(ch_handle* h, const ch_rollout* rb, int32_t t, const float* obs, const float* mean,
+                     const float* value, const float* log_std, uint64_t seed, float* env_actions, void* stream) {
+    RolloutArgs a;
+    int rc = rollout_args(h, rb, a, "ch_rollout_store");
+    if (rc) return rc;
+    if (t < 0 || t >= rb->n_steps) return fail(h, CH_ERR_INVALID, "ch_rollout_store: t outside [0, n_steps)");
+    if (!obs || !mean || !value || !log_std || !env_actions || !rb->obs || !rb->actions || !rb->values ||
+        !rb->log_probs || !rb->episode_starts || !rb->last_episode_starts)
+        return fail(h, CH_ERR_INVALID, "ch_rollout_store: NULL buffer");
+    if ((reinterpret_cast<uintptr_t>(obs) | reinterpret_cast<uintptr_t>(rb->obs)) & 15)
+        return fail(h, CH_ERR_INVALID, "ch_rollout_store: obs buffers must be 16-byte aligned");
+    a.t = t; a.obs_now = obs; a.mean = mean; a.value = value; a.log_std = log_std; a.seed = seed;
+    a.env_actions = env_actions;
+    HIP_TRY(h, hipSetDevice(h->device));
+    HIP_TRY(h, launch_rollout(a, 0, (hipStream_t)stream));
+    return CH_OK;
+}
+
+int ch_rollout_post(ch_handle* h, const ch_rollout* rb, int32_t t, const float* reward, const uint8_t* terminated,
+                    const uint8_t* truncated, const float* terminal_value, float gamma, void* stream) {
+    RolloutArgs a;
+    int rc = rollout_args(h, rb, a, "ch_rollout_post");
+    if (rc) return rc;
+    if (t < 0 || t >= rb->n_steps) return fail(h, CH_ERR_INVALID, "ch_rollout_post: t outside [0, n_steps)");
+    if (!reward || !terminated || !truncated || !rb->rewards || !rb->last_episode_starts)
+        return fail(h, CH_ERR_INVALID, "ch_rollout_post: NULL buffer");
+    a.t = t; a.reward = reward; a.terminated = terminated; a.truncated = truncated; a.terminal_value = terminal_value;
+    a.gamma = gamma;
+    HIP_TRY(h, hipSetDevice(h->device));
+    HIP_TRY(h, launch_rollout(a, 1, (hipStream_t)stream));
+    return CH_OK;
+}
+
+int ch_rollout_gae(ch_handle* h, const ch_rollout* rb, const float* last_value, float gamma, float gae_lambda,
+                   void* stream) {
+    RolloutArgs a;
+    int rc = rollout_args(h, rb, a, "ch_rollout_gae");
+    if (rc) return rc;
+    if (!last_value || !rb->rewards || !rb->values || !rb->episode_starts || !rb->advantages || !rb->returns)
+        return fail(h, CH_ERR_INVALID, "ch_rollout_gae: NULL buffer");
+    a.value = last_value; a.gamma = gamma;
+    a.gamma_lambda = (float)((double)gamma * (double)gae_lambda);   // SB3: float32(self.gamma * self.gae_lambda)
+    HIP_TRY(h, hipSetDevice(h->device));
+    HIP_TRY(h, launch_rollout(a, 2, (hipStream_t)stream));
+    return CH_OK;
+}
+
 int ch_metrics(ch_handle* h, double* out, int32_t reset_after, void* stream) {
     if (!h || !out) return fail(h, CH_ERR_INVALID, "ch_metrics: NULL argument");
     HIP_TRY(h, hipSetDevice(h->device));

@@ -43,4 +43,98 @@ hipError_t launch_metrics_reduce(double* metrics, long long E, double* out, cons
     return hipGetLastError();
 }
 
+
+// ---- on-device PPO rollout buffer (the SB3 loop of CTDECattleHerder.py:107-150) -------------
+// stable_baselines3 2.7 OnPolicyAlgorithm.collect_rollouts / RolloutBuffer.compute_returns_and_advantage
+// (SB3 is not in this image: restated from its published algorithm, "parity unpinned" to its source):
+//   actions ~ N(mean, exp(log_std)) stored unclipped, the env gets them clipped to the Box [-1, 1];
+//   log_prob = sum_i Normal(mean_i, std_i).log_prob(a_i); episode_start = the previous step's done;
+//   a done that is a truncation (TimeLimit.truncated = truncated and not terminated) bootstraps the
+//   reward with gamma V(terminal_observation); GAE(gamma, lambda) backwards over the buffer in float32.
+namespace {
+__device__ __forceinline__ void philox_k(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        uint32_t lo0 = 0xD2511F53u * c[0], hi0 = __umulhi(0xD2511F53u, c[0]);
+        uint32_t lo1 = 0xCD9E8D57u * c[2], hi1 = __umulhi(0xCD9E8D57u, c[2]);
+        uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+        c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+}
+constexpr int kRollThreads = 256;
+}  // namespace
+
+// one workgroup per env: the observation row into the buffer, the Gaussian sample, its log-probability
+// (summed in action order by one lane), the clipped env action, value and episode start
+__global__ __launch_bounds__(kRollThreads) void k_rollout_store(RolloutArgs a) {
+    __shared__ float lp[kRollThreads];
+    const long long e = blockIdx.x;
+    const int tid = threadIdx.x;
+    const long long row = (long long)a.t * a.rows + e;
+    const float4* src = reinterpret_cast<const float4*>(a.obs_now + e * a.obs_dim);
+    float4* dst = reinterpret_cast<float4*>(a.obs + row * a.obs_dim);
+    for (int k = tid; k < a.obs_dim / 4; k += kRollThreads) dst[k] = src[k];
+    for (int k = tid; k < a.act_dim; k += kRollThreads) {
+        // standard normal from Philox4x32-10 (seed, step, env, action) by Box-Muller
+        uint32_t c[4] = {(uint32_t)a.t, (uint32_t)k, (uint32_t)e, (uint32_t)(e >> 32)};
+        philox_k(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+        const float u1 = ((float)(c[0] >> 8) + 1.0f) * (1.0f / 16777216.0f);   // (0, 1]
+        const float u2 = (float)(c[1] >> 8) * (1.0f / 16777216.0f);
+        const float eps = sqrtf(-2.0f * logf(u1)) * cosf(6.2831853071795865f * u2);
+        const float mu = a.mean[e * a.act_dim + k], ls = a.log_std[k], sd = expf(ls);
+        const float act = mu + sd * eps;
+        a.actions[row * a.act_dim + k] = act;
+        // torch.distributions.Normal.log_prob: -((x - mu)^2) / (2 var) - log(std) - log(sqrt(2 pi))
+        const float d = act - mu, var = sd * sd;
+        lp[k] = -(d * d) / (2.0f * var) - ls - 0.91893853320467274f;
+        if (k < a.env_act_dim) a.env_actions[e * a.env_act_dim + k] = fminf(fmaxf(act, -1.0f), 1.0f);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        float s = 0.0f;
+        for (int k = 0; k < a.act_dim; ++k) s += lp[k];
+        a.log_probs[row] = s;
+        a.values[row] = a.value[e];
+        a.episode_starts[row] = a.last_episode_starts[e];
+    }
+}
+
+// after the env step: reward (+ gamma V(terminal obs) for truncations), next episode start
+__global__ void k_rollout_post(RolloutArgs a) {
+    const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= a.rows) return;
+    const long long row = (long long)a.t * a.rows + e;
+    const bool te = a.terminated[e] != 0, tr = a.truncated[e] != 0;
+    float r = a.reward[e];
+    if (tr && !te && a.terminal_value) r += a.gamma * a.terminal_value[e];   // rewards[idx] += gamma * terminal_value
+    a.rewards[row] = r;
+    a.last_episode_starts[e] = (te || tr) ? 1.0f : 0.0f;
+}
+
+// RolloutBuffer.compute_returns_and_advantage, one env per thread, backwards over the buffer in float32
+__global__ void k_rollout_gae(RolloutArgs a) {
+    const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= a.rows) return;
+    const float g = a.gamma, gl = a.gamma_lambda;
+    float last = 0.0f;
+    for (int s = a.T - 1; s >= 0; --s) {
+        const long long row = (long long)s * a.rows + e;
+        float nnt, nv;
+        if (s == a.T - 1) { nnt = 1.0f - a.last_episode_starts[e]; nv = a.value[e]; }
+        else { nnt = 1.0f - a.episode_starts[row + a.rows]; nv = a.values[row + a.rows]; }
+        const float delta = (a.rewards[row] + (g * nv) * nnt) - a.values[row];
+        last = delta + (gl * nnt) * last;
+        a.advantages[row] = last;
+        a.returns[row] = last + a.values[row];
+    }
+}
+
+hipError_t launch_rollout(const RolloutArgs& a, int which, hipStream_t st) {
+    if (which == 0) hipLaunchKernelGGL(k_rollout_store, dim3((unsigned)a.rows), dim3(kRollThreads), 0, st, a);
+    else if (which == 1) hipLaunchKernelGGL(k_rollout_post, dim3((unsigned)((a.rows + 255) / 256)), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(k_rollout_gae, dim3((unsigned)((a.rows + 63) / 64)), dim3(64), 0, st, a);
+    return hipGetLastError();
+}
+
 }  // namespace ch

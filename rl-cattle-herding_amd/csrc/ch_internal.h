@@ -148,6 +148,19 @@ hipError_t launch_mlp(const MlpArgs& a, hipStream_t st);
 hipError_t launch_metrics_reduce(double* metrics, long long E, double* out, const int* err_word, double* err_out,
                                  int reset, hipStream_t st);
 
+// ch_aux.hip: the on-device PPO rollout buffer (ch_rollout_*)
+struct RolloutArgs {
+    int T, t, obs_dim, act_dim, env_act_dim;
+    long long rows;
+    unsigned long long seed;
+    float gamma, gamma_lambda;
+    const float *obs_now, *mean, *value, *log_std, *terminal_value, *reward;
+    const uint8_t *terminated, *truncated;
+    float *env_actions, *obs, *actions, *rewards, *episode_starts, *values, *log_probs, *advantages, *returns,
+        *last_episode_starts;
+};
+hipError_t launch_rollout(const RolloutArgs& a, int which, hipStream_t st);   // 0 store, 1 post, 2 gae
+
 template <class R> hipError_t launch_step(const StepParams<R>& p, int team, hipStream_t st);
 template <class R> hipError_t launch_reset(const StepParams<R>& p, int team, hipStream_t st);
 // launch = false only performs the once-per-device function-attribute opt-in (at ch_create, so that a

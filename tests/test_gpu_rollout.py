@@ -1,0 +1,89 @@
+"""GPU tests of the on-device PPO rollout buffer (cattleherd.rollout; ch_rollout_*), against plain torch
+/ NumPy restatements of SB3 2.7's collect_rollouts, DiagGaussianDistribution and
+compute_returns_and_advantage (SB3 is not installed: parity unpinned to its source; the reference's PPO
+setup is CTDECattleHerder.py:107-127).  Tolerances: log-probabilities 1e-5 relative (float32 sums in a
+different order than torch's), values / bootstrapped rewards 1e-5 (MFMA vs torch matmul), GAE 2e-6
+against the float32 NumPy recursion fed with the buffer's own rewards and values."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _gae_numpy(rewards, values, episode_starts, last_values, dones, gamma, lam):
+    """RolloutBuffer.compute_returns_and_advantage (float32 arrays, NumPy >= 2 scalar promotion)."""
+    T = rewards.shape[0]
+    adv = np.zeros_like(rewards)
+    last = np.zeros_like(rewards[0])
+    for step in reversed(range(T)):
+        if step == T - 1:
+            nnt = np.float32(1.0) - dones.astype(np.float32)
+            nv = last_values
+        else:
+            nnt = np.float32(1.0) - episode_starts[step + 1]
+            nv = values[step + 1]
+        delta = rewards[step] + gamma * nv * nnt - values[step]
+        last = delta + gamma * lam * nnt * last
+        adv[step] = last
+    return adv, adv + values
+
+
+def test_rollout_buffer_matches_sb3_semantics():
+    import torch
+    from cattleherd.env import HerdBatch
+    from cattleherd.policy import DevicePolicy
+    from cattleherd.rollout import DeviceRolloutBuffer
+    E, T, n, m = 512, 40, 4, 16
+    A = 4 * n                        # the CTDE action space is Box((NUM_DRONES, 4)), flattened by SB3
+    sc = 4800 - 30 + (np.arange(E) % 60)   # half the envs reach the 80 s time limit inside the rollout
+
+    def make():
+        bb = HerdBatch(E, n, m, mode="ctde", curriculum_level=2)
+        bb.reset()
+        bb.set_state({"step_counter": sc})
+        return bb
+    b = make()
+    actor = DevicePolicy(DevicePolicy.random_layers([12 * 86, 128, 128, A], seed=1), "tanh", None)
+    critic = DevicePolicy(DevicePolicy.random_layers([12 * 86, 128, 128, 1], seed=2), "tanh", None)
+    log_std = torch.full((A,), -1.0, device=b.device)
+    rb = DeviceRolloutBuffer(b, T)
+    assert rb.act_dim == A
+    rb.collect(actor, critic, log_std, seed=123)
+    torch.cuda.synchronize()
+    obs = rb.obs.cpu()
+    # 1. log-probabilities and values of the stored samples under the torch reference forward
+    mean = actor.reference(rb.obs.view(T * E, -1)).view(T, E, A)
+    std = torch.exp(log_std)
+    want_lp = torch.distributions.Normal(mean, std).log_prob(rb.actions).sum(-1)
+    assert torch.allclose(rb.log_probs, want_lp, rtol=1e-5, atol=1e-4)
+    want_v = critic.reference(rb.obs.view(T * E, -1)).view(T, E)
+    assert torch.allclose(rb.values, want_v, rtol=1e-5, atol=1e-5)
+    eps = (rb.actions - mean) / std
+    assert abs(float(eps.mean())) < 0.02 and abs(float(eps.std()) - 1.0) < 0.02   # standard normal noise
+    # 2. episode starts: first step all ones (after reset), then the previous step's dones
+    es = rb.episode_starts.cpu().numpy()
+    assert np.all(es[0] == 1.0)
+    # 3. the same rollout replayed step by step on a twin batch with the stored (clipped) actions
+    b2 = make()
+    rew, dn, tl = [], [], []
+    for t in range(T):
+        assert torch.equal(b2.obs.view(E, -1).cpu(), obs[t]), t
+        a = rb.actions[t].clamp(-1.0, 1.0).view(E, n, 4)
+        _, r, te, tr = b2.step(a, autoreset=True, terminal_obs=True)
+        tv = critic.reference(b2.terminal_obs.view(E, -1))[:, 0]
+        te, tr = te[:, 0].bool(), tr[:, 0].bool()
+        rr = r[:, 0].clone()
+        rr[tr & ~te] += 0.99 * tv[tr & ~te]
+        rew.append(rr.cpu().numpy()); dn.append((te | tr).cpu().numpy()); tl.append((tr & ~te).cpu().numpy())
+    rew, dn = np.array(rew), np.array(dn)
+    assert np.allclose(rb.rewards.cpu().numpy(), rew, rtol=1e-5, atol=1e-5)   # V(terminal) MFMA vs torch
+    assert np.array_equal(es[1:], dn[:-1].astype(np.float32))
+    assert dn.any() and np.array(tl).any()
+    # 4. GAE bit for bit against the float32 recursion
+    last_v = critic.reference(b2.obs.view(E, -1))[:, 0].cpu().numpy()
+    adv, ret = _gae_numpy(rb.rewards.cpu().numpy(), rb.values.cpu().numpy(), es, last_v, dn[-1],
+                          0.99, 0.95)
+    assert np.allclose(rb.advantages.cpu().numpy(), adv, rtol=2e-6, atol=2e-6)
+    assert np.allclose(rb.returns.cpu().numpy(), ret, rtol=2e-6, atol=2e-6)
+    b.close()
+    b2.close()
