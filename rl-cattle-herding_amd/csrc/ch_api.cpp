@@ -31,7 +31,7 @@ struct ch_handle {
     // step (it needs them for the observation anyway) and read by the next one instead of
     // recomputing atan2/asin/atan2; any other writer of the state clears rpy_valid.
     void* rpy = nullptr;
-    int* ctl = nullptr;   // device [4]: StepParams::ctl (Euler cache stale, obs bytes unknown, v2 done count)
+    uint8_t* stale = nullptr;   // device [2][E]: StepParams::stale (Euler cache stale, obs bytes unknown, per env)
     void* cattle = nullptr;
     void* phys = nullptr;   // [kPhysComps][E][NC]: last_clipped_action, DYN rpy_rates
     void* envr = nullptr;
@@ -50,6 +50,7 @@ struct ch_handle {
     long long* tstamp = nullptr;
     int G = 1, block = 64, P = 0;
     bool pw = false;   // v2 with per-wave env tables (herds of kPwMinCattle cows and more)
+    bool sep = false;  // v2 shared tables with the shepherd terms in their own LDS region
     size_t lds = 0;
     uint16_t* pairs = nullptr;
     int* errw = nullptr;        // device error word (CH_DEVERR_* bits), sticky
@@ -158,11 +159,11 @@ static StepParams<R> params(ch_handle* h) {
     p.k0 = (uint32_t)c.seed; p.k1 = (uint32_t)(c.seed >> 32);
     p.env_off = c.env_id_offset;
     p.cs_cc = cattle_spacing_cc();
-    p.drone = (R*)h->drone; p.rpy = (R*)h->rpy; p.ctl = h->ctl; p.cattle = (R*)h->cattle; p.envr = (R*)h->envr; p.envi = h->envi;
+    p.drone = (R*)h->drone; p.rpy = (R*)h->rpy; p.stale = h->stale; p.cattle = (R*)h->cattle; p.envr = (R*)h->envr; p.envi = h->envi;
     p.metrics = h->metrics; p.spawn = h->spawn; p.n_scen = h->n_scen; p.n_cows = h->n_cows;
     p.debug = h->debug;
     p.phase_mask = h->phase_mask;
-    p.G = h->G; p.P = h->P; p.pairs = h->pairs; p.pw = h->pw;
+    p.G = h->G; p.P = h->P; p.pairs = h->pairs; p.pw = h->pw; p.sep = h->sep;
     p.tstamp = h->tstamp;
     p.physics = c.physics; p.gnd_h_clip = gnd_eff_h_clip(); p.phys = (R*)h->phys;
     p.err = h->errw;
@@ -225,7 +226,7 @@ const char* ch_last_error(const ch_handle* h) { return h ? h->err.c_str() : g_cr
 
 static void free_all(ch_handle* h) {
     void* ptrs[] = {h->drone, h->rpy, h->cattle, h->phys, h->envr, h->envi, h->metrics, h->spawn, h->pairs,
-                    h->errw, h->mdev, h->ctl, h->evald, h->rdn, h->rdv};
+                    h->errw, h->mdev, h->stale, h->evald, h->rdn, h->rdv};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (h->mhost) (void)hipHostFree(h->mhost);
@@ -317,9 +318,8 @@ int ch_create(const ch_config* c, int64_t n_envs, int32_t device, ch_handle** ou
     CTRY(hipMalloc(&h->envi, sizeof(int) * kEnvInt * E));
     CTRY(hipMalloc(&h->metrics, sizeof(double) * kMetricRows * E));
     {
-        const int ctl0[4] = {1, 1, 0, 0};   // no Euler cache yet; obs bytes unknown
-        CTRY(hipMalloc(&h->ctl, sizeof(ctl0)));
-        CTRY(hipMemcpy(h->ctl, ctl0, sizeof(ctl0), hipMemcpyHostToDevice));
+        CTRY(hipMalloc(&h->stale, 2 * (size_t)E));
+        CTRY(hipMemset(h->stale, 1, 2 * (size_t)E));   // no Euler cache yet; obs bytes unknown
     }
     if (c->eval_metrics) {
         CTRY(hipMalloc(&h->evald, sizeof(double) * E * h->NC));
@@ -386,6 +386,12 @@ int ch_create(const ch_config* c, int64_t n_envs, int32_t device, ch_handle** ou
                     break;
                 }
             }
+        }
+        // shared tables: the shepherd terms in their own region when it fits, so they need not wait for every
+        // alpha row to have read the pair table
+        if (!h->pw) {
+            const size_t l = V2Layout(h->G, h->NC, h->M, h->P, c->mode, (int)h->rsize, 0, true).bytes();
+            if (l <= budget) { h->sep = true; h->lds = l; }
         }
         if (h->lds > budget) h->kernel = 1;   // one env's pair table alone exceeds the budget
         std::vector<uint16_t> pl((size_t)std::max(h->P, 1));
@@ -583,10 +589,8 @@ int ch_set_state(ch_handle* h, const double* hd, const int32_t* hi, void* stream
     hipStream_t st = (hipStream_t)stream;
     HIP_TRY(h, hipStreamSynchronize(st));
     h->obs_zero_ptr = nullptr;   // NUM_DRONES may change: the next step writes every obs block in full
-    {   // the same on the device, for steps replayed from a graph captured earlier
-        const int ctl[2] = {1, 1};
-        HIP_TRY(h, hipMemcpy(h->ctl, ctl, sizeof(ctl), hipMemcpyHostToDevice));
-    }
+    // the same on the device, for steps replayed from a graph captured earlier
+    HIP_TRY(h, hipMemset(h->stale, 1, 2 * (size_t)h->E));
     const size_t nd = (size_t)kDroneComps * h->E * h->NC, nc = (size_t)kCattleComps * h->E * h->M,
                  nr = (size_t)kEnvReal * h->E, np_ = (size_t)kPhysComps * h->E * h->NC;
     if (hd) {
@@ -636,9 +640,14 @@ int ch__set_geometry(ch_handle* h, int32_t G, int32_t block) {
         block > ((h->pw || h->cfg.physics != CH_PHYS_PYB) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK))
         return CH_ERR_INVALID;
     if (G * h->M > 3 * (block - 64)) return CH_ERR_UNSUPPORTED;   // the cow waves prefetch <= 3 spawn slots per lane
-    const size_t lds = V2Layout(G, h->NC, h->M, h->P, h->cfg.mode, (int)h->rsize, h->pw ? block / 64 - 1 : 0).bytes();
+    size_t lds = V2Layout(G, h->NC, h->M, h->P, h->cfg.mode, (int)h->rsize, h->pw ? block / 64 - 1 : 0).bytes();
     if (lds > 160 * 1024) return CH_ERR_UNSUPPORTED;
-    h->G = G; h->block = block; h->lds = lds;
+    bool sep = false;
+    if (!h->pw) {
+        const size_t l = V2Layout(G, h->NC, h->M, h->P, h->cfg.mode, (int)h->rsize, 0, true).bytes();
+        if (l <= 160 * 1024) { sep = true; lds = l; }
+    }
+    h->G = G; h->block = block; h->lds = lds; h->sep = sep;
     HIP_TRY(h, prepare_step(h));
     return CH_OK;
 }
@@ -659,9 +668,9 @@ int ch__geometry(const ch_handle* h, int32_t* G, int32_t* block, int64_t* lds, i
 int ch__obs_invalidate(ch_handle* h, void* stream) {
     if (!h) return CH_ERR_INVALID;
     h->obs_zero_ptr = nullptr;
-    // and on the device (ctl[1]), for steps replayed from a graph captured before this call
+    // and on the device (stale row 1), for steps replayed from a graph captured before this call
     HIP_TRY(h, hipSetDevice(h->device));
-    HIP_TRY(h, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(h->ctl + 1), 1, 1, (hipStream_t)stream));
+    HIP_TRY(h, hipMemsetAsync(h->stale + h->E, 1, (size_t)h->E, (hipStream_t)stream));
     return CH_OK;
 }
 

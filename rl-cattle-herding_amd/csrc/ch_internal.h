@@ -27,11 +27,12 @@ struct StepParams {
     long long env_off;
     double cs_cc;   // CattleSpacingRewardFunction continuation constant (host-evaluated)
     R* drone;       // [22][E][NC]
-    R* rpy;         // v2: [3][E][NC] Euler angles of the stored quaternion (valid unless ctl[0])
+    R* rpy;         // v2: [3][E][NC] Euler angles of the stored quaternion (valid unless stale[e])
     // device control words of the handle, read by the v2 step at its start (so a captured HIP graph
     // sees state changes made after capture): [0] the Euler cache is stale, [1] the constant-zero
     // observation bytes are unknown, [2] v2 workgroups finished (the last one clears [0] and [1])
-    int* ctl;
+    uint8_t* stale; // [2][E] per env: row 0 the Euler cache is stale, row 1 the obs block's constant bytes are
+                    // unknown; set by every other writer (v1, ch_reset, ch_set_state, invalidate), cleared by the v2 step
     R* cattle;      // [4][E][M]
     R* envr;        // [2][E]
     int* envi;      // [10][E]
@@ -60,6 +61,7 @@ struct StepParams {
     R* phys;                  // [kPhysComps][E][NC]
     int* err;                 // device error word of the handle (CH_DEVERR_* bits), read by ch_sync & co.
     int pw;                   // v2: per-wave env tables (V2Layout W = block / 64 - 1)
+    int sep;                  // v2 shared tables: separate shepherd-term region (V2Layout sep)
     double* evald;            // optional [E][NC]: update_evaluation_metrics' per-drone episode distance
     const int* reset_n;       // optional (ch_reset_with): NUM_DRONES of each reset env instead of the Philox draw
     const double* reset_vel;  // optional (ch_reset_with): [E][M][2] cattle spawn velocities instead of Philox
@@ -86,30 +88,32 @@ struct Level {
 #ifndef CH_V2_MAX_BLOCK_PW
 #define CH_V2_MAX_BLOCK_PW 512   // per-wave-table and physics-variant kernels: 8 waves (their register use allows 2 per SIMD)
 #endif
-constexpr int kV2EnvInts = 13;
-constexpr int kV2Flags = 20;         // LDS hand-off counters between the drone wave and the cow waves + work counters
+constexpr int kV2EnvInts = 14;
+constexpr int kV2Flags = 24;         // LDS hand-off counters between the drone wave and the cow waves + work counters
 // W = 0: one alpha pair table for the whole workgroup (4 reals per pair, G*P pairs), reused for the
 // shepherd terms.  W > 0 ("per-wave env tables", large herds): each of the W cow waves owns a slot for
 // ONE env at a time -- 3 reals per pair (gradient x, y and the bump; the consensus term is recomputed
 // from the velocities when the rows are summed), reused for that env's shepherd terms -- so the LDS
 // no longer grows with G*P and a whole CU's envs fit in one workgroup.
 struct V2Layout {
-    enum { CX = 0, DRONE, DCOW, ENVR, PAIRS, MET, IMG, EI, LEVELS, PAIRL, BYTES, NOFF };
+    enum { CX = 0, DRONE, DCOW, ENVR, PAIRS, TD, MET, IMG, EI, LEVELS, PAIRL, BYTES, NOFF };
     int G, N, M, P, rows, W;
+    bool sep;      // shared tables: the shepherd terms in a region of their own (not reusing the pair table)
     size_t slot;   // W > 0: reals per wave slot
     size_t off[NOFF + 1];
     static __host__ __device__ size_t al(size_t x) { return (x + 15) & ~size_t(15); }
-    __host__ __device__ V2Layout(int G_, int N_, int M_, int P_, int mode, int rb, int W_ = 0)
-        : G(G_), N(N_), M(M_), P(P_), W(W_) {
+    __host__ __device__ V2Layout(int G_, int N_, int M_, int P_, int mode, int rb, int W_ = 0, bool sep_ = false)
+        : G(G_), N(N_), M(M_), P(P_), W(W_), sep(W_ == 0 && sep_) {
         rows = mode == CH_MODE_CTDE ? 12 : N;
         slot = 3 * (size_t)P > 6 * (size_t)M * N ? 3 * (size_t)P : 6 * (size_t)M * N;
-        const size_t shared = 4 * (size_t)G * P > 6 * (size_t)G * M * N ? 4 * (size_t)G * P : 6 * (size_t)G * M * N;
+        const size_t shared = (sep || 4 * (size_t)G * P > 6 * (size_t)G * M * N) ? 4 * (size_t)G * P : 6 * (size_t)G * M * N;
         size_t o = 0;
         off[CX] = o;     o = al(o + 8 * (size_t)G * M * rb);         // cx cy cvx cvy aux auy spx spy
-        off[DRONE] = o;  o = al(o + 14 * (size_t)G * N * rb);        // dx dy dz pa pb sa sb ca cb scat psp mrew mq meor
+        off[DRONE] = o;  o = al(o + 18 * (size_t)G * N * rb);        // dx dy dz pa pb sa sb ca cb scat psp mrew mq meor q[4]
         off[DCOW] = o;   o = al(o + (size_t)G * N * M * rb);         // cow-drone distances
         off[ENVR] = o;   o = al(o + 4 * (size_t)G * rb);             // prev clock, herd centroid x y
         off[PAIRS] = o;  o = al(o + (W ? (size_t)W * slot : shared) * rb);   // alpha pair table(s), then shepherd terms
+        off[TD] = o;     o = al(o + (sep ? 6 * (size_t)G * M * N * rb + 4 * (size_t)G * M : 0));   // sep: terms, per-cow counts
         off[MET] = o;    o = al(o + (size_t)kMetricRows * G * 8);
         off[IMG] = o;                                                // (observations go straight to HBM)
         off[EI] = o;     o = al(o + ((size_t)kV2EnvInts * G + 2 * G + 2 + kV2Flags) * 4);   // + flock/reset lists

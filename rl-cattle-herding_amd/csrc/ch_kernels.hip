@@ -545,10 +545,8 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
     // ---- observation + scalars back to HBM --------------------------------------------------
     const bool write = valid && (!RESET_ONLY || do_reset);
     if (write && !(p.phase_mask & 8)) write_obs(p.obs + (long long)e * p.rows * 86, p.rows, S, t, m_obs, cat_off);
-    // this kernel does not keep the Euler-angle cache of the v2 step: mark it stale (every block
-    // stores the same word; the v2 step reads it at its start)
-    if (threadIdx.x == 0 && p.ctl) p.ctl[0] = 1;
     if (write && t == 0) {
+        if (p.stale) p.stale[e] = 1;   // this kernel does not keep the v2 step's Euler-angle cache
         p.envi[0 * E + e] = n; p.envi[1 * E + e] = sc; p.envi[2 * E + e] = scA; p.envi[3 * E + e] = has_prev;
         p.envi[4 * E + e] = level; p.envi[5 * E + e] = tally; p.envi[6 * E + e] = spawn; p.envi[7 * E + e] = active;
         p.envi[8 * E + e] = episode;

@@ -33,11 +33,14 @@ namespace ch {
 
 // per-env integer scalars kept in LDS (index I * G + g)
 enum { I_N = 0, I_SC, I_SCA, I_HASPREV, I_LEVEL, I_TALLY, I_SPAWN, I_ACTIVE, I_EPISODE, I_FLOCK, I_RESET, I_NEWN,
-       I_HERD, I_COUNT };
+       I_HERD, I_OBSD, I_COUNT };
 static_assert(I_COUNT == kV2EnvInts, "LDS env-int rows");
-enum { F_D = 0, F_T, F_H, F_A, F_E, F_R, F_X0, F_X1, F_X2,     // hand-off counters
+enum { F_D = 0, F_T, F_H, F_A, F_E, F_R, F_X0, F_X1, F_X2,     // hand-off counters (F_H counts finished items)
        C_PAIRS, C_ROWS, C_COWS, C_FLOCK, C_DELTA, F_W, F_Q,      // work counters (grab), cow-wave syncs
-       Q_LEN, C_QUEUE, F_C };                                     // shared alpha queue: length, grab, cheap pass done
+       Q_LEN, C_QUEUE, F_C,                                       // shared alpha queue: length, grab, cheap pass done
+       C_EULER,                                                   // Euler angles of the new attitudes (cow waves)
+       FLAG_COUNT };
+static_assert(FLAG_COUNT <= kV2Flags, "LDS flag words");
 // after the per-env rows: flocking-env list [G], reset-env list [G], their counts, then the counters
 #define FL_LIST (I_COUNT * G)
 #define RS_LIST (I_COUNT * G + G)
@@ -130,10 +133,12 @@ struct V2Smem {
     R *pa, *pb, *sa, *sb, *ca, *cb, *scat, *psp;     // [G*N] per-drone reward terms
     R* mrew;                                         // [G*N] MARL per-agent reward scratch
     R *mq, *meor;                                    // [G*N] MARL: reward without the approach term, end-of-episode bonus
-    R* dcow;                                         // [G*N*M] cow-drone distances, (g*N + k)*M + j
+    R* dq;                                           // [4][G*N] drone attitude after physics (for the Euler angles)
+    R* dcow;                                         // [G*N*M] squared cow-drone distances, (g*N + k)*M + j
     R *prev, *clock, *hcx, *hcy;                     // [G] env reals; herd centroid (cow waves)
     R *tgx, *tgy, *tcx, *tcy;                        // [G*P] alpha pair table
-    R* td;                                           // [6][G*M*N] shepherd/predator terms (reuses the pair table)
+    R* td;                                           // [6][G*M*N] shepherd/predator terms (the pair table's space unless sep)
+    int* cnt;                                        // sep: [G*M] per-cow arrivals (alpha row 1, shepherd terms N)
     double* met;                                     // [kMetricRows*G]
     int* ei;                                         // [I_COUNT*G] + list [G] + 2 + flags
     int* flags;
@@ -151,12 +156,13 @@ struct V2Smem {
         spx = auy + GM; spy = spx + GM;
         dx = (R*)(base + L.off[V2Layout::DRONE]); dy = dx + GN; dz = dy + GN;
         pa = dz + GN; pb = pa + GN; sa = pb + GN; sb = sa + GN; ca = sb + GN; cb = ca + GN; scat = cb + GN;
-        psp = scat + GN; mrew = psp + GN; mq = mrew + GN; meor = mq + GN;
+        psp = scat + GN; mrew = psp + GN; mq = mrew + GN; meor = mq + GN; dq = meor + GN;
         dcow = (R*)(base + L.off[V2Layout::DCOW]);
         prev = (R*)(base + L.off[V2Layout::ENVR]); clock = prev + L.G; hcx = clock + L.G; hcy = hcx + L.G;
         pl = (const uint16_t*)(base + L.off[V2Layout::PAIRL]);
         tgx = (R*)(base + L.off[V2Layout::PAIRS]); tgy = tgx + GP; tcx = tgy + GP; tcy = tcx + GP;
-        td = tgx;
+        td = L.sep ? (R*)(base + L.off[V2Layout::TD]) : tgx;
+        cnt = (int*)(base + L.off[V2Layout::TD] + 6 * (size_t)L.G * L.M * L.N * sizeof(R));
         met = (double*)(base + L.off[V2Layout::MET]);
         ei = (int*)(base + L.off[V2Layout::EI]);
         flags = ei + I_COUNT * L.G + 2 * L.G + 2;
@@ -177,8 +183,23 @@ struct V2Smem {
 // (drone wave, after the reward terms), cattle offsets (cow waves, after the distance table), and the
 // always-zero bytes (cow waves, during the alpha phase).  `eb` is the env's block (row 0, col 0); 86 is
 // even, so every float2 below is 8-byte aligned.
-#ifndef CH_NO_NT_STORES
-#define CH_ST(ptr, val) __builtin_nontemporal_store((val), (ptr))   // streaming: fewer dirty L2 lines at the kernel-end release
+#if !defined(CH_NT_STORES) && !defined(CH_NO_NT_STORES)
+// Write-through stores (an agent-scope relaxed atomic store is a global_store ... sc1): the lines leave the
+// XCD's L2 while the kernel runs instead of in the kernel-end write-back, which the next launch waits for.
+// Measured at C4 (tools/gpu_ab_store.sh): inter-kernel gap 2.6 -> 1.75 us, 164 -> 171 M env-steps/s;
+// non-temporal (nt, CH_NT_STORES) and plain stores both leave the lines dirty in L2.
+template <class T> __device__ __forceinline__ void ch_st_wt(T* ptr, T v) {
+    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "4- or 8-byte stores");
+    if constexpr (sizeof(T) == 8)
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(ptr), __builtin_bit_cast(unsigned long long, v),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        __hip_atomic_store(reinterpret_cast<unsigned*>(ptr), __builtin_bit_cast(unsigned, v), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+#define CH_ST(ptr, val) ch_st_wt((ptr), static_cast<std::remove_pointer_t<decltype(ptr)>>(val))
+#elif defined(CH_NT_STORES)
+#define CH_ST(ptr, val) __builtin_nontemporal_store((val), (ptr))
 #else
 #define CH_ST(ptr, val) (*(ptr) = (val))
 #endif
@@ -197,6 +218,23 @@ __device__ __forceinline__ void obs_own(float* eb, int row, R z, const R rpy[3],
     st2(eb, o + 4, (float)v[0], (float)v[1]);
     st2(eb, o + 6, (float)v[2], (float)w[0]);
     st2(eb, o + 8, (float)w[1], (float)w[2]);
+}
+
+// the own-state row but its Euler angles (drone wave), and the Euler angles (cow waves, from the published
+// attitude): the same entries obs_own writes
+template <class R>
+__device__ __forceinline__ void obs_own_nrpy(float* eb, int row, R z, const R v[3], const R w[3]) {
+    const int o = row * 86;
+    CH_ST(eb + o, (float)z);
+    st2(eb, o + 4, (float)v[0], (float)v[1]);
+    st2(eb, o + 6, (float)v[2], (float)w[0]);
+    st2(eb, o + 8, (float)w[1], (float)w[2]);
+}
+template <class R>
+__device__ __forceinline__ void obs_rpy(float* eb, int row, const R rpy[3]) {
+    const int o = row * 86;
+    CH_ST(eb + o + 1, (float)rpy[0]);
+    st2(eb, o + 2, (float)rpy[1], (float)rpy[2]);
 }
 
 // nearest-neighbour entries (columns 10..13) of drone i from its two nearest drones i1, i2
@@ -322,13 +360,26 @@ __device__ __forceinline__ void alpha_row(V2Smem<R>& S, int M, int P, int u, int
     const R C2A = R(2 * 1.7320508075688772);
     R gx = 0, gy = 0, cxx = 0, cyy = 0, ux = 0, uy = 0;
     const int pb = g * P;
-    for (unsigned long long m = S.nbm[u]; m; m &= m - 1) {
-        const int k = __ffsll((long long)m) - 1;
-        const bool fwd = j < k;
-        const int idx = pb + (fwd ? tri(j, k, M) : tri(k, j, M));
-        const R tgx = S.tgx[idx], tgy = S.tgy[idx], tcx = S.tcx[idx], tcy = S.tcy[idx];
-        gx += fwd ? tgx : -tgx; gy += fwd ? tgy : -tgy;
-        cxx += fwd ? tcx : -tcx; cyy += fwd ? tcy : -tcy;
+    // four neighbours per round: their table loads are issued together, then summed in neighbour order
+    for (unsigned long long m = S.nbm[u]; m;) {
+        R t[4][4];
+        bool v[4], fwd[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            v[r] = m != 0;
+            const int k = v[r] ? __ffsll((long long)m) - 1 : j + 1;
+            m &= m - 1;
+            fwd[r] = j < k;
+            const int idx = pb + (fwd[r] ? tri(j, k, M) : tri(k, j, M));
+            t[r][0] = t[r][1] = t[r][2] = t[r][3] = R(0);
+            if (v[r]) { t[r][0] = S.tgx[idx]; t[r][1] = S.tgy[idx]; t[r][2] = S.tcx[idx]; t[r][3] = S.tcy[idx]; }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            if (!v[r]) break;
+            gx += fwd[r] ? t[r][0] : -t[r][0]; gy += fwd[r] ? t[r][1] : -t[r][1];
+            cxx += fwd[r] ? t[r][2] : -t[r][2]; cyy += fwd[r] ? t[r][3] : -t[r][3];
+        }
     }
     if (S.hasnb[u]) { ux = C2A * gx + C2A * cxx; uy = C2A * gy + C2A * cyy; }
     S.aux[u] = ux; S.auy[u] = uy;
@@ -396,16 +447,32 @@ __device__ __forceinline__ void alpha_row_pw(V2Smem<R>& S, int M, int P, int g, 
     const int u = g * M + j;
     R gx = 0, gy = 0, cxx = 0, cyy = 0, ux = 0, uy = 0;
     const R pjx = S.cvx[u], pjy = S.cvy[u];
-    for (unsigned long long m = S.nbm[u]; m; m &= m - 1) {
-        const int k = __ffsll((long long)m) - 1;
-        const bool fwd = j < k;
-        const int idx = fwd ? tri(j, k, M) : tri(k, j, M);
-        const R tgx = tb[idx], tgy = tb[P + idx], b = tb[2 * P + idx];
-        const R pkx = S.cvx[g * M + k], pky = S.cvy[g * M + k];
-        const R dvx = fwd ? pkx - pjx : pjx - pkx, dvy = fwd ? pky - pjy : pjy - pky;
-        const R tcx = b * dvx, tcy = b * dvy;
-        gx += fwd ? tgx : -tgx; gy += fwd ? tgy : -tgy;
-        cxx += fwd ? tcx : -tcx; cyy += fwd ? tcy : -tcy;
+    // four neighbours per round: their loads are issued together, then summed in neighbour order
+    for (unsigned long long m = S.nbm[u]; m;) {
+        R t[4][5];
+        bool v[4], fwd[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            v[r] = m != 0;
+            const int k = v[r] ? __ffsll((long long)m) - 1 : j + 1;
+            m &= m - 1;
+            fwd[r] = j < k;
+            const int idx = fwd[r] ? tri(j, k, M) : tri(k, j, M);
+            t[r][0] = t[r][1] = t[r][2] = t[r][3] = t[r][4] = R(0);
+            if (v[r]) {
+                t[r][0] = tb[idx]; t[r][1] = tb[P + idx]; t[r][2] = tb[2 * P + idx];
+                t[r][3] = S.cvx[g * M + k]; t[r][4] = S.cvy[g * M + k];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            if (!v[r]) break;
+            const R b = t[r][2], pkx = t[r][3], pky = t[r][4];
+            const R dvx = fwd[r] ? pkx - pjx : pjx - pkx, dvy = fwd[r] ? pky - pjy : pjy - pky;
+            const R tcx = b * dvx, tcy = b * dvy;
+            gx += fwd[r] ? t[r][0] : -t[r][0]; gy += fwd[r] ? t[r][1] : -t[r][1];
+            cxx += fwd[r] ? tcx : -tcx; cyy += fwd[r] ? tcy : -tcy;
+        }
     }
     if (S.hasnb[u]) { ux = C2A * gx + C2A * cxx; uy = C2A * gy + C2A * cyy; }
     S.aux[u] = ux; S.auy[u] = uy;
@@ -489,7 +556,8 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
     constexpr bool marl = MODE == 1;
     const int G = GT ? GT : p.G, N = NT ? NT : p.NC, M = MT ? MT : p.M, P = MT ? MT * (MT - 1) / 2 : p.P;
     const int rows = marl ? N : 12;
-    const V2Layout L(G, N, M, P, MODE, (int)sizeof(R), PW ? (int)(blockDim.x >> 6) - 1 : 0);
+    const V2Layout L(G, N, M, P, MODE, (int)sizeof(R), PW ? (int)(blockDim.x >> 6) - 1 : 0, !PW && p.sep);
+    const bool sep = L.sep;
     V2Smem<R> S(smem, L);
     const int BS = blockDim.x, tid = threadIdx.x;
     const int e0 = blockIdx.x * G;
@@ -519,12 +587,12 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
     R spx_r[3] = {0, 0, 0}, spy_r[3] = {0, 0, 0};   // cow waves: prefetched spawn positions
     bool rpy_valid = false;
     if (tid < 64) {
-        rpy_valid = p.ctl[0] == 0;
         // the drone wave loads only what its chain reads, so the chain starts after one round trip; the
         // cow waves stage the env scalars, the curriculum table and the pair list meanwhile
         __builtin_amdgcn_s_setprio(3);   // the drone wave is the critical path: it wins issue on a shared SIMD
         if (dlane) {
             n0 = p.envi[0 * E + e0 + dg];
+            rpy_valid = p.stale[e0 + dg] == 0;   // this env's Euler cache (written by the last v2 step)
             if (marl) act0 = p.envi[7 * E + e0 + dg];
             pos[0] = p.drone[0 * DS + di]; pos[1] = p.drone[1 * DS + di]; pos[2] = p.drone[2 * DS + di];
 #pragma unroll
@@ -534,7 +602,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
 #pragma unroll
             for (int c = 0; c < 9; ++c) pid[c] = p.drone[(13 + c) * DS + di];
             // Euler angles of this quaternion, stored by the previous step (used iff the cache is
-            // valid; loaded regardless so the loads issue with the state's, not after ctl returns)
+            // valid; loaded regardless so the loads issue with the state's, not after the stale flag returns)
 #pragma unroll
             for (int c = 0; c < 3; ++c) rpy_in[c] = p.rpy[c * DS + di];
             stepi = p.envi[9 * E + e0 + dg];   // ch_step calls on this env so far: the Philox action counter
@@ -562,7 +630,10 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         for (int k = ct; k < (int)(sizeof(kLevels) / 4); k += CW)
             reinterpret_cast<uint32_t*>(S.LT)[k] = reinterpret_cast<const uint32_t*>(kLevels)[k];
         for (int k = ct; k < P; k += CW) const_cast<uint16_t*>(S.pl)[k] = p.pairs[k];
-        for (int k = ct; k < G * M; k += CW) { S.hasnb[k] = 0; S.nbm[k] = 0; }
+        for (int k = ct; k < G * M; k += CW) {
+            S.hasnb[k] = 0; S.nbm[k] = 0;
+            if (sep) S.cnt[k] = 0;
+        }
         if (ct < 64) {   // the first cow wave: env scalars, one env per lane
         const int g = ct;
         bool flk = false;
@@ -575,6 +646,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             ei[I_TALLY * G + g] = p.envi[5 * E + e]; ei[I_SPAWN * G + g] = p.envi[6 * E + e];
             ei[I_ACTIVE * G + g] = p.envi[7 * E + e]; ei[I_EPISODE * G + g] = p.envi[8 * E + e];
             ei[I_FLOCK * G + g] = flk; ei[I_RESET * G + g] = 0; ei[I_HERD * G + g] = 0;
+            ei[I_OBSD * G + g] = p.stale[E + e];   // the obs block's constant bytes are unknown
             S.prev[g] = p.envr[e]; S.clock[g] = p.envr[E + e];
 #pragma unroll
             for (int r = 0; r < kMetricRows; ++r) S.met[r * G + g] = p.metrics[r * E + e];
@@ -613,7 +685,6 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         // ============ drone wave: the critical path ============================================
         const int n = dlane ? n0 : 0;
         const bool live = dlane && dk < n;
-        R rpy_out[3] = {0, 0, 0};
         R px0 = 0, py0 = 0;
         if (live) {
             px0 = pos[0]; py0 = pos[1];
@@ -658,19 +729,16 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
 #pragma unroll
             for (int c = 0; c < 9; ++c) CH_ST(&D[(13 + c) * DS + di], pid[c]);
             S.dx[tid] = pos[0]; S.dy[tid] = pos[1]; S.dz[tid] = pos[2];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) S.dq[c * (G * N) + tid] = q[c];
         }
         wave_sync();
         lds_signal(fl + F_D);   // positions published: the cow waves' distance work starts now
-        // the Euler angles (obs row, next step's PID cache) are only the drone wave's: after the hand-off
-        if (live) {
-            quat_to_euler(q, rpy_out);
-#pragma unroll
-            for (int c = 0; c < 3; ++c) CH_ST(&p.rpy[c * DS + di], rpy_out[c]);
-        }
-        if (live && wobs) obs_own(obs_wg + dg * RW, dk, pos[2], rpy_out, v, w);
+        // the own-state row but its Euler angles, which a cow wave computes from S.dq (obs_euler)
+        if (live && wobs) obs_own_nrpy(obs_wg + dg * RW, dk, pos[2], v, w);
         if (tid == 0) TS(4, (long long)clock64());
         lds_wait(fl + F_E, W1, p.err);   // env scalars and the curriculum table (staged by the cow waves)
-        if (p.evald && live) p.evald[di] = eval_distance_step(ev_acc, ei[I_SC * G + dg] == 0, px0, py0, pos[0], pos[1]);
+        if (p.evald && live) CH_ST(&p.evald[di], eval_distance_step(ev_acc, ei[I_SC * G + dg] == 0, px0, py0, pos[0], pos[1]));
 
         // per-drone reward terms (CattleAviary.py:230-246, 572-679) and neighbour obs (BaseRLAviary.py:303-317)
         if (live && task) {
@@ -705,16 +773,20 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         }
         lds_signal(fl + F_T);
         if (tid == 0) TS(5, (long long)clock64());
-        lds_wait(fl + F_H, W1 + ((p.phase_mask & CH_PHASE_FORCE_TIMEOUT) ? 1 : 0), p.err);
+        // every cow item (distances, winding, cattle obs) and herd centroid done
+        lds_wait(fl + F_H, Gv * M + Gv + ((p.phase_mask & CH_PHASE_FORCE_TIMEOUT) ? 1 : 0), p.err);
         if (tid == 0) TS(6, (long long)clock64());
         if (live && task) {
             // closest cow (CattleAviary.py:248-252) from the cow waves' distance table -> cattle term
+            // min over cows of |y - q|^2, then one square root: sqrt is correctly rounded and monotonic, so
+            // this is the minimum of the distances (a NaN entry is skipped either way)
             const R* dc = S.dcow + tid * M;
             R best = R(INFINITY);
             CH_UNROLL for (int j = 0; j < M; ++j) {
                 const R d = dc[j];
                 if (d < best) best = d;
             }
+            best = sqrt(best);
             S.scat[tid] = cattle_spacing(best, R(p.cs_cc));
             if constexpr (marl) {
                 // MARLCattleAviary._computeReward's per-agent part at the step's starting level
@@ -943,7 +1015,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                                 if (trr) rr -= R(50);
                                 done = 0;
                             }
-                            p.reward[(long long)e * N + i] = (float)rr;
+                            CH_ST(&p.reward[(long long)e * N + i], (float)rr);
                             p.term[(long long)e * N + i] = 0;
                             p.trunc[(long long)e * N + i] = trr;
                             if (i < n && rr == rr) ret += (double)rr;
@@ -977,7 +1049,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                                 tt = term_call_L(Lc, level, clock, inc, ms, cent, eff);
                                 trr = trunc_i(i, time_up_w);
                             }
-                            p.reward[(long long)e * N + i] = (float)rr;
+                            CH_ST(&p.reward[(long long)e * N + i], (float)rr);
                             p.term[(long long)e * N + i] = tt;
                             p.trunc[(long long)e * N + i] = trr;
                             if (i < n && rr == rr) ret += (double)rr;
@@ -997,7 +1069,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                                 trr = trunc_i(i, time_up);
                                 done &= tt;
                             }
-                            p.reward[(long long)e * N + i] = (float)rr;
+                            CH_ST(&p.reward[(long long)e * N + i], (float)rr);
                             p.term[(long long)e * N + i] = tt;
                             p.trunc[(long long)e * N + i] = trr;
                             if (i < n && rr == rr) ret += (double)rr;
@@ -1048,7 +1120,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                 R tot = 0;
                 CH_UNROLL for (int i = 0; i < N; ++i) tot += i < n ? rg + R(0.5) * ((psp_i[i] - msp) + (scat_i[i] - mcat)) : R(0);
                 R rew = divc(tot, nn);
-                p.reward[e] = (float)rew;
+                CH_ST(&p.reward[e], (float)rew);
                 p.term[e] = te2; p.trunc[e] = tr;
                 ret = (double)rew;
                 n_term = te2; n_trunc = tr; n_nan = rew != rew;
@@ -1102,6 +1174,16 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         // one unit of PW alpha work (a cheap-pass chunk or an expensive-pass wave of queued pairs, plus the
         // env's rows after its last unit); false when no flocking env is left.  The state is wave-uniform
         // (grab is readfirstlane'd, the queue length a ballot count).
+        // sep: one of a cow's inputs to its velocity update is complete -- its alpha row (weight 1) or shepherd
+        // terms (weight N in total); the arrival that completes the count N + 1 runs the update
+        auto arrive = [&](int u, int g, int w) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+            const int old = __hip_atomic_fetch_add(&S.cnt[u], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (old + w == N + 1) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+                flock_combine(p, S, N, M, e0, u, ei[I_N * G + g], S.td, S.tdf, u * N, G * M * N);
+            }
+        };
         auto alpha_step = [&]() -> bool {
             if (f_cur < 0) {
                 f_cur = grab(fl + C_PAIRS, 1);
@@ -1145,8 +1227,9 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         }
         // the constant-zero bytes of the observation blocks, when the host cannot vouch that this buffer
         // already holds them (first step into a buffer, after ch_set_state, ...; ch_api.cpp obs_zero_ptr)
-        if (wobs && (p.obs_full || p.ctl[1]))
-            for (int g = 0; g < Gv; ++g) obs_zero_env(obs_wg + g * RW, ei[I_N * G + g], rows, cat_off, m_obs, ct, CW);
+        if (wobs)
+            for (int g = 0; g < Gv; ++g)
+                if (p.obs_full || ei[I_OBSD * G + g]) obs_zero_env(obs_wg + g * RW, ei[I_N * G + g], rows, cat_off, m_obs, ct, CW);
         if constexpr (PW) {
             // whole envs' alpha tables and rows, one env per wave at a time, until the drone positions arrive
             while (lds_peek(fl + F_D) < 1 && alpha_step()) {
@@ -1165,6 +1248,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                 if (u < nf * M) {
                     const int f = qdiv(u, M, rM), g = flist[f], j = u - f * M;
                     alpha_row(S, M, P, g * M + j, g, j);
+                    if (sep) arrive(g * M + j, g, 1);
                 }
                 CHUNK_T1(2);
             }
@@ -1190,7 +1274,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             CH_UNROLL for (int k = 0; k < N; ++k) {
                 if (k >= n) break;   // |y_k - q_j| for the shepherd term and the closest-cow search
                 const R ex = S.dx[b0 + k] - qix, ey = S.dy[b0 + k] - qiy;
-                S.dcow[(b0 + k) * M + j] = sqrt(ex * ex + ey * ey);
+                S.dcow[(b0 + k) * M + j] = ex * ex + ey * ey;
             }
             if (task) {
                 // evaluate_herding_effectiveness winding number (evaluation.py:100-138)
@@ -1207,10 +1291,30 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             }
             if (j < m_obs && wobs) obs_cattle(obs_wg + g * RW, S.dx, S.dy, b0, j, n, cat_off, qix, qiy);
             }
+            // H counts finished items, so a wave still busy with an alpha chunk does not hold the drone wave up
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+            if (lane == 0) __hip_atomic_fetch_add(fl + F_H, min(64, Gv * M + Gv - b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             CHUNK_T1(1);
         }
-        lds_signal(fl + F_H);
         const float rN = 1.0f / (float)N;
+        for (;;) {   // getEulerFromQuaternion of the new attitudes (BaseAviary.py:704-766): the own row's roll,
+                     // pitch, yaw and the next step's PID input (the Euler cache)
+            const int b = grab(fl + C_EULER, 64), u = b + lane;
+            if (b >= Gv * N) break;
+            if (u < Gv * N) {
+                const int g = qdiv(u, N, rN), k = u - g * N;
+                if (k < ei[I_N * G + g]) {
+                    const int GN = G * N;
+                    const R qq[4] = {S.dq[u], S.dq[GN + u], S.dq[2 * GN + u], S.dq[3 * GN + u]};
+                    R r3[3];
+                    quat_to_euler(qq, r3);
+                    const long long dd = (long long)e0 * N + u;
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) CH_ST(&p.rpy[c * DS + dd], r3[c]);
+                    if (wobs) obs_rpy(obs_wg + g * RW, k, r3);
+                }
+            }
+        }
         if constexpr (PW) {
             while (alpha_step()) {   // the rest of the alpha work (the current env first)
             }
@@ -1235,61 +1339,104 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             }
             if (ct == 0) TS(16, (long long)clock64());
         } else {
-        // the alpha rows only feed the velocity update: they wait until the drone wave has its hand-off
-        lds_wait(fl + F_A, W1, p.err);   // every pair of the table
-        if (ct == 0) TS(20, (long long)clock64());
-        for (;;) {   // alpha rows of the cows of flocking envs
-            const int b = grab(fl + C_ROWS, 64), u = b + lane;
-            if (b >= nf * M) break;
-            CHUNK_T0;
-            if (u < nf * M) {
-                const int f = qdiv(u, M, rM), g = flist[f], j = u - f * M;
-                alpha_row(S, M, P, g * M + j, g, j);
+        if (sep) {
+            // the shepherd/predator (cow, drone) items need only the drone positions: they run before the alpha
+            // rows that remain; each cow's velocity update runs as soon as its row and its N terms are in
+            const int MN = M * N;
+            const float rMN = 1.0f / (float)MN;
+            const bool fuse = (64 % N) == 0;   // a chunk holds whole cows: one arrival of weight N per cow
+            for (;;) {
+                const int b = grab(fl + C_DELTA, 64), q = b + lane;
+                if (b >= nf * MN) break;
+                CHUNK_T0;
+                int j = 0, k = 0, g = 0;
+                const bool valid = q < nf * MN;
+                if (valid) {
+                    const int f = qdiv(q, MN, rMN), rem = q - f * MN;
+                    j = qdiv(rem, N, rN); k = rem - j * N;
+                    g = flist[f];
+                    if (k < ei[I_N * G + g]) delta_term(S, N, g * M + j, g, k, S.td, S.tdf, (g * M + j) * N + k, G * MN);
+                }
+                if (fuse) {
+                    wave_sync();   // the cow's terms, written by other lanes of this wave
+                    if (valid && k == 0) arrive(g * M + j, g, N);
+                } else if (valid) {
+                    arrive(g * M + j, g, 1);
+                }
+                CHUNK_T1(3);
             }
-            CHUNK_T1(2);
-        }
-        cow_sync(fl + F_W, W1, false, p.err);   // every alpha row read the pair table: its space now takes the drone terms
-        if (ct == 0) TS(21, (long long)clock64());
-        const int T = G * M * N, MN = M * N;
-        const float rMN = 1.0f / (float)MN;
-        // (cow, drone) items of flocking envs: shepherd and predator terms.  A chunk of 64 items holds
-        // whole cows when N divides 64 (the cow's N items are consecutive): the wave that computed a cow's
-        // terms then finishes that cow's velocity update itself (lane k = 0), with no workgroup sync.
-        const bool fuse = (64 % N) == 0;
-        for (;;) {
-            const int b = grab(fl + C_DELTA, 64), q = b + lane;
-            if (b >= nf * MN) break;
-            CHUNK_T0;
-            int f = 0, j = 0, k = 0, g = 0, n = 0;
-            const bool valid = q < nf * MN;
-            if (valid) {
-                f = qdiv(q, MN, rMN);
-                const int rem = q - f * MN;
-                j = qdiv(rem, N, rN); k = rem - j * N;
-                g = flist[f]; n = ei[I_N * G + g];
-                if (k < n) delta_term(S, N, g * M + j, g, k, S.td, S.tdf, (g * M + j) * N + k, T);
-            }
-            if (fuse) {
-                wave_sync();   // the cow's terms, written by other lanes of this wave
-                if (valid && k == 0) flock_combine(p, S, N, M, e0, g * M + j, n, S.td, S.tdf, (g * M + j) * N, T);
-            }
-            CHUNK_T1(3);
-        }
-        if (ct == 0) TS(16, (long long)clock64());
-        if (!fuse) {
-            cow_sync(fl + F_Q, W1, false, p.err);   // every drone term of every cow
-            if (ct == 0) TS(17, (long long)clock64());
-            for (;;) {   // cows of flocking envs only
-                const int b = grab(fl + C_FLOCK, 64), u = b + lane;
+            if (ct == 0) TS(16, (long long)clock64());
+            lds_wait(fl + F_A, W1, p.err);   // every pair of the table
+            if (ct == 0) TS(20, (long long)clock64());
+            for (;;) {   // the alpha rows that remain
+                const int b = grab(fl + C_ROWS, 64), u = b + lane;
                 if (b >= nf * M) break;
                 CHUNK_T0;
                 if (u < nf * M) {
                     const int f = qdiv(u, M, rM), g = flist[f], j = u - f * M;
-                    flock_combine(p, S, N, M, e0, g * M + j, ei[I_N * G + g], S.td, S.tdf, (g * M + j) * N, T);
+                    alpha_row(S, M, P, g * M + j, g, j);
+                    arrive(g * M + j, g, 1);
                 }
-                CHUNK_T1(4);
+                CHUNK_T1(2);
             }
-        }
+            if (ct == 0) TS(21, (long long)clock64());
+        } else {
+        // the alpha rows only feed the velocity update: they wait until the drone wave has its hand-off
+            lds_wait(fl + F_A, W1, p.err);   // every pair of the table
+            if (ct == 0) TS(20, (long long)clock64());
+            for (;;) {   // alpha rows of the cows of flocking envs
+                const int b = grab(fl + C_ROWS, 64), u = b + lane;
+                if (b >= nf * M) break;
+                CHUNK_T0;
+                if (u < nf * M) {
+                    const int f = qdiv(u, M, rM), g = flist[f], j = u - f * M;
+                    alpha_row(S, M, P, g * M + j, g, j);
+                }
+                CHUNK_T1(2);
+            }
+            cow_sync(fl + F_W, W1, false, p.err);   // every alpha row read the pair table: its space now takes the drone terms
+            if (ct == 0) TS(21, (long long)clock64());
+            const int T = G * M * N, MN = M * N;
+            const float rMN = 1.0f / (float)MN;
+            // (cow, drone) items of flocking envs: shepherd and predator terms.  A chunk of 64 items holds
+            // whole cows when N divides 64 (the cow's N items are consecutive): the wave that computed a cow's
+            // terms then finishes that cow's velocity update itself (lane k = 0), with no workgroup sync.
+            const bool fuse = (64 % N) == 0;
+            for (;;) {
+                const int b = grab(fl + C_DELTA, 64), q = b + lane;
+                if (b >= nf * MN) break;
+                CHUNK_T0;
+                int f = 0, j = 0, k = 0, g = 0, n = 0;
+                const bool valid = q < nf * MN;
+                if (valid) {
+                    f = qdiv(q, MN, rMN);
+                    const int rem = q - f * MN;
+                    j = qdiv(rem, N, rN); k = rem - j * N;
+                    g = flist[f]; n = ei[I_N * G + g];
+                    if (k < n) delta_term(S, N, g * M + j, g, k, S.td, S.tdf, (g * M + j) * N + k, T);
+                }
+                if (fuse) {
+                    wave_sync();   // the cow's terms, written by other lanes of this wave
+                    if (valid && k == 0) flock_combine(p, S, N, M, e0, g * M + j, n, S.td, S.tdf, (g * M + j) * N, T);
+                }
+                CHUNK_T1(3);
+            }
+            if (ct == 0) TS(16, (long long)clock64());
+            if (!fuse) {
+                cow_sync(fl + F_Q, W1, false, p.err);   // every drone term of every cow
+                if (ct == 0) TS(17, (long long)clock64());
+                for (;;) {   // cows of flocking envs only
+                    const int b = grab(fl + C_FLOCK, 64), u = b + lane;
+                    if (b >= nf * M) break;
+                    CHUNK_T0;
+                    if (u < nf * M) {
+                        const int f = qdiv(u, M, rM), g = flist[f], j = u - f * M;
+                        flock_combine(p, S, N, M, e0, g * M + j, ei[I_N * G + g], S.td, S.tdf, (g * M + j) * N, T);
+                    }
+                    CHUNK_T1(4);
+                }
+            }
+            }
         }
         if (lane == 0) TS(40 + (tid >> 6), (long long)clock64());   // this cow wave's flock work done
         if (ct == 0) TS(31, (long long)nf);
@@ -1365,17 +1512,14 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
     // ---- env scalars back to HBM (the drone wave's env lanes hold them) -----------------------------
     if (tid < Gv) {
         const int e = e0 + tid;
-        p.envi[0 * E + e] = f_n; p.envi[1 * E + e] = f_sc; p.envi[2 * E + e] = f_scA; p.envi[3 * E + e] = f_hp;
-        p.envi[4 * E + e] = f_level; p.envi[5 * E + e] = f_tally; p.envi[6 * E + e] = f_spawn;
-        p.envi[7 * E + e] = f_active; p.envi[8 * E + e] = f_episode;
-        p.envi[9 * E + e] += 1;   // ch_step calls on this env
-        p.envr[0 * E + e] = f_prev; p.envr[1 * E + e] = f_clock;
-    }
-    // the last workgroup to finish clears the control words: every workgroup read them at its start
-    // (every read of ctl in this workgroup was consumed before the barrier above)
-    if (tid == 0) {
-        const unsigned done = atomicAdd(reinterpret_cast<unsigned*>(p.ctl + 2), 1u);
-        if (done == gridDim.x - 1) { p.ctl[0] = 0; p.ctl[1] = 0; p.ctl[2] = 0; }
+        CH_ST(&p.envi[0 * E + e], f_n); CH_ST(&p.envi[1 * E + e], f_sc); CH_ST(&p.envi[2 * E + e], f_scA);
+        CH_ST(&p.envi[3 * E + e], f_hp); CH_ST(&p.envi[4 * E + e], f_level); CH_ST(&p.envi[5 * E + e], f_tally);
+        CH_ST(&p.envi[6 * E + e], f_spawn); CH_ST(&p.envi[7 * E + e], f_active); CH_ST(&p.envi[8 * E + e], f_episode);
+        CH_ST(&p.envi[9 * E + e], p.envi[9 * E + e] + 1);   // ch_step calls on this env
+        CH_ST(&p.envr[0 * E + e], f_prev); CH_ST(&p.envr[1 * E + e], f_clock);
+        // this step wrote the env's Euler cache and, unless obs were masked off, its whole obs block
+        p.stale[e] = 0;
+        if (wobs) p.stale[E + e] = 0;
     }
     if (tid == 0) { TS(14, (long long)clock64()); TS(1, (long long)wall_clock64()); }
 }
