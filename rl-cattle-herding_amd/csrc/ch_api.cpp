@@ -662,7 +662,8 @@ int ch__geometry(const ch_handle* h, int32_t* G, int32_t* block, int64_t* lds, i
     return CH_OK;
 }
 
-/* Internal diagnostics: skip kernel phases (1 drones, 2 flock, 4 task, 8 obs) to attribute time. */
+/* Internal diagnostics: skip kernel phases (1 drones, 2 flock, 4 task, 8 obs) to attribute time; 128 / 256: cow waves
+ * on the drone wave's SIMD take no chunks after / before the drone hand-off (v2 scheduling experiments). */
 /* Internal: forget which obs buffer holds valid constant-zero bytes (the caller wrote into it); the
  * next ch_step writes every obs block in full. */
 int ch__obs_invalidate(ch_handle* h, void* stream) {

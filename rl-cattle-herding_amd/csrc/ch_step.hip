@@ -39,6 +39,7 @@ enum { F_D = 0, F_T, F_H, F_A, F_E, F_R, F_X0, F_X1, F_X2,     // hand-off count
        C_PAIRS, C_ROWS, C_COWS, C_FLOCK, C_DELTA, F_W, F_Q,      // work counters (grab), cow-wave syncs
        Q_LEN, C_QUEUE, F_C,                                       // shared alpha queue: length, grab, cheap pass done
        C_EULER,                                                   // Euler angles of the new attitudes (cow waves)
+       V_DSIMD,                                                   // 1 + the SIMD the drone wave runs on
        FLAG_COUNT };
 static_assert(FLAG_COUNT <= kV2Flags, "LDS flag words");
 // after the per-env rows: flocking-env list [G], reset-env list [G], their counts, then the counters
@@ -101,7 +102,8 @@ __device__ __forceinline__ void lds_wait(int* f, int target, int* err) {
 // counter.  The cow waves do not run at equal speed (one of them shares its SIMD with the other
 // resident workgroup's prioritised drone wave), so a static lane -> item split leaves the slowest
 // wave with as many items as the fastest.
-__device__ __forceinline__ int grab(int* ctr, int n) {
+__device__ __forceinline__ int grab(int* ctr, int n, bool skip = false) {
+    if (skip) return 1 << 28;   // (wave-uniform) this wave takes no more items of the loop
     int b = 0;
     if ((threadIdx.x & 63) == 0) b = atomicAdd(ctr, n);
     return __builtin_amdgcn_readfirstlane(b);
@@ -187,7 +189,8 @@ struct V2Smem {
 // Write-through stores (an agent-scope relaxed atomic store is a global_store ... sc1): the lines leave the
 // XCD's L2 while the kernel runs instead of in the kernel-end write-back, which the next launch waits for.
 // Measured at C4 (tools/gpu_ab_store.sh): inter-kernel gap 2.6 -> 1.75 us, 164 -> 171 M env-steps/s;
-// non-temporal (nt, CH_NT_STORES) and plain stores both leave the lines dirty in L2.
+// non-temporal (nt, CH_NT_STORES) and plain stores both leave the lines dirty in L2.  Used for the outputs
+// (observations, rewards); the state uses CH_STS below.
 template <class T> __device__ __forceinline__ void ch_st_wt(T* ptr, T v) {
     static_assert(sizeof(T) == 4 || sizeof(T) == 8, "4- or 8-byte stores");
     if constexpr (sizeof(T) == 8)
@@ -202,6 +205,17 @@ template <class T> __device__ __forceinline__ void ch_st_wt(T* ptr, T v) {
 #define CH_ST(ptr, val) __builtin_nontemporal_store((val), (ptr))
 #else
 #define CH_ST(ptr, val) (*(ptr) = (val))
+#endif
+// State the next step reads back (drones, cattle, env scalars, metrics, Euler cache) stays in the XCD's L2
+// (nt): the next launch's first loads then hit L2 instead of MALL.  Same box, same build otherwise
+// (tools/gpu_ab_store.sh, profiles/r02/ab/): state nt + outputs write-through 161.7 M/s (span 23.5 us, gap
+// 2.3 us) vs everything write-through 158.8 M/s (24.2, 1.7).  CH_STATE_WT / CH_STATE_PLAIN for the A/B.
+#if defined(CH_STATE_WT)
+#define CH_STS(ptr, val) CH_ST(ptr, val)
+#elif defined(CH_STATE_PLAIN)
+#define CH_STS(ptr, val) (*(ptr) = (val))
+#else
+#define CH_STS(ptr, val) __builtin_nontemporal_store(static_cast<std::remove_pointer_t<decltype(ptr)>>(val), (ptr))
 #endif
 typedef float f2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void st2(float* eb, int off, float a, float b) {
@@ -298,11 +312,11 @@ template <class R> __device__ __forceinline__ bool in_sensing(R n2) {
 }
 
 template <class R>
-__device__ __forceinline__ void alpha_cheap(V2Smem<R>& S, int* fl, int M, int P, int nf, const int* flist) {
+__device__ __forceinline__ void alpha_cheap(V2Smem<R>& S, int* fl, int M, int P, int nf, const int* flist, bool skip) {
     const float rP = 1.0f / (float)P;
     const int lane = threadIdx.x & 63;
     for (;;) {
-        const int b = grab(fl + C_PAIRS, 64);
+        const int b = grab(fl + C_PAIRS, 64, skip);
         if (b >= nf * P) break;
         const int q = b + lane;
         bool cand = false;
@@ -331,13 +345,13 @@ __device__ __forceinline__ void alpha_cheap(V2Smem<R>& S, int* fl, int M, int P,
 }
 
 template <class R>
-__device__ __forceinline__ void alpha_full(V2Smem<R>& S, int* fl, int M, int P) {
+__device__ __forceinline__ void alpha_full(V2Smem<R>& S, int* fl, int M, int P, bool skip) {
     const R ra = sigma_norm_n(R(1.2)), da = ra;
     const int qn = lds_peek(fl + Q_LEN);   // final: every cow wave's cheap pass is done (F_C)
     const float rP = 1.0f / (float)P;
     const int lane = threadIdx.x & 63;
     for (;;) {
-        const int b = grab(fl + C_QUEUE, 64);
+        const int b = grab(fl + C_QUEUE, 64, skip);
         if (b >= qn) break;
         if (b + lane < qn) {
             const int gi = S.queue[b + lane];
@@ -545,7 +559,7 @@ __device__ __forceinline__ void flock_combine(const StepParams<R>& p, V2Smem<R>&
     R sp = norm2(vx, vy);
     if (sp > R(kMaxVelCattle)) { R f = R(kMaxVelCattle) / sp; vx *= f; vy *= f; }
     const long long ci = (long long)e0 * M + u;
-    CH_ST(&p.cattle[2 * CS + ci], vx); CH_ST(&p.cattle[3 * CS + ci], vy);
+    CH_STS(&p.cattle[2 * CS + ci], vx); CH_STS(&p.cattle[3 * CS + ci], vy);
 }
 
 // GT/NT/MT > 0 specialise the kernel for one geometry (envs per workgroup, drones, cattle): the LDS
@@ -586,10 +600,14 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
     double ev_acc = 0;   // update_evaluation_metrics' distance of this drone (optional)
     R spx_r[3] = {0, 0, 0}, spy_r[3] = {0, 0, 0};   // cow waves: prefetched spawn positions
     bool rpy_valid = false;
+    bool co_simd = false;   // a cow wave on the drone wave's SIMD (starved while the drone wave issues)
     if (tid < 64) {
         // the drone wave loads only what its chain reads, so the chain starts after one round trip; the
         // cow waves stage the env scalars, the curriculum table and the pair list meanwhile
         __builtin_amdgcn_s_setprio(3);   // the drone wave is the critical path: it wins issue on a shared SIMD
+        if (tid == 0)
+            __hip_atomic_store(fl + V_DSIMD, 1 + (int)((__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
         if (dlane) {
             n0 = p.envi[0 * E + e0 + dg];
             rpy_valid = p.stale[e0 + dg] == 0;   // this env's Euler cache (written by the last v2 step)
@@ -624,7 +642,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             // frictionless cube (trace-pinned); no p.stepSimulation under Physics.DYN (BaseAviary.py:447-448)
             if (!PHYS || (p.physics != CH_PHYS_DYN && p.physics != CH_PHYS_DYN_RK4))
                 for (int s = 0; s < p.substeps; ++s) { x += vx * dt; y += vy * dt; }
-            CH_ST(&p.cattle[0 * CS + ci], x); CH_ST(&p.cattle[1 * CS + ci], y);
+            CH_STS(&p.cattle[0 * CS + ci], x); CH_STS(&p.cattle[1 * CS + ci], y);
             S.cx[u] = x; S.cy[u] = y; S.cvx[u] = vx; S.cvy[u] = vy;
         }
         for (int k = ct; k < (int)(sizeof(kLevels) / 4); k += CW)
@@ -657,6 +675,14 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         if (ct == 0) { ei[NF_AT] = __popcll(bal); ei[NR_AT] = 0; }
         }
         cow_sync(fl + F_E, W1, false, p.err);   // env scalars, flocking list, tables: seen by every cow wave
+        {
+            int ds = lds_peek(fl + V_DSIMD);
+            for (int spins = 0; ds == 0 && spins < (1 << 22); ++spins) {   // stored by the drone wave at its start
+                __builtin_amdgcn_s_sleep(1);
+                ds = lds_peek(fl + V_DSIMD);
+            }
+            co_simd = (int)((__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3) + 1 == ds;
+        }
         if (ct == 0) TS(11, (long long)clock64());
         // spawn positions of the episode an auto-reset would start: scenario index + 1 (BaseAviary.py:600-606).
         // Loaded into registers here and parked in LDS after the pair loop, so the load latency hides
@@ -711,9 +737,9 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                 if constexpr (PHYS) {
                     variant_substeps(p, dg * N, N, n, pos, q, v, w, rpm, ph_lr, ph_rr);
 #pragma unroll
-                    for (int c = 0; c < 4; ++c) CH_ST(&p.phys[c * DS + di], ph_lr[c]);
+                    for (int c = 0; c < 4; ++c) CH_STS(&p.phys[c * DS + di], ph_lr[c]);
 #pragma unroll
-                    for (int c = 0; c < 3; ++c) CH_ST(&p.phys[(4 + c) * DS + di], ph_rr[c]);
+                    for (int c = 0; c < 3; ++c) CH_STS(&p.phys[(4 + c) * DS + di], ph_rr[c]);
                 } else {
                     for (int s = 0; s < p.substeps; ++s)
                         drone_substep(pos, q, v, w, rpm, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0);
@@ -721,13 +747,13 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             }
             R* D = p.drone;
 #pragma unroll
-            for (int c = 0; c < 3; ++c) CH_ST(&D[c * DS + di], pos[c]);
+            for (int c = 0; c < 3; ++c) CH_STS(&D[c * DS + di], pos[c]);
 #pragma unroll
-            for (int c = 0; c < 4; ++c) CH_ST(&D[(3 + c) * DS + di], q[c]);
+            for (int c = 0; c < 4; ++c) CH_STS(&D[(3 + c) * DS + di], q[c]);
 #pragma unroll
-            for (int c = 0; c < 3; ++c) { CH_ST(&D[(7 + c) * DS + di], v[c]); CH_ST(&D[(10 + c) * DS + di], w[c]); }
+            for (int c = 0; c < 3; ++c) { CH_STS(&D[(7 + c) * DS + di], v[c]); CH_STS(&D[(10 + c) * DS + di], w[c]); }
 #pragma unroll
-            for (int c = 0; c < 9; ++c) CH_ST(&D[(13 + c) * DS + di], pid[c]);
+            for (int c = 0; c < 9; ++c) CH_STS(&D[(13 + c) * DS + di], pid[c]);
             S.dx[tid] = pos[0]; S.dy[tid] = pos[1]; S.dz[tid] = pos[2];
 #pragma unroll
             for (int c = 0; c < 4; ++c) S.dq[c * (G * N) + tid] = q[c];
@@ -738,7 +764,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         if (live && wobs) obs_own_nrpy(obs_wg + dg * RW, dk, pos[2], v, w);
         if (tid == 0) TS(4, (long long)clock64());
         lds_wait(fl + F_E, W1, p.err);   // env scalars and the curriculum table (staged by the cow waves)
-        if (p.evald && live) CH_ST(&p.evald[di], eval_distance_step(ev_acc, ei[I_SC * G + dg] == 0, px0, py0, pos[0], pos[1]));
+        if (p.evald && live) CH_STS(&p.evald[di], eval_distance_step(ev_acc, ei[I_SC * G + dg] == 0, px0, py0, pos[0], pos[1]));
 
         // per-drone reward terms (CattleAviary.py:230-246, 572-679) and neighbour obs (BaseRLAviary.py:303-317)
         if (live && task) {
@@ -1147,7 +1173,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                 o[kMetricCurLen] = 0;
             }
 #pragma unroll
-            for (int r = 0; r < kMetricRows; ++r) CH_ST(&p.metrics[r * E + e], o[r]);
+            for (int r = 0; r < kMetricRows; ++r) CH_STS(&p.metrics[r * E + e], o[r]);
             if (g == 0) TS(28, (long long)clock64());
             if (p.reset_happened) p.reset_happened[e] = rs;
             // SB3 auto-reset: the new episode's scalars (the cow waves rebuild its bodies and observation)
@@ -1164,6 +1190,11 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         const int nf = ei[NF_AT];
         const int* flist = ei + FL_LIST;
         const int lane = tid & 63;
+        // a cow wave on the drone wave's SIMD takes no chunks (phase-mask bits 128: after the drone hand-off,
+        // 256: before it): a chunk it holds finishes late, as the prioritised drone wave wins the SIMD's issue
+        const bool co = co_simd && W1 >= 4;   // the other cow waves (>= 2 of them) take the work
+        const bool skip_pre = co && (p.phase_mask & 256), skip_post = co && (p.phase_mask & 128);
+        bool skip_now = skip_pre;
         // PW: this wave's env slot and queue, the env (flock-list index) it holds, the next cheap-pass
         // chunk, and the queue length / position of the expensive pass
         R* tb = nullptr;
@@ -1186,7 +1217,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         };
         auto alpha_step = [&]() -> bool {
             if (f_cur < 0) {
-                f_cur = grab(fl + C_PAIRS, 1);
+                f_cur = grab(fl + C_PAIRS, 1, skip_now);
                 ch = 0; qn = 0; qd = 0;
             }
             if (f_cur >= nf) return false;
@@ -1214,10 +1245,10 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             tf = S.tdf + (size_t)(tid / 64 - 1) * M * N;
             qu = S.queue + (size_t)(tid / 64 - 1) * P;
         } else {
-            alpha_cheap(S, fl, M, P, nf, flist);
+            alpha_cheap(S, fl, M, P, nf, flist, skip_pre);
             lds_signal(fl + F_C);
             lds_wait(fl + F_C, W1, p.err);   // the queue is complete
-            alpha_full(S, fl, M, P);
+            alpha_full(S, fl, M, P, skip_pre);
         }
         if (ct == 0) TS(18, (long long)clock64());
 #pragma unroll
@@ -1242,7 +1273,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                 if (lds_peek(fl + F_D) >= 1) break;
                 if (lds_peek(fl + F_A) < W1) { __builtin_amdgcn_s_sleep(1); continue; }
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");   // the pair table
-                const int b = grab(fl + C_ROWS, 64), u = b + lane;
+                const int b = grab(fl + C_ROWS, 64, skip_pre), u = b + lane;
                 if (b >= nf * M) break;
                 CHUNK_T0;
                 if (u < nf * M) {
@@ -1256,8 +1287,9 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         if (ct == 0) TS(8, (long long)clock64());
         lds_wait(fl + F_D, 1, p.err);
         if (ct == 0) TS(9, (long long)clock64());
+        skip_now = skip_post;
         for (;;) {   // per cow: distances, winding number, observation entries; then per env: herd centroid
-            const int b = grab(fl + C_COWS, 64), u = b + lane;
+            const int b = grab(fl + C_COWS, 64, skip_post), u = b + lane;
             if (b >= Gv * M + Gv) break;
             CHUNK_T0;
             if (u >= Gv * M) {
@@ -1299,7 +1331,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         const float rN = 1.0f / (float)N;
         for (;;) {   // getEulerFromQuaternion of the new attitudes (BaseAviary.py:704-766): the own row's roll,
                      // pitch, yaw and the next step's PID input (the Euler cache)
-            const int b = grab(fl + C_EULER, 64), u = b + lane;
+            const int b = grab(fl + C_EULER, 64, skip_post), u = b + lane;
             if (b >= Gv * N) break;
             if (u < Gv * N) {
                 const int g = qdiv(u, N, rN), k = u - g * N;
@@ -1310,7 +1342,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                     quat_to_euler(qq, r3);
                     const long long dd = (long long)e0 * N + u;
 #pragma unroll
-                    for (int c = 0; c < 3; ++c) CH_ST(&p.rpy[c * DS + dd], r3[c]);
+                    for (int c = 0; c < 3; ++c) CH_STS(&p.rpy[c * DS + dd], r3[c]);
                     if (wobs) obs_rpy(obs_wg + g * RW, k, r3);
                 }
             }
@@ -1324,7 +1356,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             // slot: the env's (cow, drone) items, then each cow's terms in drone order
             const int MN = M * N;
             for (;;) {
-                const int f = grab(fl + C_DELTA, 1);
+                const int f = grab(fl + C_DELTA, 1, skip_post);
                 if (f >= nf) break;
                 CHUNK_T0;
                 const int g = flist[f], n = ei[I_N * G + g];
@@ -1346,7 +1378,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             const float rMN = 1.0f / (float)MN;
             const bool fuse = (64 % N) == 0;   // a chunk holds whole cows: one arrival of weight N per cow
             for (;;) {
-                const int b = grab(fl + C_DELTA, 64), q = b + lane;
+                const int b = grab(fl + C_DELTA, 64, skip_post), q = b + lane;
                 if (b >= nf * MN) break;
                 CHUNK_T0;
                 int j = 0, k = 0, g = 0;
@@ -1369,7 +1401,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             lds_wait(fl + F_A, W1, p.err);   // every pair of the table
             if (ct == 0) TS(20, (long long)clock64());
             for (;;) {   // the alpha rows that remain
-                const int b = grab(fl + C_ROWS, 64), u = b + lane;
+                const int b = grab(fl + C_ROWS, 64, skip_post), u = b + lane;
                 if (b >= nf * M) break;
                 CHUNK_T0;
                 if (u < nf * M) {
@@ -1385,7 +1417,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             lds_wait(fl + F_A, W1, p.err);   // every pair of the table
             if (ct == 0) TS(20, (long long)clock64());
             for (;;) {   // alpha rows of the cows of flocking envs
-                const int b = grab(fl + C_ROWS, 64), u = b + lane;
+                const int b = grab(fl + C_ROWS, 64, skip_post), u = b + lane;
                 if (b >= nf * M) break;
                 CHUNK_T0;
                 if (u < nf * M) {
@@ -1403,7 +1435,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             // terms then finishes that cow's velocity update itself (lane k = 0), with no workgroup sync.
             const bool fuse = (64 % N) == 0;
             for (;;) {
-                const int b = grab(fl + C_DELTA, 64), q = b + lane;
+                const int b = grab(fl + C_DELTA, 64, skip_post), q = b + lane;
                 if (b >= nf * MN) break;
                 CHUNK_T0;
                 int f = 0, j = 0, k = 0, g = 0, n = 0;
@@ -1426,7 +1458,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                 cow_sync(fl + F_Q, W1, false, p.err);   // every drone term of every cow
                 if (ct == 0) TS(17, (long long)clock64());
                 for (;;) {   // cows of flocking envs only
-                    const int b = grab(fl + C_FLOCK, 64), u = b + lane;
+                    const int b = grab(fl + C_FLOCK, 64, skip_post), u = b + lane;
                     if (b >= nf * M) break;
                     CHUNK_T0;
                     if (u < nf * M) {
@@ -1441,6 +1473,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         if (lane == 0) TS(40 + (tid >> 6), (long long)clock64());   // this cow wave's flock work done
         if (ct == 0) TS(31, (long long)nf);
         lds_wait(fl + F_R, 1, p.err);    // the reset list
+        if (tid == 64) TS(37, (long long)clock64());
         const int nr = ei[NR_AT];
         if (nr) {   // uniform across the cow waves
             // ---- SB3 auto-reset of the listed envs (BaseAviary.reset, BaseAviary.py:280-331), rebuilt from
@@ -1463,11 +1496,11 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                 reset_drone(p, (long long)e0 * N + ud, k, n, x, y, z);
                 if constexpr (PHYS) {   // last_clipped_action, rpy_rates = 0 (_housekeeping, BaseAviary.py:565, 581-582)
 #pragma unroll
-                    for (int c = 0; c < kPhysComps; ++c) CH_ST(&p.phys[c * DS + (long long)e0 * N + ud], R(0));
+                    for (int c = 0; c < kPhysComps; ++c) CH_STS(&p.phys[c * DS + (long long)e0 * N + ud], R(0));
                 }
                 {   // identity attitude: Euler angles (+0, -0, +0) for the next step's cache
                     const long long dd = (long long)e0 * N + ud;
-                    CH_ST(&p.rpy[dd], R(0)); CH_ST(&p.rpy[DS + dd], -R(0)); CH_ST(&p.rpy[2 * DS + dd], R(0));
+                    CH_STS(&p.rpy[dd], R(0)); CH_STS(&p.rpy[DS + dd], -R(0)); CH_STS(&p.rpy[2 * DS + dd], R(0));
                 }
                 S.dx[ud] = x; S.dy[ud] = y; S.dz[ud] = z;
                 if (!wobs) continue;
@@ -1506,17 +1539,19 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             }
         }
     }
+    if (tid == 0) TS(35, (long long)clock64());
+    if (tid == 64) TS(36, (long long)clock64());
     lds_barrier();
     if (tid == 0) TS(13, (long long)clock64());
 
     // ---- env scalars back to HBM (the drone wave's env lanes hold them) -----------------------------
     if (tid < Gv) {
         const int e = e0 + tid;
-        CH_ST(&p.envi[0 * E + e], f_n); CH_ST(&p.envi[1 * E + e], f_sc); CH_ST(&p.envi[2 * E + e], f_scA);
-        CH_ST(&p.envi[3 * E + e], f_hp); CH_ST(&p.envi[4 * E + e], f_level); CH_ST(&p.envi[5 * E + e], f_tally);
-        CH_ST(&p.envi[6 * E + e], f_spawn); CH_ST(&p.envi[7 * E + e], f_active); CH_ST(&p.envi[8 * E + e], f_episode);
-        CH_ST(&p.envi[9 * E + e], p.envi[9 * E + e] + 1);   // ch_step calls on this env
-        CH_ST(&p.envr[0 * E + e], f_prev); CH_ST(&p.envr[1 * E + e], f_clock);
+        CH_STS(&p.envi[0 * E + e], f_n); CH_STS(&p.envi[1 * E + e], f_sc); CH_STS(&p.envi[2 * E + e], f_scA);
+        CH_STS(&p.envi[3 * E + e], f_hp); CH_STS(&p.envi[4 * E + e], f_level); CH_STS(&p.envi[5 * E + e], f_tally);
+        CH_STS(&p.envi[6 * E + e], f_spawn); CH_STS(&p.envi[7 * E + e], f_active); CH_STS(&p.envi[8 * E + e], f_episode);
+        CH_STS(&p.envi[9 * E + e], p.envi[9 * E + e] + 1);   // ch_step calls on this env
+        CH_STS(&p.envr[0 * E + e], f_prev); CH_STS(&p.envr[1 * E + e], f_clock);
         // this step wrote the env's Euler cache and, unless obs were masked off, its whole obs block
         p.stale[e] = 0;
         if (wobs) p.stale[E + e] = 0;

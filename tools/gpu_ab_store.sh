@@ -8,7 +8,7 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 out=gpurun_out/ab_store.log
 : > $out
-for v in "" _nt _plain; do
+for v in "" ${AB_VARIANTS:-_nt _plain}; do
   lib=rl-cattle-herding_amd/cattleherd/libcattleherd${v}.so
   [ -f $lib ] || continue
   echo "== variant '${v}'" >> $out

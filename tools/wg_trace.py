@@ -60,6 +60,7 @@ def trace(mode, E, n, m, prec, G=None, B=None, steps=4):
                   f"D {r2(9):.0f} H(drone) {r2(6):.0f} delta {r2(16):.0f} Q {r2(17):.0f} flock {r2(10):.0f} "
                   f"| cow waves done (mean per wave) {' '.join(f'{(t[sel, 40 + w] - t[sel, 2]).mean():.0f}' for w in range(1, blk.value // 64))} "
                   f"| drone book {r2(7):.0f} B1 {r2(13):.0f} end {r2(14):.0f}")
+        print(f"   at the last barrier: drone wave {rel(35):.0f} cow wave 1 {rel(36):.0f} (F_R seen {rel(37):.0f})")
         print(f"   bookkeeping: scalars+centroid {rel(32):.0f} marl-prep {rel(33):.0f} env.step dicts {rel(34):.0f}")
         print(f"   drone wave after H: dtaskB {rel(26):.0f} pre-fence {rel(27):.0f} published {rel(15):.0f} "
               f"reward {rel(19):.0f} metrics stored {rel(28):.0f} book {rel(7):.0f}")
