@@ -5,15 +5,17 @@
 //
 // Layout: a workgroup owns 16 input rows (envs or agents) and carries them through every layer.
 // The 4 waves split each layer's output columns into 16x16 tiles (v_mfma_f32_16x16x4_f32: exact f32,
-// a k-ordered fma chain per output element).  The K dimension streams in chunks of 32 through LDS:
-// the next chunk of the input rows and of the weight rows is loaded into registers while the current
-// one is multiplied.  Hidden activations stay in LDS between layers.  The grid is rows/16
+// a k-ordered fma chain per output element).  The K dimension streams in chunks of 64 through LDS, from
+// a register ring that keeps the next 3 chunks of input and weight rows in flight (1 for 256-wide
+// layers) while the current one is multiplied.  Hidden activations stay in LDS between layers.  The grid is rows/16
 // workgroups: 4096 envs fill 256 CUs with one workgroup each.
 //
 // Zero input columns.  An observation row has NUM_DRONES live rows of 86 features and zeros after
 // them (BaseRLAviary.py:272-342).  With per-row live widths the tile multiplies only the chunks below
 // its widest live row: the skipped products are 0 * w, which add +-0 to the sums.
 #include <hip/hip_runtime.h>
+
+#include <atomic>
 
 #include "ch_internal.h"
 
@@ -40,7 +42,7 @@ __device__ __forceinline__ float act_fn(float v, int act) {
 // TW = 16-column tiles per wave (the layer's tiles rounded up to 4 TW): every wave runs the same
 // straight-line MFMA sequence; tiles past the layer width multiply zero weight rows (a branch per
 // tile would make the compiler shuffle the accumulators around every MFMA).
-template <bool AG, int TW>
+template <bool AG, int TW, int DEPTH>
 __device__ __forceinline__ void mlp_layer(const MlpArgs& a, int li, const float* __restrict__ Ag, long long lda,
                                           const float* Al, int ldl, int K, int kloop, float* xs, float* ws, float* out,
                                           int ldo, bool last) {
@@ -55,75 +57,96 @@ __device__ __forceinline__ void mlp_layer(const MlpArgs& a, int li, const float*
 #pragma unroll
     for (int j = 0; j < TW; ++j) acc[j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 
-    // register prefetch of one chunk: 4 input floats and 4 TW float4 of weights per thread.  Thread
-    // t covers weight row n = t / 16 + 16 i, columns 4 (t % 16) .. +3 of the chunk (a 256-B row
-    // segment per 16 lanes); rows past the layer width are zero.  Loads are branch-free: clamped
-    // (always valid) addresses and a select, so a chunk's loads are all in flight together.
+    // Register ring of DEPTH chunks: 4 input floats and 4 TW float4 of weights per thread and chunk.  Thread
+    // t covers weight row n = t / 16 + 16 i, columns 4 (t % 16) .. +3 of the chunk (a 256-B row segment
+    // per 16 lanes); rows past the layer width are zero.  Loads are branch-free: clamped (always valid)
+    // addresses and a select.  DEPTH chunks are in flight while one is multiplied: a chunk's multiplies
+    // take a few hundred cycles, its loads (L2/MALL) thousands.
     constexpr int kWP = 4 * TW;                     // float4 per thread: 64 TW rows x kKC / 4 / 256
     const bool vec = (K & 3) == 0;   // weight rows 16-B aligned: float4 loads
-    float xr[4];
-    float4 wr[kWP];
+    float xr[DEPTH][4];
+    float4 wr[DEPTH][kWP];
     const int wn0 = tid >> 4, wc = (tid & 15) * 4;
-    auto fetch = [&](int kc) {
-        if constexpr (AG) {
-            const int r = tid >> 4, c = (tid & 15) * 4;
-            const bool rv = row0 + r < a.rows;
-            const float* src = Ag + min(row0 + r, a.rows - 1) * lda;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float v = src[min(kc + c + q, K - 1)];
-                xr[q] = rv && kc + c + q < K ? v : 0.0f;
-            }
-        }
-        if (vec) {
-#pragma unroll
-            for (int i = 0; i < kWP; ++i) {
-                const int n = wn0 + 16 * i, k = kc + wc;
-                const float4 v = *reinterpret_cast<const float4*>(W + min(n, N - 1) * K + min(k, K - 4));
-                wr[i] = n < N && k < K ? v : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            }
-        } else {
-#pragma unroll
-            for (int i = 0; i < kWP; ++i) {
-                const int n = wn0 + 16 * i, k = kc + wc;
-                const bool nv = n < N;
-                const float* src = W + min(n, N - 1) * K;
-                const float v0 = src[min(k, K - 1)], v1 = src[min(k + 1, K - 1)], v2 = src[min(k + 2, K - 1)],
-                            v3 = src[min(k + 3, K - 1)];
-                wr[i] = make_float4(nv && k < K ? v0 : 0.0f, nv && k + 1 < K ? v1 : 0.0f, nv && k + 2 < K ? v2 : 0.0f,
-                                    nv && k + 3 < K ? v3 : 0.0f);
-            }
-        }
-    };
-    if (kloop > 0) fetch(0);
-    for (int kc = 0; kc < kloop; kc += kKC) {
-        if constexpr (AG) {
-            const int r = tid >> 4, c = (tid & 15) * 4;
-            *reinterpret_cast<float4*>(xs + r * kKS + c) = make_float4(xr[0], xr[1], xr[2], xr[3]);
-        }
-#pragma unroll
-        for (int i = 0; i < kWP; ++i) *reinterpret_cast<float4*>(ws + (wn0 + 16 * i) * kKS + wc) = wr[i];
-        __syncthreads();
-        if (kc + kKC < kloop) fetch(kc + kKC);   // in flight during the multiplies below
-        // A[row l&15][k = 4 ks + (l >> 4)], B[k][col l&15] (16x16x4 f32 operand map).  All operands of
-        // the chunk are read first (one LDS latency), then the MFMAs issue back to back.  Hidden-layer A
-        // columns past K read zeros or finite stale values, which meet zero weight rows.
-        float av[kKC / 4], bv[TW][kKC / 4];
-#pragma unroll
-        for (int ks = 0; ks < kKC / 4; ++ks) {
-            const int kk = ks * 4 + (lane >> 4);
-            if constexpr (AG) av[ks] = xs[(lane & 15) * kKS + kk];
-            else av[ks] = Al[(lane & 15) * ldl + kc + kk];
-#pragma unroll
-            for (int j = 0; j < TW; ++j) bv[j][ks] = ws[((wave + 4 * j) * 16 + (lane & 15)) * kKS + kk];
-        }
-#pragma unroll
-        for (int ks = 0; ks < kKC / 4; ++ks) {
-#pragma unroll
-            for (int j = 0; j < TW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[ks], bv[j][ks], acc[j], 0, 0, 0);
-        }
-        __syncthreads();
+    // fetch chunk kc into ring slot S (a literal: the ring stays in registers)
+#define CH_MLP_FETCH(S, kc_)                                                                                        \
+    do {                                                                                                            \
+        const int kcf = (kc_);                                                                                      \
+        if constexpr (AG) {                                                                                         \
+            const int r = tid >> 4, c = (tid & 15) * 4;                                                             \
+            const float* src = Ag + min(row0 + r, a.rows - 1) * lda;                                                \
+            _Pragma("unroll") for (int q = 0; q < 4; ++q) xr[S][q] = src[min(kcf + c + q, K - 1)];                  \
+        }                                                                                                           \
+        if (vec) {                                                                                                  \
+            _Pragma("unroll") for (int i = 0; i < kWP; ++i) {                                                       \
+                const int n = wn0 + 16 * i, k = kcf + wc;                                                           \
+                wr[S][i] = *reinterpret_cast<const float4*>(W + min(n, N - 1) * K + min(k, K - 4));                 \
+            }                                                                                                       \
+        } else {                                                                                                    \
+            _Pragma("unroll") for (int i = 0; i < kWP; ++i) {                                                       \
+                const int n = wn0 + 16 * i, k = kcf + wc;                                                           \
+                const float* src = W + min(n, N - 1) * K;                                                           \
+                wr[S][i] = make_float4(src[min(k, K - 1)], src[min(k + 1, K - 1)], src[min(k + 2, K - 1)],         \
+                                       src[min(k + 3, K - 1)]);                                                     \
+            }                                                                                                       \
+        }                                                                                                           \
+    } while (0)
+    // chunk c from ring slot S into LDS -- out-of-range rows and columns masked to zero here, not at the load,
+    // so that no instruction waits for a load before its store -- then the fetch of chunk c + DEPTH into the
+    // freed slot (DEPTH chunks in flight during the multiplies), then the multiplies
+#define CH_MLP_STEP(S)                                                                                              \
+    if constexpr (S < DEPTH) {                                                                                      \
+        const int c = c0 + S, kc = c * kKC;                                                                         \
+        if (c < nch) {                                                                                              \
+            if constexpr (AG) {                                                                                     \
+                const int r = tid >> 4, cc = (tid & 15) * 4;                                                        \
+                const bool rv = row0 + r < a.rows;                                                                  \
+                float xq[4];                                                                                        \
+                _Pragma("unroll") for (int q = 0; q < 4; ++q) xq[q] = rv && kc + cc + q < K ? xr[S][q] : 0.0f;      \
+                *reinterpret_cast<float4*>(xs + r * kKS + cc) = make_float4(xq[0], xq[1], xq[2], xq[3]);            \
+            }                                                                                                       \
+            _Pragma("unroll") for (int i = 0; i < kWP; ++i) {                                                       \
+                const int n = wn0 + 16 * i, k = kc + wc;                                                            \
+                const bool nv = n < N;                                                                              \
+                const float4 v = wr[S][i];                                                                          \
+                *reinterpret_cast<float4*>(ws + n * kKS + wc) =                                                     \
+                    make_float4(nv && k < K ? v.x : 0.0f, nv && k + 1 < K ? v.y : 0.0f, nv && k + 2 < K ? v.z : 0.0f, \
+                                nv && k + 3 < K ? v.w : 0.0f);                                                      \
+            }                                                                                                       \
+            __syncthreads();                                                                                        \
+            if (c + DEPTH < nch) CH_MLP_FETCH(S, kc + DEPTH * kKC);                                                 \
+            float av[kKC / 4], bv[TW][kKC / 4];                                                                     \
+            _Pragma("unroll") for (int ks = 0; ks < kKC / 4; ++ks) {                                                \
+                const int kk = ks * 4 + (lane >> 4);                                                                \
+                if constexpr (AG) av[ks] = xs[(lane & 15) * kKS + kk];                                              \
+                else av[ks] = Al[(lane & 15) * ldl + kc + kk];                                                      \
+                _Pragma("unroll") for (int j = 0; j < TW; ++j)                                                      \
+                    bv[j][ks] = ws[((wave + 4 * j) * 16 + (lane & 15)) * kKS + kk];                                 \
+            }                                                                                                       \
+            _Pragma("unroll") for (int ks = 0; ks < kKC / 4; ++ks) {                                                \
+                _Pragma("unroll") for (int j = 0; j < TW; ++j)                                                      \
+                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[ks], bv[j][ks], acc[j], 0, 0, 0);              \
+            }                                                                                                       \
+            __syncthreads();                                                                                        \
+        }                                                                                                           \
     }
+    const int nch = (kloop + kKC - 1) / kKC;
+    const int c0 = 0;   // (the prologue's chunk indices)
+    (void)c0;
+    if (0 < nch) CH_MLP_FETCH(0, 0);
+    if constexpr (DEPTH > 1) { if (1 < nch) CH_MLP_FETCH(1, kKC); }
+    if constexpr (DEPTH > 2) { if (2 < nch) CH_MLP_FETCH(2, 2 * kKC); }
+    if constexpr (DEPTH > 3) { if (3 < nch) CH_MLP_FETCH(3, 3 * kKC); }
+    // A[row l&15][k = 4 ks + (l >> 4)], B[k][col l&15] (16x16x4 f32 operand map).  All operands of a chunk
+    // are read first (one LDS latency), then the MFMAs issue back to back.  Hidden-layer A columns past K
+    // read zeros or finite stale values, which meet zero weight rows.
+    for (int c0 = 0; c0 < nch; c0 += DEPTH) {
+        CH_MLP_STEP(0)
+        CH_MLP_STEP(1)
+        CH_MLP_STEP(2)
+        CH_MLP_STEP(3)
+    }
+#undef CH_MLP_STEP
+#undef CH_MLP_FETCH
     // epilogue: C/D map col = lane & 15, row = 4 (lane >> 4) + r
 #pragma unroll
     for (int j = 0; j < TW; ++j) {
@@ -152,6 +175,14 @@ __device__ __forceinline__ void mlp_layer(const MlpArgs& a, int li, const float*
     __syncthreads();
 }
 
+
+// WIDE: some layer is wider than 128 (the RLlib 256-wide model): 16-column tiles up to 4 per wave, one
+// chunk in flight; otherwise (the SB3 actor / critic, 128 wide) up to 2 tiles per wave and two chunks in
+// flight.  Separate kernels keep the narrow one's register ring from spilling.  (Tried and reverted: a
+// split-K layer with each wave loading its K chunks straight from global memory into the MFMA operand
+// layout, no LDS staging: 85 us for one 16-row tile of the 1032-wide forward vs 35 us, the 16-row x
+// 64-byte operand loads being far slower than the coalesced staging loads.)
+template <bool WIDE>
 __global__ __launch_bounds__(256) void k_mlp(MlpArgs a) {
     extern __shared__ __align__(16) float sm[];
     float* xs = sm;                                  // [16][kKS]
@@ -181,16 +212,28 @@ __global__ __launch_bounds__(256) void k_mlp(MlpArgs a) {
     for (int li = 0; li < a.layers; ++li) {
         const bool last = li == a.layers - 1;
         const int nt = (a.dims[li + 1] + 15) >> 4;
-        if (li == 0) {
-            if (nt <= 4) mlp_layer<true, 1>(a, 0, a.x, a.dims[0], nullptr, 0, a.dims[0], kloop0, xs, ws, cur, ldh, last);
-            else if (nt <= 8) mlp_layer<true, 2>(a, 0, a.x, a.dims[0], nullptr, 0, a.dims[0], kloop0, xs, ws, cur, ldh, last);
-            else mlp_layer<true, 4>(a, 0, a.x, a.dims[0], nullptr, 0, a.dims[0], kloop0, xs, ws, cur, ldh, last);
-        } else {
-            const int K = a.dims[li];
-            if (nt <= 4) mlp_layer<false, 1>(a, li, nullptr, 0, cur, ldh, K, K, xs, ws, nxt, ldh, last);
-            else if (nt <= 8) mlp_layer<false, 2>(a, li, nullptr, 0, cur, ldh, K, K, xs, ws, nxt, ldh, last);
-            else mlp_layer<false, 4>(a, li, nullptr, 0, cur, ldh, K, K, xs, ws, nxt, ldh, last);
-            float* t = cur; cur = nxt; nxt = t;
+        if constexpr (WIDE) {
+            if (li == 0) {
+                if (nt <= 4) mlp_layer<true, 1, 1>(a, 0, a.x, a.dims[0], nullptr, 0, a.dims[0], kloop0, xs, ws, cur, ldh, last);
+                else if (nt > 8) mlp_layer<true, 4, 1>(a, 0, a.x, a.dims[0], nullptr, 0, a.dims[0], kloop0, xs, ws, cur, ldh, last);
+                else mlp_layer<true, 2, 1>(a, 0, a.x, a.dims[0], nullptr, 0, a.dims[0], kloop0, xs, ws, cur, ldh, last);
+            } else {
+                const int K = a.dims[li];
+                if (nt <= 4) mlp_layer<false, 1, 1>(a, li, nullptr, 0, cur, ldh, K, K, xs, ws, nxt, ldh, last);
+                else if (nt > 8) mlp_layer<false, 4, 1>(a, li, nullptr, 0, cur, ldh, K, K, xs, ws, nxt, ldh, last);
+                else mlp_layer<false, 2, 1>(a, li, nullptr, 0, cur, ldh, K, K, xs, ws, nxt, ldh, last);
+                float* t = cur; cur = nxt; nxt = t;
+            }
+        } else {   // two chunks in flight (a deeper ring measured no faster: 3 chunks 27.5 us vs 2 chunks 24.8)
+            if (li == 0) {
+                if (nt <= 4) mlp_layer<true, 1, 2>(a, 0, a.x, a.dims[0], nullptr, 0, a.dims[0], kloop0, xs, ws, cur, ldh, last);
+                else mlp_layer<true, 2, 2>(a, 0, a.x, a.dims[0], nullptr, 0, a.dims[0], kloop0, xs, ws, cur, ldh, last);
+            } else {
+                const int K = a.dims[li];
+                if (nt <= 4) mlp_layer<false, 1, 2>(a, li, nullptr, 0, cur, ldh, K, K, xs, ws, nxt, ldh, last);
+                else mlp_layer<false, 2, 2>(a, li, nullptr, 0, cur, ldh, K, K, xs, ws, nxt, ldh, last);
+                float* t = cur; cur = nxt; nxt = t;
+            }
         }
     }
 }
@@ -200,16 +243,25 @@ __global__ __launch_bounds__(256) void k_mlp(MlpArgs a) {
 size_t mlp_lds_bytes() { return sizeof(float) * (kTM * kKS + kWMax * kKS + 2 * kTM * (kWMax + 4)); }
 
 hipError_t launch_mlp(const MlpArgs& a, hipStream_t st) {
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mlp),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp_lds_bytes());
-        if (e != hipSuccess) return e;
-        attr_set = true;
+    // the dynamic-LDS opt-in, once per device (the attribute is per device context)
+    static std::atomic<unsigned long long> attr_set{0};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const unsigned long long bit = 1ull << (dev & 63);
+    if (!(attr_set.load(std::memory_order_relaxed) & bit)) {
+        for (const void* f : {reinterpret_cast<const void*>(&k_mlp<false>), reinterpret_cast<const void*>(&k_mlp<true>)}) {
+            e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp_lds_bytes());
+            if (e != hipSuccess) return e;
+        }
+        attr_set.fetch_or(bit, std::memory_order_relaxed);
     }
     const long long grid = (a.rows + kTM - 1) / kTM;
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_mlp, dim3((unsigned)grid), dim3(256), mlp_lds_bytes(), st, a);
+    bool wide = false;
+    for (int i = 1; i <= a.layers; ++i) wide |= a.dims[i] > 128;
+    if (wide) hipLaunchKernelGGL(k_mlp<true>, dim3((unsigned)grid), dim3(256), mlp_lds_bytes(), st, a);
+    else hipLaunchKernelGGL(k_mlp<false>, dim3((unsigned)grid), dim3(256), mlp_lds_bytes(), st, a);
     return hipGetLastError();
 }
 
