@@ -215,6 +215,13 @@ typedef struct ch_mlp {
  * y[rows][dims[L]] = MLP(x[rows][dims[0]]); x and y are device buffers. */
 int ch_mlp_forward(const ch_mlp* net, const float* x, int64_t rows, float* y, void* stream);
 
+/* ch_mlp_forward for the rows whose byte in row_mask (device uint8 [rows]) is non-zero; the other rows of y
+ * are left untouched, and 16-row tiles with no selected row cost next to nothing.  Replaces the SB3 rollout's
+ * predict_values(terminal_observation) for the envs that just reset (OnPolicyAlgorithm.collect_rollouts'
+ * TimeLimit.truncated bootstrap, CTDECattleHerder.py:107-150), evaluated only where it is used. */
+int ch_mlp_forward_masked(const ch_mlp* net, const float* x, int64_t rows, const uint8_t* row_mask, float* y,
+                          void* stream);
+
 /* ch_mlp_forward on a handle's observation buffer: one row per env for CTDE (x = obs [E][R][86]
  * flattened, dims[0] = R*86) or per agent for MARL (x = obs [E][N][86], dims[0] = 86, E*N rows).
  * Input features past an env's NUM_DRONES rows (CTDE) or of agents past NUM_DRONES (MARL) are zero
@@ -260,6 +267,23 @@ int ch_rollout_post(ch_handle* h, const ch_rollout* rb, int32_t t, const float* 
  * last_value [rows] = V(obs after the last step). */
 int ch_rollout_gae(ch_handle* h, const ch_rollout* rb, const float* last_value, float gamma, float gae_lambda,
                    void* stream);
+
+/* The whole collection in one call (the native loop behind cattleherd.rollout.DeviceRolloutBuffer.collect):
+ * for t < n_steps, on `stream`: actor and critic forwards on step->obs (ch_policy_forward), ch_rollout_store,
+ * ch_step with auto-reset and terminal observations, the critic on the terminal observations of the envs that
+ * reset (ch_mlp_forward_masked; skipped with bootstrap_truncated = 0), ch_rollout_post; then the critic on the
+ * last observations and ch_rollout_gae.  Device scratch (caller-owned): */
+typedef struct ch_rollout_io {
+    const ch_step_io* step;    /* the env's step buffers; obs, reward, terminated, truncated, terminal_obs and
+                                  reset_happened are required (actions are env_actions below) */
+    float* mean;               /* [rows][act_dim] */
+    float* value;              /* [rows] */
+    float* terminal_value;     /* [rows] */
+    float* env_actions;        /* [rows][num_drones][4] */
+} ch_rollout_io;
+int ch_rollout_collect(ch_handle* h, const ch_rollout* rb, const ch_rollout_io* io, const ch_mlp* actor,
+                       const ch_mlp* critic, const float* log_std, uint64_t seed, float gamma, float gae_lambda,
+                       int32_t bootstrap_truncated, void* stream);
 
 #ifdef __cplusplus
 }

@@ -23,8 +23,8 @@ PHYSICS = {"pyb": 0, "dyn": 1, "pyb_gnd": 2, "pyb_drag": 3, "pyb_dw": 4, "pyb_gn
 EXPORTS = ("ch_default_config", "ch_create", "ch_destroy", "ch_last_error", "ch_shape", "ch_reset", "ch_reset_with",
            "ch_step",
            "ch_state_size", "ch_get_state", "ch_set_state", "ch_metrics", "ch_metrics_device", "ch_sync",
-           "ch_get_eval", "ch_builtin_spawn_table", "ch_rollout_store", "ch_rollout_post", "ch_rollout_gae",
-           "ch_spawn_table", "ch_mlp_forward", "ch_policy_forward")
+           "ch_get_eval", "ch_builtin_spawn_table", "ch_rollout_store", "ch_rollout_post", "ch_rollout_gae", "ch_rollout_collect",
+           "ch_spawn_table", "ch_mlp_forward", "ch_mlp_forward_masked", "ch_policy_forward")
 CH_ACT_NONE, CH_ACT_TANH, CH_ACT_RELU = 0, 1, 2
 
 
@@ -91,6 +91,7 @@ def lib():
     L.ch_builtin_spawn_table.argtypes = [vp, P(i32), P(i32)]
     L.ch_spawn_table.argtypes = [i32, vp, P(i32), P(i32)]
     L.ch_mlp_forward.argtypes = [P(ChMlp), vp, i64, vp, vp]
+    L.ch_mlp_forward_masked.argtypes = [P(ChMlp), vp, i64, vp, vp, vp]
     L.ch_policy_forward.argtypes = [vp, P(ChMlp), vp, vp, vp]
     for name in EXPORTS:
         if name not in ("ch_last_error",):

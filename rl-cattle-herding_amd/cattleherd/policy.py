@@ -101,8 +101,10 @@ class DevicePolicy:
     def _stream(self):
         return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
 
-    def forward(self, x, out=None):
-        """y[rows, dims[-1]] = MLP(x[rows, dims[0]]) on the device (x float32, contiguous)."""
+    def forward(self, x, out=None, row_mask=None):
+        """y[rows, dims[-1]] = MLP(x[rows, dims[0]]) on the device (x float32, contiguous).  ``row_mask``
+        (uint8/bool [rows] device tensor): only the selected rows are computed and written
+        (ch_mlp_forward_masked)."""
         torch = self.torch
         x = x.to(device=self.device, dtype=torch.float32).contiguous()
         rows = x.numel() // self.dims[0]
@@ -110,6 +112,15 @@ class DevicePolicy:
             raise ValueError(f"input has {x.numel()} floats, not a multiple of {self.dims[0]}")
         if out is None:
             out = torch.empty((rows, self.dims[-1]), dtype=torch.float32, device=self.device)
+        if row_mask is not None:
+            m = row_mask.to(device=self.device, dtype=torch.uint8).contiguous()
+            if m.numel() != rows:
+                raise ValueError(f"row_mask has {m.numel()} entries, not {rows}")
+            self._mask_keep = m
+            L.check(L.lib().ch_mlp_forward_masked(ctypes.byref(self._net), ctypes.c_void_p(x.data_ptr()), rows,
+                                                  ctypes.c_void_p(m.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                                  self._stream()))
+            return out
         L.check(L.lib().ch_mlp_forward(ctypes.byref(self._net), ctypes.c_void_p(x.data_ptr()), rows,
                                        ctypes.c_void_p(out.data_ptr()), self._stream()))
         return out

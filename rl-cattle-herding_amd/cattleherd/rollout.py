@@ -24,6 +24,11 @@ class ChRollout(ctypes.Structure):
                                         "advantages", "returns", "last_episode_starts")]
 
 
+class ChRolloutIO(ctypes.Structure):
+    _fields_ = [("step", ctypes.POINTER(L.ChStepIO))] + \
+        [(k, ctypes.c_void_p) for k in ("mean", "value", "terminal_value", "env_actions")]
+
+
 def _bind():
     lib = L.lib()
     vp, i32, u64, f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint64, ctypes.c_float
@@ -31,7 +36,9 @@ def _bind():
     lib.ch_rollout_store.argtypes = [vp, P, i32, vp, vp, vp, vp, u64, vp, vp]
     lib.ch_rollout_post.argtypes = [vp, P, i32, vp, vp, vp, vp, f32, vp]
     lib.ch_rollout_gae.argtypes = [vp, P, vp, f32, f32, vp]
-    for f in (lib.ch_rollout_store, lib.ch_rollout_post, lib.ch_rollout_gae):
+    lib.ch_rollout_collect.argtypes = [vp, P, ctypes.POINTER(ChRolloutIO), ctypes.POINTER(L.ChMlp),
+                                       ctypes.POINTER(L.ChMlp), vp, u64, f32, f32, i32, vp]
+    for f in (lib.ch_rollout_store, lib.ch_rollout_post, lib.ch_rollout_gae, lib.ch_rollout_collect):
         f.restype = ctypes.c_int
     return lib
 
@@ -63,9 +70,30 @@ class DeviceRolloutBuffer:
         self._lib = _bind()
 
     def collect(self, actor, critic, log_std, seed=0, bootstrap_truncated=True):
-        """SB3 collect_rollouts for n_steps steps of every env, on the device.  ``actor``: DevicePolicy of
-        the action mean (no clip: SB3's action_net output), ``critic``: DevicePolicy of V, ``log_std``:
+        """SB3 collect_rollouts for n_steps steps of every env, on the device, in one native call
+        (ch_rollout_collect: the loop of collect_steps below runs in C++).  ``actor``: DevicePolicy of the
+        action mean (no clip: SB3's action_net output), ``critic``: DevicePolicy of V, ``log_std``:
         float32 [act_dim] device tensor."""
+        b, lib = self.batch, self._lib
+        torch = b.torch
+        log_std = log_std.to(device=b.device, dtype=torch.float32).contiguous()
+        io = ChRolloutIO()
+        io.step = ctypes.pointer(b._io)
+        io.mean, io.value = self.mean.data_ptr(), self.value.data_ptr()
+        io.terminal_value, io.env_actions = self.terminal_value.data_ptr(), self.env_actions.data_ptr()
+        keep = b._io.terminal_obs
+        b._io.terminal_obs = b.terminal_obs.data_ptr()
+        try:
+            L.check(lib.ch_rollout_collect(b.handle, ctypes.byref(self._rb), ctypes.byref(io), ctypes.byref(actor._net),
+                                           ctypes.byref(critic._net), log_std.data_ptr(), int(seed), self.gamma,
+                                           self.gae_lambda, int(bool(bootstrap_truncated)), b._stream()), b.handle)
+        finally:
+            b._io.terminal_obs = keep
+        return self
+
+    def collect_steps(self, actor, critic, log_std, seed=0, bootstrap_truncated=True):
+        """The same collection driven from Python one kernel at a time (the reference loop the native
+        call restates; kept for the parity test)."""
         b, lib, rb = self.batch, self._lib, ctypes.byref(self._rb)
         torch = b.torch
         log_std = log_std.to(device=b.device, dtype=torch.float32).contiguous()
@@ -78,7 +106,8 @@ class DeviceRolloutBuffer:
             b.step(self.env_actions, autoreset=True, terminal_obs=True)
             tv = None
             if bootstrap_truncated:
-                critic.forward(b.terminal_obs.view(b.n_envs, -1), self.terminal_value)
+                # V(terminal obs) only for the envs that just reset (the only rows ch_rollout_post reads)
+                critic.forward(b.terminal_obs.view(b.n_envs, -1), self.terminal_value, row_mask=b.reset_happened)
                 tv = self.terminal_value.data_ptr()
             L.check(lib.ch_rollout_post(b.handle, rb, t, b.reward.data_ptr(), b.terminated.data_ptr(),
                                         b.truncated.data_ptr(), tv, self.gamma, b._stream()), b.handle)

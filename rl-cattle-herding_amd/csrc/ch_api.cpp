@@ -711,6 +711,20 @@ int ch_mlp_forward(const ch_mlp* net, const float* x, int64_t rows, float* y, vo
     return CH_OK;
 }
 
+int ch_mlp_forward_masked(const ch_mlp* net, const float* x, int64_t rows, const uint8_t* row_mask, float* y,
+                          void* stream) {
+    MlpArgs a;
+    std::string err;
+    const int rc = mlp_args(net, x, rows, y, a, err);
+    if (rc) return fail(nullptr, rc, "ch_mlp_forward_masked: " + err);
+    if (!row_mask) return fail(nullptr, CH_ERR_INVALID, "ch_mlp_forward_masked: NULL row mask");
+    a.row_mask = row_mask;
+    const hipError_t e = launch_mlp(a, (hipStream_t)stream);
+    if (e != hipSuccess)
+        return fail(nullptr, CH_ERR_DEVICE, std::string("ch_mlp_forward_masked launch: ") + hipGetErrorString(e));
+    return CH_OK;
+}
+
 int ch_policy_forward(ch_handle* h, const ch_mlp* net, const float* obs, float* y, void* stream) {
     if (!h) return fail(nullptr, CH_ERR_INVALID, "ch_policy_forward: NULL handle");
     const bool marl = h->cfg.mode == CH_MODE_MARL;
@@ -792,6 +806,45 @@ int ch_rollout_gae(ch_handle* h, const ch_rollout* rb, const float* last_value, 
     HIP_TRY(h, hipSetDevice(h->device));
     HIP_TRY(h, launch_rollout(a, 2, (hipStream_t)stream));
     return CH_OK;
+}
+
+int ch_rollout_collect(ch_handle* h, const ch_rollout* rb, const ch_rollout_io* io, const ch_mlp* actor,
+                       const ch_mlp* critic, const float* log_std, uint64_t seed, float gamma, float gae_lambda,
+                       int32_t bootstrap_truncated, void* stream) {
+    RolloutArgs ra;
+    int rc = rollout_args(h, rb, ra, "ch_rollout_collect");
+    if (rc) return rc;
+    if (!io || !io->step || !io->mean || !io->value || !io->env_actions || !log_std || !actor || !critic)
+        return fail(h, CH_ERR_INVALID, "ch_rollout_collect: NULL argument");
+    const ch_step_io* sio = io->step;
+    if (!sio->obs || !sio->reward || !sio->terminated || !sio->truncated || !sio->terminal_obs || !sio->reset_happened ||
+        (bootstrap_truncated && !io->terminal_value))
+        return fail(h, CH_ERR_INVALID, "ch_rollout_collect: the step buffers (obs, reward, terminated, truncated, "
+                                       "terminal_obs, reset_happened) and terminal_value are required");
+    if (actor->dims[actor->n_layers] != rb->act_dim || critic->dims[critic->n_layers] != 1)
+        return fail(h, CH_ERR_INVALID, "ch_rollout_collect: actor output must be act_dim wide, critic output 1");
+    hipStream_t st = (hipStream_t)stream;
+    ch_step_io s = *sio;
+    s.actions = io->env_actions; s.actions_out = nullptr;
+    s.flags = (s.flags & ~CH_STEP_RANDOM_ACTIONS) | CH_STEP_AUTORESET;
+    for (int32_t t = 0; t < rb->n_steps; ++t) {
+        // SB3 collect_rollouts, one step of every env: policy(obs) -> sample, log-prob, value -> env.step ->
+        // bootstrap truncated rewards with V(terminal obs) -> buffer (OnPolicyAlgorithm.collect_rollouts)
+        if ((rc = ch_policy_forward(h, actor, sio->obs, io->mean, stream))) return rc;
+        if ((rc = ch_policy_forward(h, critic, sio->obs, io->value, stream))) return rc;
+        if ((rc = ch_rollout_store(h, rb, t, sio->obs, io->mean, io->value, log_std, seed, io->env_actions, stream)))
+            return rc;
+        if ((rc = ch_step(h, &s, stream))) return rc;
+        if (bootstrap_truncated &&
+            (rc = ch_mlp_forward_masked(critic, sio->terminal_obs, h->E, sio->reset_happened, io->terminal_value, stream)))
+            return fail(h, rc, "ch_rollout_collect: " + std::string(ch_last_error(nullptr)));
+        if ((rc = ch_rollout_post(h, rb, t, sio->reward, sio->terminated, sio->truncated,
+                                  bootstrap_truncated ? io->terminal_value : nullptr, gamma, stream)))
+            return rc;
+    }
+    if ((rc = ch_policy_forward(h, critic, sio->obs, io->value, stream))) return rc;
+    (void)st;
+    return ch_rollout_gae(h, rb, io->value, gamma, gae_lambda, stream);
 }
 
 int ch_metrics(ch_handle* h, double* out, int32_t reset_after, void* stream) {

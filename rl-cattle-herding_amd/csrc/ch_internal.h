@@ -141,6 +141,7 @@ struct MlpArgs {
     long long rows;
     float* y;
     const int* env_n;          // optional: NUM_DRONES per env (handle envi row 0) -> live input width
+    const uint8_t* row_mask;   // optional: only rows with a non-zero byte are computed and written
     long long rows_per_env;    // 1: CTDE (live width n * k_unit); N: MARL (agent j live iff j < n)
     int k_unit;
 };

@@ -42,7 +42,7 @@ __device__ __forceinline__ float act_fn(float v, int act) {
 // TW = 16-column tiles per wave (the layer's tiles rounded up to 4 TW): every wave runs the same
 // straight-line MFMA sequence; tiles past the layer width multiply zero weight rows (a branch per
 // tile would make the compiler shuffle the accumulators around every MFMA).
-template <bool AG, int TW, int DEPTH>
+template <bool AG, int TW, int DEPTH, int NW>
 __device__ __forceinline__ void mlp_layer(const MlpArgs& a, int li, const float* __restrict__ Ag, long long lda,
                                           const float* Al, int ldl, int K, int kloop, float* xs, float* ws, float* out,
                                           int ldo, bool last) {
@@ -71,19 +71,19 @@ __device__ __forceinline__ void mlp_layer(const MlpArgs& a, int li, const float*
 #define CH_MLP_FETCH(S, kc_)                                                                                        \
     do {                                                                                                            \
         const int kcf = (kc_);                                                                                      \
-        if constexpr (AG) {                                                                                         \
+        if (AG && tid < 256) {                                                                                      \
             const int r = tid >> 4, c = (tid & 15) * 4;                                                             \
             const float* src = Ag + min(row0 + r, a.rows - 1) * lda;                                                \
             _Pragma("unroll") for (int q = 0; q < 4; ++q) xr[S][q] = src[min(kcf + c + q, K - 1)];                  \
         }                                                                                                           \
         if (vec) {                                                                                                  \
             _Pragma("unroll") for (int i = 0; i < kWP; ++i) {                                                       \
-                const int n = wn0 + 16 * i, k = kcf + wc;                                                           \
+                const int n = wn0 + 4 * NW * i, k = kcf + wc;                                                           \
                 wr[S][i] = *reinterpret_cast<const float4*>(W + min(n, N - 1) * K + min(k, K - 4));                 \
             }                                                                                                       \
         } else {                                                                                                    \
             _Pragma("unroll") for (int i = 0; i < kWP; ++i) {                                                       \
-                const int n = wn0 + 16 * i, k = kcf + wc;                                                           \
+                const int n = wn0 + 4 * NW * i, k = kcf + wc;                                                           \
                 const float* src = W + min(n, N - 1) * K;                                                           \
                 wr[S][i] = make_float4(src[min(k, K - 1)], src[min(k + 1, K - 1)], src[min(k + 2, K - 1)],         \
                                        src[min(k + 3, K - 1)]);                                                     \
@@ -97,7 +97,7 @@ __device__ __forceinline__ void mlp_layer(const MlpArgs& a, int li, const float*
     if constexpr (S < DEPTH) {                                                                                      \
         const int c = c0 + S, kc = c * kKC;                                                                         \
         if (c < nch) {                                                                                              \
-            if constexpr (AG) {                                                                                     \
+            if (AG && tid < 256) {                                                                                  \
                 const int r = tid >> 4, cc = (tid & 15) * 4;                                                        \
                 const bool rv = row0 + r < a.rows;                                                                  \
                 float xq[4];                                                                                        \
@@ -105,7 +105,7 @@ __device__ __forceinline__ void mlp_layer(const MlpArgs& a, int li, const float*
                 *reinterpret_cast<float4*>(xs + r * kKS + cc) = make_float4(xq[0], xq[1], xq[2], xq[3]);            \
             }                                                                                                       \
             _Pragma("unroll") for (int i = 0; i < kWP; ++i) {                                                       \
-                const int n = wn0 + 16 * i, k = kc + wc;                                                            \
+                const int n = wn0 + 4 * NW * i, k = kc + wc;                                                            \
                 const bool nv = n < N;                                                                              \
                 const float4 v = wr[S][i];                                                                          \
                 *reinterpret_cast<float4*>(ws + n * kKS + wc) =                                                     \
@@ -120,7 +120,7 @@ __device__ __forceinline__ void mlp_layer(const MlpArgs& a, int li, const float*
                 if constexpr (AG) av[ks] = xs[(lane & 15) * kKS + kk];                                              \
                 else av[ks] = Al[(lane & 15) * ldl + kc + kk];                                                      \
                 _Pragma("unroll") for (int j = 0; j < TW; ++j)                                                      \
-                    bv[j][ks] = ws[((wave + 4 * j) * 16 + (lane & 15)) * kKS + kk];                                 \
+                    bv[j][ks] = ws[((wave + NW * j) * 16 + (lane & 15)) * kKS + kk];                                 \
             }                                                                                                       \
             _Pragma("unroll") for (int ks = 0; ks < kKC / 4; ++ks) {                                                \
                 _Pragma("unroll") for (int j = 0; j < TW; ++j)                                                      \
@@ -150,7 +150,7 @@ __device__ __forceinline__ void mlp_layer(const MlpArgs& a, int li, const float*
     // epilogue: C/D map col = lane & 15, row = 4 (lane >> 4) + r
 #pragma unroll
     for (int j = 0; j < TW; ++j) {
-        const int t = wave + 4 * j;
+        const int t = wave + NW * j;
         if (t >= nt) continue;
         const int col = t * 16 + (lane & 15);
         const float bv = col < N && bias ? bias[col] : 0.0f;
@@ -160,14 +160,14 @@ __device__ __forceinline__ void mlp_layer(const MlpArgs& a, int li, const float*
             float v = acc[j][r] + bv;
             if (!last) {
                 out[row * ldo + col] = col < N ? act_fn(v, a.hidden_act) : 0.0f;
-            } else if (col < N && row0 + row < a.rows) {
+            } else if (col < N && row0 + row < a.rows && (!a.row_mask || a.row_mask[row0 + row])) {
                 if (a.clip) v = fminf(fmaxf(v, a.lo), a.hi);
                 a.y[(row0 + row) * (long long)N + col] = v;
             }
         }
     }
     if (!last) {   // columns past this layer's tiles: zero for the next layer's chunk reads
-        for (int idx = tid; idx < kTM * (kWMax - 16 * nt); idx += 256) {
+        for (int idx = tid; idx < kTM * (kWMax - 16 * nt); idx += 64 * NW) {
             const int r = idx / (kWMax - 16 * nt), c = 16 * nt + idx - r * (kWMax - 16 * nt);
             out[r * ldo + c] = 0.0f;
         }
@@ -183,7 +183,8 @@ __device__ __forceinline__ void mlp_layer(const MlpArgs& a, int li, const float*
 // layout, no LDS staging: 85 us for one 16-row tile of the 1032-wide forward vs 35 us, the 16-row x
 // 64-byte operand loads being far slower than the coalesced staging loads.)
 template <bool WIDE>
-__global__ __launch_bounds__(256) void k_mlp(MlpArgs a) {
+__global__ __launch_bounds__(WIDE ? 256 : 512) void k_mlp(MlpArgs a) {
+    constexpr int NW = WIDE ? 4 : 8;   // waves: the narrow kernel gives every wave one 16-column tile
     extern __shared__ __align__(16) float sm[];
     float* xs = sm;                                  // [16][kKS]
     float* ws = xs + kTM * kKS;                      // [kWMax][kKS]
@@ -205,7 +206,11 @@ __global__ __launch_bounds__(256) void k_mlp(MlpArgs a) {
         }
         atomicMax(&kmax, k);
     }
-    __syncthreads();
+    // masked forward: a tile with no selected row has nothing to do (the usual case for the terminal-value
+    // forward of a rollout, where only the envs that just reset are selected)
+    const bool any = __syncthreads_or(a.row_mask && threadIdx.x < kTM && row0 + threadIdx.x < a.rows &&
+                                      a.row_mask[row0 + threadIdx.x] != 0);
+    if (a.row_mask && !any) return;
     const int kloop0 = kmax;
     float* cur = h0;
     float* nxt = h1;
@@ -214,24 +219,22 @@ __global__ __launch_bounds__(256) void k_mlp(MlpArgs a) {
         const int nt = (a.dims[li + 1] + 15) >> 4;
         if constexpr (WIDE) {
             if (li == 0) {
-                if (nt <= 4) mlp_layer<true, 1, 1>(a, 0, a.x, a.dims[0], nullptr, 0, a.dims[0], kloop0, xs, ws, cur, ldh, last);
-                else if (nt > 8) mlp_layer<true, 4, 1>(a, 0, a.x, a.dims[0], nullptr, 0, a.dims[0], kloop0, xs, ws, cur, ldh, last);
-                else mlp_layer<true, 2, 1>(a, 0, a.x, a.dims[0], nullptr, 0, a.dims[0], kloop0, xs, ws, cur, ldh, last);
+                if (nt <= 4) mlp_layer<true, 1, 1, NW>(a, 0, a.x, a.dims[0], nullptr, 0, a.dims[0], kloop0, xs, ws, cur, ldh, last);
+                else if (nt > 8) mlp_layer<true, 4, 1, NW>(a, 0, a.x, a.dims[0], nullptr, 0, a.dims[0], kloop0, xs, ws, cur, ldh, last);
+                else mlp_layer<true, 2, 1, NW>(a, 0, a.x, a.dims[0], nullptr, 0, a.dims[0], kloop0, xs, ws, cur, ldh, last);
             } else {
                 const int K = a.dims[li];
-                if (nt <= 4) mlp_layer<false, 1, 1>(a, li, nullptr, 0, cur, ldh, K, K, xs, ws, nxt, ldh, last);
-                else if (nt > 8) mlp_layer<false, 4, 1>(a, li, nullptr, 0, cur, ldh, K, K, xs, ws, nxt, ldh, last);
-                else mlp_layer<false, 2, 1>(a, li, nullptr, 0, cur, ldh, K, K, xs, ws, nxt, ldh, last);
+                if (nt <= 4) mlp_layer<false, 1, 1, NW>(a, li, nullptr, 0, cur, ldh, K, K, xs, ws, nxt, ldh, last);
+                else if (nt > 8) mlp_layer<false, 4, 1, NW>(a, li, nullptr, 0, cur, ldh, K, K, xs, ws, nxt, ldh, last);
+                else mlp_layer<false, 2, 1, NW>(a, li, nullptr, 0, cur, ldh, K, K, xs, ws, nxt, ldh, last);
                 float* t = cur; cur = nxt; nxt = t;
             }
-        } else {   // two chunks in flight (a deeper ring measured no faster: 3 chunks 27.5 us vs 2 chunks 24.8)
+        } else {   // 8 waves, one tile each; two chunks in flight (3 measured no faster)
             if (li == 0) {
-                if (nt <= 4) mlp_layer<true, 1, 2>(a, 0, a.x, a.dims[0], nullptr, 0, a.dims[0], kloop0, xs, ws, cur, ldh, last);
-                else mlp_layer<true, 2, 2>(a, 0, a.x, a.dims[0], nullptr, 0, a.dims[0], kloop0, xs, ws, cur, ldh, last);
+                mlp_layer<true, 1, 2, NW>(a, 0, a.x, a.dims[0], nullptr, 0, a.dims[0], kloop0, xs, ws, cur, ldh, last);
             } else {
                 const int K = a.dims[li];
-                if (nt <= 4) mlp_layer<false, 1, 2>(a, li, nullptr, 0, cur, ldh, K, K, xs, ws, nxt, ldh, last);
-                else mlp_layer<false, 2, 2>(a, li, nullptr, 0, cur, ldh, K, K, xs, ws, nxt, ldh, last);
+                mlp_layer<false, 1, 2, NW>(a, li, nullptr, 0, cur, ldh, K, K, xs, ws, nxt, ldh, last);
                 float* t = cur; cur = nxt; nxt = t;
             }
         }
@@ -261,7 +264,7 @@ hipError_t launch_mlp(const MlpArgs& a, hipStream_t st) {
     bool wide = false;
     for (int i = 1; i <= a.layers; ++i) wide |= a.dims[i] > 128;
     if (wide) hipLaunchKernelGGL(k_mlp<true>, dim3((unsigned)grid), dim3(256), mlp_lds_bytes(), st, a);
-    else hipLaunchKernelGGL(k_mlp<false>, dim3((unsigned)grid), dim3(256), mlp_lds_bytes(), st, a);
+    else hipLaunchKernelGGL(k_mlp<false>, dim3((unsigned)grid), dim3(512), mlp_lds_bytes(), st, a);
     return hipGetLastError();
 }
 

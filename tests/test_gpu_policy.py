@@ -120,3 +120,26 @@ def test_policy_rollout_matches_host_policy_loop():
         b.step(a, autoreset=True)
     assert worst < 5e-5, worst
     b.close()
+
+
+@pytest.mark.parametrize("dims,rows", [((1032, 128, 128, 1), 4096), ((86, 256, 256, 8), 1000)])
+def test_masked_forward_computes_selected_rows_only(dims, rows):
+    """ch_mlp_forward_masked: selected rows equal the unmasked forward bit for bit, the others keep what
+    the output buffer held; an all-zero mask writes nothing (the rollout's terminal-value forward)."""
+    import torch
+    from cattleherd.policy import DevicePolicy
+    pol = DevicePolicy(DevicePolicy.random_layers(dims, seed=5), "tanh", None)
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(rows, dims[0], generator=g).cuda()
+    full = pol.forward(x)
+    mask = (torch.rand(rows, generator=g) < 0.02).to(torch.uint8).cuda()
+    mask[3] = 1
+    out = torch.full((rows, dims[-1]), 123.0, device="cuda")
+    pol.forward(x, out, row_mask=mask)
+    none = torch.full((rows, dims[-1]), -7.0, device="cuda")
+    pol.forward(x, none, row_mask=torch.zeros(rows, dtype=torch.uint8, device="cuda"))
+    torch.cuda.synchronize()
+    sel = mask.bool()
+    assert torch.equal(out[sel], full[sel])
+    assert torch.all(out[~sel] == 123.0)
+    assert torch.all(none == -7.0)

@@ -87,3 +87,31 @@ def test_rollout_buffer_matches_sb3_semantics():
     assert np.allclose(rb.returns.cpu().numpy(), ret, rtol=2e-6, atol=2e-6)
     b.close()
     b2.close()
+
+
+def test_native_collect_equals_python_loop():
+    """ch_rollout_collect (the loop in C++) and collect_steps (the same kernels launched from Python) fill
+    identical buffers, across auto-resets and truncation bootstraps."""
+    import torch
+    from cattleherd.env import HerdBatch
+    from cattleherd.policy import DevicePolicy
+    from cattleherd.rollout import DeviceRolloutBuffer
+    E, T, n, m = 256, 24, 4, 16
+    sc = 4800 - 12 + (np.arange(E) % 24)
+    bufs = []
+    for native in (True, False):
+        b = HerdBatch(E, n, m, mode="ctde", curriculum_level=2)
+        b.reset()
+        b.set_state({"step_counter": sc})
+        actor = DevicePolicy(DevicePolicy.random_layers([12 * 86, 128, 128, 4 * n], seed=1), "tanh", None)
+        critic = DevicePolicy(DevicePolicy.random_layers([12 * 86, 128, 128, 1], seed=2), "tanh", None)
+        rb = DeviceRolloutBuffer(b, T)
+        log_std = torch.full((4 * n,), -1.0, device=b.device)
+        (rb.collect if native else rb.collect_steps)(actor, critic, log_std, seed=9)
+        torch.cuda.synchronize()
+        bufs.append({k: getattr(rb, k).cpu() for k in ("obs", "actions", "rewards", "episode_starts", "values",
+                                                        "log_probs", "advantages", "returns")})
+        assert rb.episode_starts[1:].sum() > 0
+        b.close()
+    for k in bufs[0]:
+        assert torch.equal(bufs[0][k], bufs[1][k]), k
