@@ -1,0 +1,100 @@
+"""Parity at the BASELINE sizes themselves (-m gpu): configs[3]'s 4096 envs x (4 drones, 16 cattle) after
+a long random rollout, spot-checked env by env against the fp64 oracle for one step, and configs[0]'s single
+env with one drone and 4 cattle (the reference's CPU case; compat = 0, since one drone in compat mode is the
+reference's own ValueError), stepped in lockstep with the oracle.  Tolerances as in test_gpu_parity.py: obs
+rtol 1e-6 / atol 1e-7 (the f32 output cast), reward rtol 1e-6, state 1e-9, flags exact."""
+import numpy as np
+import pytest
+
+from helpers import close, stack
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_view(g, e, nmax):
+    out = {}
+    for k, v in g.items():
+        x = np.asarray(v[e])
+        if k in ("drone_pos", "drone_quat", "drone_vel", "drone_angv", "pid_last_rpy", "pid_int_pos", "pid_int_rpy",
+                 "last_rpm", "rpy_rates", "active"):
+            pad = np.zeros((nmax,) + x.shape[1:], x.dtype)
+            pad[:x.shape[0]] = x
+            if k == "drone_quat":
+                pad[x.shape[0]:, 3] = 1
+            x = pad
+        out[k] = x
+    return out
+
+
+def test_configs3_full_size_spot_parity():
+    """4096 envs, 300 device-drawn random steps with auto-reset, then one step with host actions; 64 envs
+    (a fixed random sample, incl. the first and last workgroup) re-run that step on the oracle from the
+    device state before it."""
+    import torch
+    import oracle as O
+    from cattleherd._lib import spawn_table
+    from cattleherd.env import HerdBatch
+    E, n, m = 4096, 4, 16
+    b = HerdBatch(E, n, m)
+    b.reset()
+    for _ in range(300):
+        b.step(random_actions=True, autoreset=True)
+    torch.cuda.synchronize()
+    g = b.get_state()
+    rng = np.random.default_rng(11)
+    pick = np.unique(np.concatenate([[0, 1, 15, 16, E - 16, E - 1], rng.choice(E, 58, replace=False)]))
+    acts = rng.uniform(-1, 1, (E, n, 4)).astype(np.float32)
+    obs, rew, te, tr = b.step(torch.tensor(acts, device=b.device), autoreset=True)
+    torch.cuda.synchronize()
+    obs, rew, te, tr = obs.cpu().numpy(), rew.cpu().numpy(), te.cpu().numpy(), tr.cpu().numpy()
+    after = b.get_state()
+    table = spawn_table(m)
+    for e in pick:
+        env = O.Env(0, n, m, table, env_id=int(e))
+        env.set_state(_oracle_view(g, e, O.NMAX))
+        env.st.episode = int(g["episode"][e])   # (set_state leaves the reset counter to the env's own resets)
+        o, r, t1, t2, done, _ = env.step(acts[e], autoreset=True)
+        assert close(obs[e], np.asarray(o).reshape(obs[e].shape), 1e-6, 1e-7)[0], e
+        assert close(rew[e], np.asarray(r, np.float32).reshape(rew[e].shape), 1e-6, 1e-6)[0], e
+        assert np.array_equal(te[e], np.asarray(t1).reshape(te[e].shape)), e
+        assert np.array_equal(tr[e], np.asarray(t2).reshape(tr[e].shape)), e
+        want = env.get_state()
+        for k in ("drone_pos", "drone_quat", "drone_vel", "drone_angv"):
+            assert close(after[k][e][:n], want[k][:n], 1e-9, 1e-9)[0], (e, k)
+        assert close(after["cow_pos"][e], want["cow_pos"][:m], 1e-12, 1e-13)[0], e
+        assert close(after["cow_vel"][e], want["cow_vel"][:m], 1e-9, 1e-12)[0], e
+        assert int(after["step_counter"][e]) == int(want["step_counter"]), e
+    assert len(pick) >= 60
+    b.close()
+
+
+def test_configs0_one_env_one_drone_lockstep():
+    """configs[0]: 1 env x (1 drone, 4 cattle), compat = 0 (NaN-safe spacing terms with a single drone),
+    240 device-drawn random steps with auto-reset, the oracle taking the device state before every step."""
+    import torch
+    import oracle as O
+    from cattleherd._lib import spawn_table
+    from cattleherd.env import HerdBatch
+    n, m, T = 1, 4, 240
+    b = HerdBatch(1, n, m, compat=False)
+    b.reset()
+    table = spawn_table(m)
+    env = O.Env(0, n, m, table, env_id=0, compat=False)
+    o0 = env.reset()
+    assert close(b.obs.cpu().numpy()[0], np.asarray(o0).reshape(12, 86), 1e-6, 1e-7)[0]
+    for t in range(T):
+        g = b.get_state()
+        env.set_state(_oracle_view(g, 0, O.NMAX))
+        env.st.episode = int(g["episode"][0])
+        b.step(random_actions=True, autoreset=True)
+        torch.cuda.synchronize()
+        a = env.random_actions(t)
+        assert np.array_equal(a, b.actions.cpu().numpy()[0]), t
+        o, r, te, tr, done, _ = env.step(a, autoreset=True)
+        assert close(b.obs.cpu().numpy()[0], np.asarray(o).reshape(12, 86), 1e-6, 1e-7)[0], t
+        rr = b.reward.cpu().numpy()[0]
+        assert np.isfinite(rr).all(), t
+        assert close(rr, np.asarray(r, np.float32).reshape(rr.shape), 1e-6, 1e-6)[0], t
+        assert bool(b.terminated.cpu().numpy()[0][0]) == bool(np.asarray(te).ravel()[0]), t
+        assert bool(b.truncated.cpu().numpy()[0][0]) == bool(np.asarray(tr).ravel()[0]), t
+    b.close()
