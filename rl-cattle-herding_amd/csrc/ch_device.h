@@ -542,10 +542,32 @@ __device__ __forceinline__ void variant_substeps(const StepParams<R>& p, int bas
 // ---- flocking: MathematicalFlock (flockUtils.py:11-382) ----------------------------------------
 constexpr double kEps = 0.1, kH = 0.2;
 template <class R> __device__ __forceinline__ R sigma_norm_n(R n) { return divc(sqrt(R(1) + R(kEps) * (n * n)) - R(1), R(kEps)); }
+// cos(x) for 0 <= x <= pi (the bump's argument): x = n pi/2 + r with n = round(x / (pi/2)) in {0, 1, 2} and
+// |r| <= pi/4 (Cody-Waite: pi/2 in three parts, each product exact), then the fdlibm kernels
+// (sincos_small): cos r, -sin r, -cos r.  <= 1 ulp like libm (tools/sincos_check.c), without the generic
+// reduction of the libm entry point.
+template <class R> __device__ __forceinline__ R cos_0pi(R x) {
+    if constexpr (sizeof(R) == 8) {
+        const double PIO2_1 = 1.57079632673412561417e+00, PIO2_2 = 6.07710050630396597660e-11,
+                     PIO2_3 = 2.02226624871116645580e-21;   // fdlibm pio2_1, pio2_2, pio2_3
+        const double n = rint(x * 6.36619772367581382433e-01);
+        const double r = ((x - n * PIO2_1) - n * PIO2_2) - n * PIO2_3;
+        double s, c;
+        sincos_small(fabs(r), &s, &c);
+        s = r < 0 ? -s : s;
+        return n == 0.0 ? c : (n == 1.0 ? -s : -c);
+    } else {
+        return cosf(x);
+    }
+}
 template <class R> __device__ __forceinline__ R bump(R z) {
     if (z < R(0)) return R(0);
     if (z < R(kH)) return R(1);
+#ifdef CH_OCML_COS
     if (z <= R(1)) return (R(1) + m_cos(divc(R(kPi) * (z - R(kH)), R(1) - R(kH)))) / R(2);
+#else
+    if (z <= R(1)) return (R(1) + cos_0pi(divc(R(kPi) * (z - R(kH)), R(1) - R(kH)))) / R(2);
+#endif
     return R(0);
 }
 template <class R> __device__ __forceinline__ R sigma_1(R z) { return z / sqrt(R(1) + z * z); }

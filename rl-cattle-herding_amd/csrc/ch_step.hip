@@ -40,6 +40,7 @@ enum { F_D = 0, F_T, F_H, F_A, F_E, F_R, F_X0, F_X1, F_X2,     // hand-off count
        Q_LEN, C_QUEUE, F_C,                                       // shared alpha queue: length, grab, cheap pass done
        C_EULER,                                                   // Euler angles of the new attitudes (cow waves)
        V_DSIMD,                                                   // 1 + the SIMD the drone wave runs on
+       F_S, C_SPC, C_SCAT,                                        // split: drone reward terms done on the cow waves
        FLAG_COUNT };
 static_assert(FLAG_COUNT <= kV2Flags, "LDS flag words");
 // after the per-env rows: flocking-env list [G], reset-env list [G], their counts, then the counters
@@ -294,6 +295,32 @@ __device__ __forceinline__ int nearest_two(const R* dx, const R* dy, int b0, int
     return (i1 + 1) | ((i2 + 1) << 8);
 }
 
+// spacing reward terms of drone slot u from its two nearest-neighbour distances (CattleAviary.py:230-246,
+// 572-679): simple and complex spacing of both, and the drone's spacing reward
+template <class R>
+__device__ __forceinline__ void spacing_terms(V2Smem<R>& S, const Level& Lv, bool compat, int u, R m1, R m2) {
+    const R sa = simple_spacing(m1, Lv), sb = simple_spacing(m2, Lv);
+    const R ca = complex_spacing(m1, Lv), cb = complex_spacing(m2, Lv);
+    R ps = 0;   // per-drone spacing reward (CattleAviary.py:238-246)
+    if (compat || m1 < R(INFINITY)) ps += (ca + sa) / R(2.0);
+    if (compat || m2 < R(INFINITY)) ps += (cb + sb) / R(2.0);
+    S.sa[u] = sa; S.sb[u] = sb; S.ca[u] = ca; S.cb[u] = cb; S.psp[u] = ps;
+}
+
+// closest cow of drone slot u (CattleAviary.py:248-252) from the cow waves' distance table -> cattle term:
+// min over cows of |y - q|^2, then one square root (sqrt is correctly rounded and monotonic, so this is
+// the minimum of the distances; a NaN entry is skipped either way)
+template <class R>
+__device__ __forceinline__ R cattle_term(const V2Smem<R>& S, int u, int M, R cc) {
+    const R* dc = S.dcow + u * M;
+    R best = R(INFINITY);
+    for (int j = 0; j < M; ++j) {
+        const R d = dc[j];
+        if (d < best) best = d;
+    }
+    return cattle_spacing(sqrt(best), cc);
+}
+
 // flock alpha term, pair form, for every flocking env (flockUtils.py:237-258, 327-337; MathUtils 11-58):
 // one table of the workgroup's unordered cow pairs, evaluated in the bump's support only.  The bump is
 // exactly 0 for sigma_norm(|z|) / r_alpha > 1 (beyond the lattice range d_alpha = 1.2 m); such a pair adds
@@ -374,25 +401,25 @@ __device__ __forceinline__ void alpha_row(V2Smem<R>& S, int M, int P, int u, int
     const R C2A = R(2 * 1.7320508075688772);
     R gx = 0, gy = 0, cxx = 0, cyy = 0, ux = 0, uy = 0;
     const int pb = g * P;
-    // four neighbours per round: their table loads are issued together, then summed in neighbour order
+    // Four neighbours per round, branch-free: the table loads of a round are issued together (an empty slot
+    // reads the env's first pair), then summed in neighbour order.  An empty slot adds +0, which leaves the
+    // sum unchanged: it starts at +0 and a round-to-nearest sum is -0 only if both addends are.
     for (unsigned long long m = S.nbm[u]; m;) {
         R t[4][4];
         bool v[4], fwd[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             v[r] = m != 0;
-            const int k = v[r] ? __ffsll((long long)m) - 1 : j + 1;
+            const int k = __ffsll((long long)m) - 1;
             m &= m - 1;
             fwd[r] = j < k;
-            const int idx = pb + (fwd[r] ? tri(j, k, M) : tri(k, j, M));
-            t[r][0] = t[r][1] = t[r][2] = t[r][3] = R(0);
-            if (v[r]) { t[r][0] = S.tgx[idx]; t[r][1] = S.tgy[idx]; t[r][2] = S.tcx[idx]; t[r][3] = S.tcy[idx]; }
+            const int idx = v[r] ? pb + tri(min(j, k), max(j, k), M) : pb;
+            t[r][0] = S.tgx[idx]; t[r][1] = S.tgy[idx]; t[r][2] = S.tcx[idx]; t[r][3] = S.tcy[idx];
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            if (!v[r]) break;
-            gx += fwd[r] ? t[r][0] : -t[r][0]; gy += fwd[r] ? t[r][1] : -t[r][1];
-            cxx += fwd[r] ? t[r][2] : -t[r][2]; cyy += fwd[r] ? t[r][3] : -t[r][3];
+            gx += v[r] ? (fwd[r] ? t[r][0] : -t[r][0]) : R(0); gy += v[r] ? (fwd[r] ? t[r][1] : -t[r][1]) : R(0);
+            cxx += v[r] ? (fwd[r] ? t[r][2] : -t[r][2]) : R(0); cyy += v[r] ? (fwd[r] ? t[r][3] : -t[r][3]) : R(0);
         }
     }
     if (S.hasnb[u]) { ux = C2A * gx + C2A * cxx; uy = C2A * gy + C2A * cyy; }
@@ -461,49 +488,45 @@ __device__ __forceinline__ void alpha_row_pw(V2Smem<R>& S, int M, int P, int g, 
     const int u = g * M + j;
     R gx = 0, gy = 0, cxx = 0, cyy = 0, ux = 0, uy = 0;
     const R pjx = S.cvx[u], pjy = S.cvy[u];
-    // four neighbours per round: their loads are issued together, then summed in neighbour order
+    // four neighbours per round, branch-free as in alpha_row (an empty slot reads pair 0 / cow j, adds +0)
     for (unsigned long long m = S.nbm[u]; m;) {
         R t[4][5];
         bool v[4], fwd[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             v[r] = m != 0;
-            const int k = v[r] ? __ffsll((long long)m) - 1 : j + 1;
+            const int k = v[r] ? __ffsll((long long)m) - 1 : j;
             m &= m - 1;
             fwd[r] = j < k;
-            const int idx = fwd[r] ? tri(j, k, M) : tri(k, j, M);
-            t[r][0] = t[r][1] = t[r][2] = t[r][3] = t[r][4] = R(0);
-            if (v[r]) {
-                t[r][0] = tb[idx]; t[r][1] = tb[P + idx]; t[r][2] = tb[2 * P + idx];
-                t[r][3] = S.cvx[g * M + k]; t[r][4] = S.cvy[g * M + k];
-            }
+            const int idx = v[r] ? tri(min(j, k), max(j, k), M) : 0;
+            t[r][0] = tb[idx]; t[r][1] = tb[P + idx]; t[r][2] = tb[2 * P + idx];
+            t[r][3] = S.cvx[g * M + k]; t[r][4] = S.cvy[g * M + k];
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            if (!v[r]) break;
             const R b = t[r][2], pkx = t[r][3], pky = t[r][4];
             const R dvx = fwd[r] ? pkx - pjx : pjx - pkx, dvy = fwd[r] ? pky - pjy : pjy - pky;
             const R tcx = b * dvx, tcy = b * dvy;
-            gx += fwd[r] ? t[r][0] : -t[r][0]; gy += fwd[r] ? t[r][1] : -t[r][1];
-            cxx += fwd[r] ? tcx : -tcx; cyy += fwd[r] ? tcy : -tcy;
+            gx += v[r] ? (fwd[r] ? t[r][0] : -t[r][0]) : R(0); gy += v[r] ? (fwd[r] ? t[r][1] : -t[r][1]) : R(0);
+            cxx += v[r] ? (fwd[r] ? tcx : -tcx) : R(0); cyy += v[r] ? (fwd[r] ? tcy : -tcy) : R(0);
         }
     }
     if (S.hasnb[u]) { ux = C2A * gx + C2A * cxx; uy = C2A * gy + C2A * cyy; }
     S.aux[u] = ux; S.auy[u] = uy;
 }
 
-// shepherd (delta, flockUtils.py:271-317) and predator (343-348) terms of drone k on cow u = g*M + j,
-// one (cow, drone) item per lane; stored in the term table for flock_combine.
+// shepherd (delta, flockUtils.py:271-317) and predator (343-348) terms of drone k on cow u = g*M + j:
+// t[0..3] the delta gradient and consensus parts, t[4..5] the predator push; returns in-range | predator << 1
 template <class R>
-__device__ __forceinline__ void delta_term(V2Smem<R>& S, int N, int u, int g, int k, R* td, uint8_t* tdf, int i,
-                                           int T) {
+__device__ __forceinline__ int delta_vals(const V2Smem<R>& S, int N, int u, int g, int k, R t[6]) {
     const R ra_b = sigma_norm_n(R(1.0)), da_b = ra_b;
     const R qix = S.cx[u], qiy = S.cy[u], pix = S.cvx[u], piy = S.cvy[u];
     const R yx = S.dx[g * N + k], yy = S.dy[g * N + k];
     const R ex = yx - qix, ey = yy - qiy;
     const R dn = sqrt(ex * ex + ey * ey);   // = the distance table entry
     const bool in = dn <= R(999 + 2), pr = dn <= R(1.1);
-    R t[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < 6; ++c) t[c] = 0;
     if (in) {
         R difx = qix - yx, dify = qiy - yy;
         R d = dn + R(1e-6);
@@ -527,20 +550,67 @@ __device__ __forceinline__ void delta_term(V2Smem<R>& S, int N, int u, int g, in
         t[4] = R(-650000.0) * ex / d3;
         t[5] = R(-650000.0) * ey / d3;
     }
-#pragma unroll
-    for (int c = 0; c < 6; ++c) td[c * T + i] = t[c];
-    tdf[i] = (uint8_t)(in | (pr << 1));
+    return (int)in | ((int)pr << 1);
 }
 
-// gamma term (flockUtils.py:150-160, 340-341), the drone terms summed in drone order, and the velocity
-// update with the speed clip (BaseAviary.py:1384-1400) of cow u.  A term out of range is +0 in the
-// table, and adding +0 to a sum that starts at +0 leaves it unchanged, so only the count needs the flag.
+// the same terms, one (cow, drone) item per lane, stored in the term table for flock_combine
+template <class R>
+__device__ __forceinline__ void delta_term(V2Smem<R>& S, int N, int u, int g, int k, R* td, uint8_t* tdf, int i,
+                                           int T) {
+    R t[6];
+    const int f = delta_vals(S, N, u, g, k, t);
+#pragma unroll
+    for (int c = 0; c < 6; ++c) td[c * T + i] = t[c];
+    tdf[i] = (uint8_t)f;
+}
+
+// the shepherd/predator sum of cow u over its env's n live drones in drone order (flockUtils.py:271-348),
+// one cow per lane with the drone terms in registers: delta = c2_beta (sum grad + sum consensus) over the
+// drones in range, plus the predator pushes.  A term out of range is +0, which leaves a sum that starts at
+// +0 unchanged (the same sums flock_combine forms from the term table).
+template <class R, int NT>
+__device__ __forceinline__ void shepherd_sum(const V2Smem<R>& S, int N, int u, int g, int n, R& ddx, R& ddy) {
+    const R C2B = R(2 * 4.47213595499958);
+    R gx = 0, gy = 0, cxx = 0, cyy = 0, sx = 0, sy = 0;
+    int nb = 0;
+    constexpr int NK = NT ? NT : 64;
+    CH_UNROLL for (int k = 0; k < NK; ++k) {
+        if (k >= N || k >= n) break;
+        R t[6];
+        const int f = delta_vals(S, N, u, g, k, t);
+        if (f & 1) { ++nb; gx += t[0]; gy += t[1]; cxx += t[2]; cyy += t[3]; }
+        if (f & 2) { sx += t[4]; sy += t[5]; }
+    }
+    ddx = 0; ddy = 0;
+    if (nb > 0) { ddx = C2B * gx + C2B * cxx; ddy = C2B * gy + C2B * cyy; }
+    ddx += sx; ddy += sy;
+}
+
+// gamma term (flockUtils.py:150-160, 340-341) and the velocity update with the speed clip
+// (BaseAviary.py:1384-1400) of cow u from its alpha row (aux, auy) and shepherd sum (ddx, ddy)
+template <class R>
+__device__ __forceinline__ void velocity_update(const StepParams<R>& p, const V2Smem<R>& S, int M, int e0, int u, R ddx,
+                                                R ddy) {
+    const long long CS = (long long)p.E * M;
+    const R C1G = R(5), C2G = R(0.2 * 2.23606797749979);
+    const R qix = S.cx[u], qiy = S.cy[u], pix = S.cvx[u], piy = S.cvy[u];
+    R gmx = -C1G * sigma_1(qix - R(1)) - C2G * pix, gmy = -C1G * sigma_1(qiy - R(1)) - C2G * piy;
+    R qx = (S.aux[u] + ddx) + gmx, qy = (S.auy[u] + ddy) + gmy;
+    const R dt_sqr = R(0.05 * 0.05);
+    R vx = pix + qx * dt_sqr, vy = piy + qy * dt_sqr;
+    R sp = norm2(vx, vy);
+    if (sp > R(kMaxVelCattle)) { R f = R(kMaxVelCattle) / sp; vx *= f; vy *= f; }
+    const long long ci = (long long)e0 * M + u;
+    CH_STS(&p.cattle[2 * CS + ci], vx); CH_STS(&p.cattle[3 * CS + ci], vy);
+}
+
+// the drone terms of cow u from the term table summed in drone order, then the velocity update.  A term
+// out of range is +0 in the table, and adding +0 to a sum that starts at +0 leaves it unchanged, so only
+// the count needs the flag.
 template <class R>
 __device__ __forceinline__ void flock_combine(const StepParams<R>& p, V2Smem<R>& S, int N, int M, int e0, int u, int n,
                                               const R* td, const uint8_t* tdf, int ib, int T) {
-    const long long CS = (long long)p.E * M;
-    const R C2B = R(2 * 4.47213595499958), C1G = R(5), C2G = R(0.2 * 2.23606797749979);
-    const R qix = S.cx[u], qiy = S.cy[u], pix = S.cvx[u], piy = S.cvy[u];
+    const R C2B = R(2 * 4.47213595499958);
     R ddx = 0, ddy = 0, sx = 0, sy = 0, gx = 0, gy = 0, cxx = 0, cyy = 0;
     int nb = 0;
     CH_UNROLL for (int k = 0; k < N; ++k) {
@@ -552,14 +622,7 @@ __device__ __forceinline__ void flock_combine(const StepParams<R>& p, V2Smem<R>&
     }
     if (nb > 0) { ddx = C2B * gx + C2B * cxx; ddy = C2B * gy + C2B * cyy; }
     ddx += sx; ddy += sy;
-    R gmx = -C1G * sigma_1(qix - R(1)) - C2G * pix, gmy = -C1G * sigma_1(qiy - R(1)) - C2G * piy;
-    R qx = (S.aux[u] + ddx) + gmx, qy = (S.auy[u] + ddy) + gmy;
-    const R dt_sqr = R(0.05 * 0.05);
-    R vx = pix + qx * dt_sqr, vy = piy + qy * dt_sqr;
-    R sp = norm2(vx, vy);
-    if (sp > R(kMaxVelCattle)) { R f = R(kMaxVelCattle) / sp; vx *= f; vy *= f; }
-    const long long ci = (long long)e0 * M + u;
-    CH_STS(&p.cattle[2 * CS + ci], vx); CH_STS(&p.cattle[3 * CS + ci], vy);
+    velocity_update(p, S, M, e0, u, ddx, ddy);
 }
 
 // GT/NT/MT > 0 specialise the kernel for one geometry (envs per workgroup, drones, cattle): the LDS
@@ -568,6 +631,15 @@ template <class R, int MODE, int GT, int NT, int MT, bool PHYS = false, bool PW 
 __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
     extern __shared__ __align__(16) unsigned char smem[];
     constexpr bool marl = MODE == 1;
+    // SPLIT (opt-in, CH_SPLIT; the CTDE 16-env x 4-drone geometry): the drones' spacing and cattle reward terms
+    // run on the cow waves, next to the drone wave's bookkeeping instead of before it; the reward waits for
+    // them (F_S).  The drone wave then ends ~3k cycles earlier, but the cow waves, already the busier side after
+    // the drone hand-off, end later: C4 168.3 vs 178.5 M env-steps/s without it (tools/gpu_ab.sh, ab4).
+#ifdef CH_SPLIT
+    constexpr bool SPLIT = !marl && GT == 16 && NT == 4;
+#else
+    constexpr bool SPLIT = false;
+#endif
     const int G = GT ? GT : p.G, N = NT ? NT : p.NC, M = MT ? MT : p.M, P = MT ? MT * (MT - 1) / 2 : p.P;
     const int rows = marl ? N : 12;
     const V2Layout L(G, N, M, P, MODE, (int)sizeof(R), PW ? (int)(blockDim.x >> 6) - 1 : 0, !PW && p.sep);
@@ -586,58 +658,85 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
     const Level* LT = S.LT;
     if (tid == 0) { TS(0, (long long)wall_clock64()); TS(2, (long long)clock64()); TS(12, (long long)__smid()); }
     if ((tid & 63) == 0 && tid < 256) TS(22 + (tid >> 6), (long long)__builtin_amdgcn_s_getreg((31 << 11) | 4));   // HW_ID
-    if (tid < kV2Flags) fl[tid] = 0;
-    lds_barrier();   // hand-off counters cleared before anyone signals
 
-    // ---- phase 0: env scalars, drone prefetch (wave 0); cattle integration, image zero-fill (cow waves)
+    // ---- phase 0: env scalars, drone prefetch (wave 0); cattle integration, image zero-fill (cow waves).
+    // Every wave issues its global loads before the first barrier, so their latency overlaps the launch of
+    // the workgroup's other waves; LDS is written only after it.
     const int nd = Gv * N;
     const bool dlane = tid < nd;
     const int dg = dlane ? tid / N : 0, dk = tid - dg * N;
     const long long di = (long long)e0 * N + tid;
     R pos[3], q[4], v[3], w[3], pid[9], rpy_in[3] = {0, 0, 0};
     R ph_lr[4] = {0, 0, 0, 0}, ph_rr[3] = {0, 0, 0};   // PHYS: last_clipped_action, DYN rpy_rates
-    int stepi = 0, n0 = 0, act0 = 0;
+    int stepi = 0, n0 = 0, act0 = 0, stepi_env = 0;
     double ev_acc = 0;   // update_evaluation_metrics' distance of this drone (optional)
     R spx_r[3] = {0, 0, 0}, spy_r[3] = {0, 0, 0};   // cow waves: prefetched spawn positions
     bool rpy_valid = false;
     bool co_simd = false;   // a cow wave on the drone wave's SIMD (starved while the drone wave issues)
-    if (tid < 64) {
+    // cow waves: the first cow of this lane and, on the first cow wave's env lanes, the env scalars
+    R c0[4] = {0, 0, 0, 0};
+    int ei0[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    R er0[2] = {0, 0};
+    double met0[kMetricRows];
+#pragma unroll
+    for (int r = 0; r < kMetricRows; ++r) met0[r] = 0;
+    if (tid >= 64) {
+        if (ct < Gv * M) {
+            const long long ci = (long long)e0 * M + ct;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) c0[c] = p.cattle[c * CS + ci];
+        }
+        if (ct < Gv) {
+            const int e = e0 + ct;
+#pragma unroll
+            for (int r = 0; r < 9; ++r) ei0[r] = p.envi[r * E + e];
+            ei0[9] = p.stale[E + e];
+            er0[0] = p.envr[e]; er0[1] = p.envr[E + e];
+#pragma unroll
+            for (int r = 0; r < kMetricRows; ++r) met0[r] = p.metrics[r * E + e];
+        }
+    } else if (dlane) {
         // the drone wave loads only what its chain reads, so the chain starts after one round trip; the
         // cow waves stage the env scalars, the curriculum table and the pair list meanwhile
+        n0 = p.envi[0 * E + e0 + dg];
+        rpy_valid = p.stale[e0 + dg] == 0;   // this env's Euler cache (written by the last v2 step)
+        if (marl) act0 = p.envi[7 * E + e0 + dg];
+        pos[0] = p.drone[0 * DS + di]; pos[1] = p.drone[1 * DS + di]; pos[2] = p.drone[2 * DS + di];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) q[c] = p.drone[(3 + c) * DS + di];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { v[c] = p.drone[(7 + c) * DS + di]; w[c] = p.drone[(10 + c) * DS + di]; }
+#pragma unroll
+        for (int c = 0; c < 9; ++c) pid[c] = p.drone[(13 + c) * DS + di];
+        // Euler angles of this quaternion, stored by the previous step (used iff the cache is
+        // valid; loaded regardless so the loads issue with the state's, not after the stale flag returns)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) rpy_in[c] = p.rpy[c * DS + di];
+        stepi = p.envi[9 * E + e0 + dg];   // ch_step calls on this env so far: the Philox action counter
+        if (p.evald) ev_acc = p.evald[di];
+        if constexpr (PHYS) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) ph_lr[c] = p.phys[c * DS + di];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) ph_rr[c] = p.phys[(4 + c) * DS + di];
+        }
+    }
+    if (tid < Gv) stepi_env = p.envi[9 * E + e0 + tid];   // env lanes: the counter the write-back advances
+    if (tid < kV2Flags) fl[tid] = 0;
+    lds_barrier();   // hand-off counters cleared before anyone signals
+
+    if (tid < 64) {
         __builtin_amdgcn_s_setprio(3);   // the drone wave is the critical path: it wins issue on a shared SIMD
         if (tid == 0)
             __hip_atomic_store(fl + V_DSIMD, 1 + (int)((__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (dlane) {
-            n0 = p.envi[0 * E + e0 + dg];
-            rpy_valid = p.stale[e0 + dg] == 0;   // this env's Euler cache (written by the last v2 step)
-            if (marl) act0 = p.envi[7 * E + e0 + dg];
-            pos[0] = p.drone[0 * DS + di]; pos[1] = p.drone[1 * DS + di]; pos[2] = p.drone[2 * DS + di];
-#pragma unroll
-            for (int c = 0; c < 4; ++c) q[c] = p.drone[(3 + c) * DS + di];
-#pragma unroll
-            for (int c = 0; c < 3; ++c) { v[c] = p.drone[(7 + c) * DS + di]; w[c] = p.drone[(10 + c) * DS + di]; }
-#pragma unroll
-            for (int c = 0; c < 9; ++c) pid[c] = p.drone[(13 + c) * DS + di];
-            // Euler angles of this quaternion, stored by the previous step (used iff the cache is
-            // valid; loaded regardless so the loads issue with the state's, not after the stale flag returns)
-#pragma unroll
-            for (int c = 0; c < 3; ++c) rpy_in[c] = p.rpy[c * DS + di];
-            stepi = p.envi[9 * E + e0 + dg];   // ch_step calls on this env so far: the Philox action counter
-            if (p.evald) ev_acc = p.evald[di];
-            if constexpr (PHYS) {
-#pragma unroll
-                for (int c = 0; c < 4; ++c) ph_lr[c] = p.phys[c * DS + di];
-#pragma unroll
-                for (int c = 0; c < 3; ++c) ph_rr[c] = p.phys[(4 + c) * DS + di];
-            }
-        }
     } else {
         const float rM0 = 1.0f / (float)M;
         for (int u = ct; u < Gv * M; u += CW) {
             const long long ci = (long long)e0 * M + u;   // the workgroup's cows are contiguous per component
-            R x = p.cattle[0 * CS + ci], y = p.cattle[1 * CS + ci];
-            const R vx = p.cattle[2 * CS + ci], vy = p.cattle[3 * CS + ci];
+            const bool first = u == ct;                  // loaded before the barrier
+            R x = first ? c0[0] : p.cattle[0 * CS + ci], y = first ? c0[1] : p.cattle[1 * CS + ci];
+            const R vx = first ? c0[2] : p.cattle[2 * CS + ci], vy = first ? c0[3] : p.cattle[3 * CS + ci];
             const R dt = R(p.dt);
             // frictionless cube (trace-pinned); no p.stepSimulation under Physics.DYN (BaseAviary.py:447-448)
             if (!PHYS || (p.physics != CH_PHYS_DYN && p.physics != CH_PHYS_DYN_RK4))
@@ -656,18 +755,17 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         const int g = ct;
         bool flk = false;
         if (g < Gv) {
-            const int e = e0 + g;
-            const int scA = p.envi[2 * E + e] + 1;
+            const int scA = ei0[2] + 1;   // the env scalars were loaded before the barrier
             flk = (scA % 2) == 0 && !(p.phase_mask & 2);
-            ei[I_N * G + g] = p.envi[0 * E + e]; ei[I_SC * G + g] = p.envi[1 * E + e]; ei[I_SCA * G + g] = scA;
-            ei[I_HASPREV * G + g] = p.envi[3 * E + e]; ei[I_LEVEL * G + g] = p.envi[4 * E + e];
-            ei[I_TALLY * G + g] = p.envi[5 * E + e]; ei[I_SPAWN * G + g] = p.envi[6 * E + e];
-            ei[I_ACTIVE * G + g] = p.envi[7 * E + e]; ei[I_EPISODE * G + g] = p.envi[8 * E + e];
+            ei[I_N * G + g] = ei0[0]; ei[I_SC * G + g] = ei0[1]; ei[I_SCA * G + g] = scA;
+            ei[I_HASPREV * G + g] = ei0[3]; ei[I_LEVEL * G + g] = ei0[4];
+            ei[I_TALLY * G + g] = ei0[5]; ei[I_SPAWN * G + g] = ei0[6];
+            ei[I_ACTIVE * G + g] = ei0[7]; ei[I_EPISODE * G + g] = ei0[8];
             ei[I_FLOCK * G + g] = flk; ei[I_RESET * G + g] = 0; ei[I_HERD * G + g] = 0;
-            ei[I_OBSD * G + g] = p.stale[E + e];   // the obs block's constant bytes are unknown
-            S.prev[g] = p.envr[e]; S.clock[g] = p.envr[E + e];
+            ei[I_OBSD * G + g] = ei0[9];   // the obs block's constant bytes are unknown
+            S.prev[g] = er0[0]; S.clock[g] = er0[1];
 #pragma unroll
-            for (int r = 0; r < kMetricRows; ++r) S.met[r * G + g] = p.metrics[r * E + e];
+            for (int r = 0; r < kMetricRows; ++r) S.met[r * G + g] = met0[r];
         }
         // compact list of flocking envs (BaseAviary.py:454: every second step_counter_A)
         const unsigned long long bal = __ballot(flk);
@@ -684,6 +782,18 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             co_simd = (int)((__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3) + 1 == ds;
         }
         if (ct == 0) TS(11, (long long)clock64());
+        if (ct < 64) {
+            // herd centroid (CattleAviary.py: HerdCentroid, np.mean over the cattle): needs only the integrated
+            // cows, so it is done before the drone hand-off; it counts Gv items of hand-off H
+            const int g = ct;
+            if (g < Gv) {
+                R sx = 0, sy = 0;
+                CH_UNROLL for (int j = 0; j < M; ++j) { sx += S.cx[g * M + j]; sy += S.cy[g * M + j]; }
+                S.hcx[g] = sx / R(M); S.hcy[g] = sy / R(M);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+            if (ct == 0) __hip_atomic_fetch_add(fl + F_H, Gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
         // spawn positions of the episode an auto-reset would start: scenario index + 1 (BaseAviary.py:600-606).
         // Loaded into registers here and parked in LDS after the pair loop, so the load latency hides
         // behind it and a reset needs no global load.  (Host geometry: G*M <= 3 * cow lanes.)
@@ -787,14 +897,8 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             }
             if (iso) f |= 4;
             if (fabs(pos[2] - R(kTargetAlt)) > R(kTargetAlt * 0.6)) f |= 1;
-            const Level& Lv = LT[ei[I_LEVEL * G + dg]];
-            const R sa = simple_spacing(m1, Lv), sb = simple_spacing(m2, Lv);
-            const R ca = complex_spacing(m1, Lv), cb = complex_spacing(m2, Lv);
-            R ps = 0;   // per-drone spacing reward (CattleAviary.py:238-246)
-            if (p.compat || m1 < R(INFINITY)) ps += (ca + sa) / R(2.0);
-            if (p.compat || m2 < R(INFINITY)) ps += (cb + sb) / R(2.0);
             S.pa[tid] = m1; S.pb[tid] = m2; S.dflags[tid] = f;
-            S.sa[tid] = sa; S.sb[tid] = sb; S.ca[tid] = ca; S.cb[tid] = cb; S.psp[tid] = ps;
+            if constexpr (!SPLIT) spacing_terms(S, LT[ei[I_LEVEL * G + dg]], p.compat != 0, tid, m1, m2);
             if (wobs) obs_nbr(obs_wg + dg * RW, S.dx, S.dy, b0, i, i1, i2);
         }
         lds_signal(fl + F_T);
@@ -802,18 +906,8 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         // every cow item (distances, winding, cattle obs) and herd centroid done
         lds_wait(fl + F_H, Gv * M + Gv + ((p.phase_mask & CH_PHASE_FORCE_TIMEOUT) ? 1 : 0), p.err);
         if (tid == 0) TS(6, (long long)clock64());
-        if (live && task) {
-            // closest cow (CattleAviary.py:248-252) from the cow waves' distance table -> cattle term
-            // min over cows of |y - q|^2, then one square root: sqrt is correctly rounded and monotonic, so
-            // this is the minimum of the distances (a NaN entry is skipped either way)
-            const R* dc = S.dcow + tid * M;
-            R best = R(INFINITY);
-            CH_UNROLL for (int j = 0; j < M; ++j) {
-                const R d = dc[j];
-                if (d < best) best = d;
-            }
-            best = sqrt(best);
-            S.scat[tid] = cattle_spacing(best, R(p.cs_cc));
+        if (live && task && !SPLIT) {
+            S.scat[tid] = cattle_term(S, tid, M, R(p.cs_cc));
             if constexpr (marl) {
                 // MARLCattleAviary._computeReward's per-agent part at the step's starting level
                 // (MARLCattleAviary.py:110-178), on every drone lane at once: the prefix
@@ -1117,6 +1211,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         lds_signal(fl + F_R);
         if (tid == 0) TS(15, (long long)clock64());
+        if constexpr (SPLIT) lds_wait(fl + F_S, 2 * Gv * N, p.err);   // spacing and cattle terms (cow waves)
         if (envl && task) {
             const int n = f_n;
             if constexpr (!marl) {
@@ -1184,6 +1279,18 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             p.reset_happened[e] = 0;
         }
         if (tid == 0) TS(7, (long long)clock64());
+        // ---- env scalars back to HBM from the env lanes' registers (nothing after this step reads them)
+        if (tid < Gv) {
+            const int e = e0 + tid;
+            CH_STS(&p.envi[0 * E + e], f_n); CH_STS(&p.envi[1 * E + e], f_sc); CH_STS(&p.envi[2 * E + e], f_scA);
+            CH_STS(&p.envi[3 * E + e], f_hp); CH_STS(&p.envi[4 * E + e], f_level); CH_STS(&p.envi[5 * E + e], f_tally);
+            CH_STS(&p.envi[6 * E + e], f_spawn); CH_STS(&p.envi[7 * E + e], f_active); CH_STS(&p.envi[8 * E + e], f_episode);
+            CH_STS(&p.envi[9 * E + e], stepi_env + 1);   // ch_step calls on this env
+            CH_STS(&p.envr[0 * E + e], f_prev); CH_STS(&p.envr[1 * E + e], f_clock);
+            // this step wrote the env's Euler cache and, unless obs were masked off, its whole obs block
+            p.stale[e] = 0;
+            if (wobs) p.stale[E + e] = 0;
+        }
     } else {
         // ============ cow waves ================================================================
         const float rM = 1.0f / (float)M;
@@ -1205,14 +1312,14 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         // one unit of PW alpha work (a cheap-pass chunk or an expensive-pass wave of queued pairs, plus the
         // env's rows after its last unit); false when no flocking env is left.  The state is wave-uniform
         // (grab is readfirstlane'd, the queue length a ballot count).
-        // sep: one of a cow's inputs to its velocity update is complete -- its alpha row (weight 1) or shepherd
-        // terms (weight N in total); the arrival that completes the count N + 1 runs the update
-        auto arrive = [&](int u, int g, int w) {
+        // sep: one of a cow's two inputs to its velocity update is complete -- its alpha row (aux, auy) or its
+        // shepherd sum (td[u], td[GM + u]); the second arrival runs the update
+        auto arrive = [&](int u) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-            const int old = __hip_atomic_fetch_add(&S.cnt[u], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (old + w == N + 1) {
+            const int old = __hip_atomic_fetch_add(&S.cnt[u], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (old == 1) {
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-                flock_combine(p, S, N, M, e0, u, ei[I_N * G + g], S.td, S.tdf, u * N, G * M * N);
+                velocity_update(p, S, M, e0, u, S.td[u], S.td[G * M + u]);
             }
         };
         auto alpha_step = [&]() -> bool {
@@ -1246,8 +1353,10 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             qu = S.queue + (size_t)(tid / 64 - 1) * P;
         } else {
             alpha_cheap(S, fl, M, P, nf, flist, skip_pre);
+            if (ct == 0) TS(38, (long long)clock64());
             lds_signal(fl + F_C);
             lds_wait(fl + F_C, W1, p.err);   // the queue is complete
+            if (ct == 0) { TS(39, (long long)clock64()); TS(29, (long long)lds_peek(fl + Q_LEN)); }
             alpha_full(S, fl, M, P, skip_pre);
         }
         if (ct == 0) TS(18, (long long)clock64());
@@ -1279,7 +1388,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                 if (u < nf * M) {
                     const int f = qdiv(u, M, rM), g = flist[f], j = u - f * M;
                     alpha_row(S, M, P, g * M + j, g, j);
-                    if (sep) arrive(g * M + j, g, 1);
+                    if (sep) arrive(g * M + j);
                 }
                 CHUNK_T1(2);
             }
@@ -1288,18 +1397,11 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         lds_wait(fl + F_D, 1, p.err);
         if (ct == 0) TS(9, (long long)clock64());
         skip_now = skip_post;
-        for (;;) {   // per cow: distances, winding number, observation entries; then per env: herd centroid
+        for (;;) {   // per cow: distances, winding number, observation entries (the herd centroid is done)
             const int b = grab(fl + C_COWS, 64, skip_post), u = b + lane;
-            if (b >= Gv * M + Gv) break;
+            if (b >= Gv * M) break;
             CHUNK_T0;
-            if (u >= Gv * M) {
-                const int g = u - Gv * M;   // herd centroid (CattleAviary.py: HerdCentroid, np.mean over the cattle)
-                if (g < Gv) {
-                    R sx = 0, sy = 0;
-                    CH_UNROLL for (int j = 0; j < M; ++j) { sx += S.cx[g * M + j]; sy += S.cy[g * M + j]; }
-                    S.hcx[g] = sx / R(M); S.hcy[g] = sy / R(M);
-                }
-            } else {
+            if (u < Gv * M) {
             const int g = qdiv(u, M, rM), j = u - g * M;
             const int n = ei[I_N * G + g], b0 = g * N;
             const R qix = S.cx[u], qiy = S.cy[u];
@@ -1325,10 +1427,31 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             }
             // H counts finished items, so a wave still busy with an alpha chunk does not hold the drone wave up
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-            if (lane == 0) __hip_atomic_fetch_add(fl + F_H, min(64, Gv * M + Gv - b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (lane == 0) __hip_atomic_fetch_add(fl + F_H, min(64, Gv * M - b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             CHUNK_T1(1);
         }
         const float rN = 1.0f / (float)N;
+        if constexpr (SPLIT) {
+            // the drones' spacing terms (from the drone wave's nearest-neighbour distances, signal T) and cattle
+            // terms (from the distance table, complete at H); each finished item counts towards F_S
+            for (int pass = 0; pass < 2; ++pass) {
+                for (;;) {
+                    const int b = grab(fl + (pass ? C_SCAT : C_SPC), 64, skip_post), u = b + lane;
+                    if (b >= Gv * N) break;
+                    if (pass) lds_wait(fl + F_H, Gv * M + Gv, p.err);
+                    else lds_wait(fl + F_T, 1, p.err);
+                    if (u < Gv * N && task) {
+                        const int g = qdiv(u, N, rN), k = u - g * N;
+                        if (k < ei[I_N * G + g]) {
+                            if (pass) S.scat[u] = cattle_term(S, u, M, R(p.cs_cc));
+                            else spacing_terms(S, LT[ei[I_LEVEL * G + g]], p.compat != 0, u, S.pa[u], S.pb[u]);
+                        }
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                    if (lane == 0) __hip_atomic_fetch_add(fl + F_S, min(64, Gv * N - b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+        }
         for (;;) {   // getEulerFromQuaternion of the new attitudes (BaseAviary.py:704-766): the own row's roll,
                      // pitch, yaw and the next step's PID input (the Euler cache)
             const int b = grab(fl + C_EULER, 64, skip_post), u = b + lane;
@@ -1372,46 +1495,38 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             if (ct == 0) TS(16, (long long)clock64());
         } else {
         if (sep) {
-            // the shepherd/predator (cow, drone) items need only the drone positions: they run before the alpha
-            // rows that remain; each cow's velocity update runs as soon as its row and its N terms are in
-            const int MN = M * N;
-            const float rMN = 1.0f / (float)MN;
-            const bool fuse = (64 % N) == 0;   // a chunk holds whole cows: one arrival of weight N per cow
-            for (;;) {
-                const int b = grab(fl + C_DELTA, 64, skip_post), q = b + lane;
-                if (b >= nf * MN) break;
-                CHUNK_T0;
-                int j = 0, k = 0, g = 0;
-                const bool valid = q < nf * MN;
-                if (valid) {
-                    const int f = qdiv(q, MN, rMN), rem = q - f * MN;
-                    j = qdiv(rem, N, rN); k = rem - j * N;
-                    g = flist[f];
-                    if (k < ei[I_N * G + g]) delta_term(S, N, g * M + j, g, k, S.td, S.tdf, (g * M + j) * N + k, G * MN);
-                }
-                if (fuse) {
-                    wave_sync();   // the cow's terms, written by other lanes of this wave
-                    if (valid && k == 0) arrive(g * M + j, g, N);
-                } else if (valid) {
-                    arrive(g * M + j, g, 1);
-                }
-                CHUNK_T1(3);
-            }
-            if (ct == 0) TS(16, (long long)clock64());
+            // The alpha rows that remain first (the longest chunks: started last they would end last), then the
+            // shepherd/predator (cow, drone) items; each cow's velocity update runs as soon as its row and its N
+            // terms are in, whichever arrives last
             lds_wait(fl + F_A, W1, p.err);   // every pair of the table
             if (ct == 0) TS(20, (long long)clock64());
-            for (;;) {   // the alpha rows that remain
+            for (;;) {
                 const int b = grab(fl + C_ROWS, 64, skip_post), u = b + lane;
                 if (b >= nf * M) break;
                 CHUNK_T0;
                 if (u < nf * M) {
                     const int f = qdiv(u, M, rM), g = flist[f], j = u - f * M;
                     alpha_row(S, M, P, g * M + j, g, j);
-                    arrive(g * M + j, g, 1);
+                    arrive(g * M + j);
                 }
                 CHUNK_T1(2);
             }
             if (ct == 0) TS(21, (long long)clock64());
+            // shepherd/predator sums, one cow of a flocking env per lane with its drones' terms in registers
+            for (;;) {
+                const int b = grab(fl + C_DELTA, 64, skip_post), u = b + lane;
+                if (b >= nf * M) break;
+                CHUNK_T0;
+                if (u < nf * M) {
+                    const int f = qdiv(u, M, rM), g = flist[f], j = u - f * M, uc = g * M + j;
+                    R ddx, ddy;
+                    shepherd_sum<R, NT>(S, N, uc, g, ei[I_N * G + g], ddx, ddy);
+                    S.td[uc] = ddx; S.td[G * M + uc] = ddy;
+                    arrive(uc);
+                }
+                CHUNK_T1(3);
+            }
+            if (ct == 0) TS(16, (long long)clock64());
         } else {
         // the alpha rows only feed the velocity update: they wait until the drone wave has its hand-off
             lds_wait(fl + F_A, W1, p.err);   // every pair of the table
@@ -1541,22 +1656,12 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
     }
     if (tid == 0) TS(35, (long long)clock64());
     if (tid == 64) TS(36, (long long)clock64());
-    lds_barrier();
-    if (tid == 0) TS(13, (long long)clock64());
-
-    // ---- env scalars back to HBM (the drone wave's env lanes hold them) -----------------------------
-    if (tid < Gv) {
-        const int e = e0 + tid;
-        CH_STS(&p.envi[0 * E + e], f_n); CH_STS(&p.envi[1 * E + e], f_sc); CH_STS(&p.envi[2 * E + e], f_scA);
-        CH_STS(&p.envi[3 * E + e], f_hp); CH_STS(&p.envi[4 * E + e], f_level); CH_STS(&p.envi[5 * E + e], f_tally);
-        CH_STS(&p.envi[6 * E + e], f_spawn); CH_STS(&p.envi[7 * E + e], f_active); CH_STS(&p.envi[8 * E + e], f_episode);
-        CH_STS(&p.envi[9 * E + e], p.envi[9 * E + e] + 1);   // ch_step calls on this env
-        CH_STS(&p.envr[0 * E + e], f_prev); CH_STS(&p.envr[1 * E + e], f_clock);
-        // this step wrote the env's Euler cache and, unless obs were masked off, its whole obs block
-        p.stale[e] = 0;
-        if (wobs) p.stale[E + e] = 0;
+    // No closing barrier: every wave leaves when its own work is done (the LDS lives until the last one
+    // has).  With timestamps on, one barrier marks the workgroup's end for the trace.
+    if (p.tstamp) {
+        lds_barrier();
+        if (tid == 0) { TS(13, (long long)clock64()); TS(14, (long long)clock64()); TS(1, (long long)wall_clock64()); }
     }
-    if (tid == 0) { TS(14, (long long)clock64()); TS(1, (long long)wall_clock64()); }
 }
 
 template <class R, int MODE, int GT, int NT, int MT, bool PHYS = false, bool PW = false>

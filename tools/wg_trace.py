@@ -61,6 +61,12 @@ def trace(mode, E, n, m, prec, G=None, B=None, steps=4):
                   f"| cow waves done (mean per wave) {' '.join(f'{(t[sel, 40 + w] - t[sel, 2]).mean():.0f}' for w in range(1, blk.value // 64))} "
                   f"| drone book {r2(7):.0f} B1 {r2(13):.0f} end {r2(14):.0f}")
         print(f"   at the last barrier: drone wave {rel(35):.0f} cow wave 1 {rel(36):.0f} (F_R seen {rel(37):.0f})")
+        nw = blk.value // 64
+        ws = np.where(t[:, 52:52 + nw] > 0, t[:, 52:52 + nw] - t[:, 2:3], 0)
+        print(f"   wave start (cycles after wave 0's): mean {' '.join(f'{ws[:, w].mean():.0f}' for w in range(nw))} | "
+              f"last wave q50/max {np.percentile(ws.max(axis=1), 50):.0f}/{ws.max():.0f} | first barrier passed {rel(3):.0f}")
+        print(f"   alpha passes (cow wave 1): cheap done {rel(38):.0f} all cheap (F_C) {rel(39):.0f} full done {rel(18):.0f}"
+              f" | queued pairs per WG {t[:, 29].mean():.1f} (per flocking env {(t[:, 29] / np.maximum(t[:, 31], 1)).mean():.1f})")
         print(f"   bookkeeping: scalars+centroid {rel(32):.0f} marl-prep {rel(33):.0f} env.step dicts {rel(34):.0f}")
         print(f"   drone wave after H: dtaskB {rel(26):.0f} pre-fence {rel(27):.0f} published {rel(15):.0f} "
               f"reward {rel(19):.0f} metrics stored {rel(28):.0f} book {rel(7):.0f}")
