@@ -12,7 +12,6 @@ def test_divc_matches_ieee_division(tmp_path):
     subprocess.run(["gcc", "-O2", "-o", str(exe), os.path.join(ROOT, "tools", "div_check.c"), "-lm"], check=True)
     out = subprocess.run([str(exe), "300000"], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout
-    assert "cos_0pi:" in out.stdout
     assert out.stdout.count("bad=0") == out.stdout.count("bad=")
 
 
@@ -25,3 +24,4 @@ def test_sincos_small_within_one_ulp_of_libm(tmp_path):
                     "-lm"], check=True)
     out = subprocess.run([str(exe), "2000000"], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout
+    assert "cos_0pi:" in out.stdout
