@@ -118,7 +118,7 @@ __device__ __forceinline__ void reset_cow_at(const StepParams<R>& p, long long c
         double u = philox_uniform53(p.k0, p.k1, episode, 1 + j, (uint32_t)env_id);
         double ang = kPi * (2 * u - 1);
         double sa, ca;
-        sincos(ang, &sa, &ca);
+        sincos_pi(ang, &sa, &ca);   // |ang| <= pi
         vx = R(kMaxVelCattle * ca); vy = R(kMaxVelCattle * sa);
     }
     p.cattle[0 * CS + ci] = x; p.cattle[1 * CS + ci] = y; p.cattle[2 * CS + ci] = vx; p.cattle[3 * CS + ci] = vy;

@@ -543,15 +543,16 @@ __device__ __forceinline__ void variant_substeps(const StepParams<R>& p, int bas
 constexpr double kEps = 0.1, kH = 0.2;
 template <class R> __device__ __forceinline__ R sigma_norm_n(R n) { return divc(sqrt(R(1) + R(kEps) * (n * n)) - R(1), R(kEps)); }
 // cos(x) for 0 <= x <= pi (the bump's argument): x = n pi/2 + r with n = round(x / (pi/2)) in {0, 1, 2} and
-// |r| <= pi/4 (Cody-Waite: pi/2 in three parts, each product exact), then the fdlibm kernels
+// |r| <= pi/4 (Cody-Waite: pi/2 in four parts, each product exact), then the fdlibm kernels
 // (sincos_small): cos r, -sin r, -cos r.  <= 1 ulp like libm (tools/sincos_check.c), without the generic
 // reduction of the libm entry point.
 template <class R> __device__ __forceinline__ R cos_0pi(R x) {
     if constexpr (sizeof(R) == 8) {
         const double PIO2_1 = 1.57079632673412561417e+00, PIO2_2 = 6.07710050630396597660e-11,
-                     PIO2_3 = 2.02226624871116645580e-21;   // fdlibm pio2_1, pio2_2, pio2_3
+                     PIO2_3 = 2.02226624871116645580e-21,
+                     PIO2_3T = 8.47842766036889956997e-32;   // fdlibm pio2_1, pio2_2, pio2_3, pio2_3t
         const double n = rint(x * 6.36619772367581382433e-01);
-        const double r = ((x - n * PIO2_1) - n * PIO2_2) - n * PIO2_3;
+        const double r = (((x - n * PIO2_1) - n * PIO2_2) - n * PIO2_3) - n * PIO2_3T;
         double s, c;
         sincos_small(fabs(r), &s, &c);
         s = r < 0 ? -s : s;
@@ -559,6 +560,20 @@ template <class R> __device__ __forceinline__ R cos_0pi(R x) {
     } else {
         return cosf(x);
     }
+}
+// sin and cos of -pi <= x <= pi (a reset's cattle velocity angle, BaseAviary.py:631-632): the same
+// reduction by pi/2 (quadrant n in -2..2) and fdlibm kernels; <= 1 ulp (tools/sincos_check.c)
+__device__ __forceinline__ void sincos_pi(double x, double* s, double* c) {
+    const double PIO2_1 = 1.57079632673412561417e+00, PIO2_2 = 6.07710050630396597660e-11,
+                 PIO2_3 = 2.02226624871116645580e-21, PIO2_3T = 8.47842766036889956997e-32;
+    const double n = rint(x * 6.36619772367581382433e-01);
+    const double r = (((x - n * PIO2_1) - n * PIO2_2) - n * PIO2_3) - n * PIO2_3T;
+    double sr, cr;
+    sincos_small(fabs(r), &sr, &cr);
+    sr = r < 0 ? -sr : sr;
+    const int q = (int)n & 3;
+    *s = q == 0 ? sr : (q == 1 ? cr : (q == 2 ? -sr : -cr));
+    *c = q == 0 ? cr : (q == 1 ? -sr : (q == 2 ? -cr : sr));
 }
 template <class R> __device__ __forceinline__ R bump(R z) {
     if (z < R(0)) return R(0);

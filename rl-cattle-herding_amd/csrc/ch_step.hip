@@ -515,11 +515,23 @@ __device__ __forceinline__ void alpha_row_pw(V2Smem<R>& S, int M, int P, int g, 
     S.aux[u] = ux; S.auy[u] = uy;
 }
 
+// the shepherd term of a drone closer than 1 m (mu < 1: the projected agent q_ik lies between cow and drone),
+// the general pair_terms evaluation.  Rare, so it is kept out of line: inlined at each of the unrolled drone
+// slots of shepherd_sum it would add ~1.2k instructions to the kernel's instruction-cache footprint.
+template <class R> struct Terms4 { R gx, gy, cx, cy; };
+template <class R>
+__device__ __noinline__ Terms4<R> near_drone_terms(R qix, R qiy, R pix, R piy, R yx, R yy, R mu, R pkx, R pky) {
+    const R ra_b = sigma_norm_n(R(1.0)), da_b = ra_b;
+    R qkx = mu * qix + (R(1) - mu) * yx, qky = mu * qiy + (R(1) - mu) * yy;
+    Terms4<R> t = {0, 0, 0, 0};
+    pair_terms(qix, qiy, pix, piy, qkx, qky, pkx, pky, ra_b, da_b, t.gx, t.gy, t.cx, t.cy);
+    return t;
+}
+
 // shepherd (delta, flockUtils.py:271-317) and predator (343-348) terms of drone k on cow u = g*M + j:
 // t[0..3] the delta gradient and consensus parts, t[4..5] the predator push; returns in-range | predator << 1
 template <class R>
 __device__ __forceinline__ int delta_vals(const V2Smem<R>& S, int N, int u, int g, int k, R t[6]) {
-    const R ra_b = sigma_norm_n(R(1.0)), da_b = ra_b;
     const R qix = S.cx[u], qiy = S.cy[u], pix = S.cvx[u], piy = S.cvy[u];
     const R yx = S.dx[g * N + k], yy = S.dy[g * N + k];
     const R ex = yx - qix, ey = yy - qiy;
@@ -541,8 +553,8 @@ __device__ __forceinline__ int delta_vals(const V2Smem<R>& S, int N, int u, int 
             t[2] = pkx - pix;
             t[3] = pky - piy;
         } else {
-            R qkx = mu * qix + (R(1) - mu) * yx, qky = mu * qiy + (R(1) - mu) * yy;
-            pair_terms(qix, qiy, pix, piy, qkx, qky, pkx, pky, ra_b, da_b, t[0], t[1], t[2], t[3]);
+            const Terms4<R> n4 = near_drone_terms(qix, qiy, pix, piy, yx, yy, mu, pkx, pky);
+            t[0] = n4.gx; t[1] = n4.gy; t[2] = n4.cx; t[3] = n4.cy;
         }
     }
     if (pr) {
@@ -1590,6 +1602,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         lds_wait(fl + F_R, 1, p.err);    // the reset list
         if (tid == 64) TS(37, (long long)clock64());
         const int nr = ei[NR_AT];
+        if (ct == 0) TS(30, (long long)nr);
         if (nr) {   // uniform across the cow waves
             // ---- SB3 auto-reset of the listed envs (BaseAviary.reset, BaseAviary.py:280-331), rebuilt from
             // the pre-step scalars (NUM_DRONES draw, spawn index + 1, episode) while the drone wave still
@@ -1603,7 +1616,9 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                 }
             }
             cow_sync(fl + F_X1, W1, true, p.err);   // terminal observation read; flock stores to the cattle state done
-            for (int u = ct; u < nr * N; u += CW) {
+            // the reset envs' drones on the first cow wave and their cattle on the others, concurrently
+            const int dl = W1 >= 2 ? 64 : CW, c0l = W1 >= 2 ? 64 : 0, cl = CW - c0l;
+            if (ct < dl) for (int u = ct; u < nr * N; u += dl) {
                 const int k0 = qdiv(u, N, rN), g = rl[k0], k = u - k0 * N, ud = g * N + k;
                 const int n = reset_draw_n(p, ei[I_EPISODE * G + g], p.env_off + e0 + g);
                 if (k == 0) ei[I_NEWN * G + g] = n;
@@ -1630,7 +1645,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                     for (int c = 0; c < 86; c += 2) st2(eb, k * 86 + c, 0.0f, 0.0f);
                 }
             }
-            for (int u = ct; u < nr * M; u += CW) {
+            if (ct >= c0l) for (int u = ct - c0l; u < nr * M; u += cl) {
                 const int k0 = qdiv(u, M, rM), g = rl[k0], j = u - k0 * M, uc = g * M + j;
                 R x, y, vx, vy;
                 reset_cow_at(p, (long long)e0 * M + uc, p.env_off + e0 + g, j, S.spx[uc], S.spy[uc],
@@ -1639,14 +1654,14 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             }
             cow_sync(fl + F_X2, W1, false, p.err);
             if (wobs) {
-                for (int u = ct; u < nr * N; u += CW) {
+                if (ct < dl) for (int u = ct; u < nr * N; u += dl) {
                     const int k0 = qdiv(u, N, rN), g = rl[k0], i = u - k0 * N;
                     const int n = ei[I_NEWN * G + g];
                     if (i >= n) continue;
                     const int nb = nearest_two(S.dx, S.dy, g * N, i, n);
                     obs_nbr(obs_wg + g * RW, S.dx, S.dy, g * N, i, (nb & 0xff) - 1, (nb >> 8) - 1);
                 }
-                for (int u = ct; u < nr * M; u += CW) {
+                if (ct >= c0l) for (int u = ct - c0l; u < nr * M; u += cl) {
                     const int k0 = qdiv(u, M, rM), g = rl[k0], j = u - k0 * M, uc = g * M + j;
                     if (j < m_obs)
                         obs_cattle(obs_wg + g * RW, S.dx, S.dy, g * N, j, ei[I_NEWN * G + g], cat_off, S.cx[uc], S.cy[uc]);

@@ -36,13 +36,25 @@ static void sincos_small(double x, double* s, double* c) {
 }
 static double cos_0pi(double x) {
     const double PIO2_1 = 1.57079632673412561417e+00, PIO2_2 = 6.07710050630396597660e-11,
-                 PIO2_3 = 2.02226624871116645580e-21;
+                 PIO2_3 = 2.02226624871116645580e-21, PIO2_3T = 8.47842766036889956997e-32;
     const double n = rint(x * 6.36619772367581382433e-01);
-    const double r = ((x - n * PIO2_1) - n * PIO2_2) - n * PIO2_3;
+    const double r = (((x - n * PIO2_1) - n * PIO2_2) - n * PIO2_3) - n * PIO2_3T;
     double s, c;
     sincos_small(fabs(r), &s, &c);
     s = r < 0 ? -s : s;
     return n == 0.0 ? c : (n == 1.0 ? -s : -c);
+}
+static void sincos_pi(double x, double* s, double* c) {
+    const double PIO2_1 = 1.57079632673412561417e+00, PIO2_2 = 6.07710050630396597660e-11,
+                 PIO2_3 = 2.02226624871116645580e-21, PIO2_3T = 8.47842766036889956997e-32;
+    const double n = rint(x * 6.36619772367581382433e-01);
+    const double r = (((x - n * PIO2_1) - n * PIO2_2) - n * PIO2_3) - n * PIO2_3T;
+    double sr, cr;
+    sincos_small(fabs(r), &sr, &cr);
+    sr = r < 0 ? -sr : sr;
+    const int q = (int)n & 3;
+    *s = q == 0 ? sr : (q == 1 ? cr : (q == 2 ? -sr : -cr));
+    *c = q == 0 ? cr : (q == 1 ? -sr : (q == 2 ? -cr : sr));
 }
 static double ulps(double a, double b) {
     if (a == b) return 0;
@@ -80,5 +92,18 @@ int main(int argc, char** argv) {
         dp += c != ref;
     }
     printf("cos_0pi: samples=%ld max_ulp=%.3f differ=%ld\n", n + 4, mp, dp);
-    return (ms <= 1.0 && mc <= 1.0 && mp <= 1.0) ? 0 : 1;
+    double m2s = 0, m2c = 0;
+    for (long i = 0; i < n + 5; ++i) {
+        st = st * 6364136223846793005ull + 1442695040888963407ull;
+        double x = ((double)(st >> 11) * (1.0 / 9007199254740992.0) * 2 - 1) * M_PI;
+        if (i == n) x = -M_PI; else if (i == n + 1) x = M_PI; else if (i == n + 2) x = -M_PI / 2;
+        else if (i == n + 3) x = 3 * M_PI / 4; else if (i == n + 4) x = -0.0;
+        double s, c;
+        sincos_pi(x, &s, &c);
+        const double us = ulps(s, sin(x)), uc = ulps(c, cos(x));
+        if (us > m2s) m2s = us;
+        if (uc > m2c) m2c = uc;
+    }
+    printf("sincos_pi: samples=%ld max_ulp_sin=%.3f max_ulp_cos=%.3f\n", n + 5, m2s, m2c);
+    return (ms <= 1.0 && mc <= 1.0 && mp <= 1.0 && m2s <= 1.0 && m2c <= 1.0) ? 0 : 1;
 }

@@ -110,7 +110,7 @@ def trace(mode, E, n, m, prec, G=None, B=None, steps=4):
               f"{simd[:3].tolist()} | co-resident WG pairs {pairs}, drone waves on the same SIMD {same}")
         tail = (t[:, 14] - t[:, 13]).astype(np.float64)
         chain = (t[:, 4] - t[:, 3]).astype(np.float64)
-        res = tail > 3000
+        res = t[:, 30] > 0   # workgroups that rebuilt auto-reset envs this step
         print(f"   spread: WG cycles q50/q90/max {np.percentile(cyc, 50):.0f}/{np.percentile(cyc, 90):.0f}/{cyc.max():.0f}"
               f" | resetting WGs {int(res.sum())}: cycles mean {cyc[res].mean() if res.any() else 0:.0f} vs "
               f"{cyc[~res].mean():.0f} | chain q50/q90/max {np.percentile(chain, 50):.0f}/{np.percentile(chain, 90):.0f}/"
