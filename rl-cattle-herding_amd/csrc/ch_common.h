@@ -79,12 +79,10 @@ __device__ __forceinline__ void reset_scalars(const StepParams<R>& p, int e, int
     episode += 1;
 }
 
-// initial pose of constructor drone k (initialize_drone_positions, BaseAviary.py:251-277): written to
-// the SoA state; returns x, y, z.  PID state persists across resets in compat mode (the reference's
-// DSLPIDControl objects are created once, BaseRLAviary.py:80).
+// initial position of constructor drone k of an episode with n_new drones (initialize_drone_positions,
+// BaseAviary.py:251-277)
 template <class R>
-__device__ __forceinline__ void reset_drone(const StepParams<R>& p, long long di, int k, int n_new, R& x, R& y, R& z) {
-    const long long DS = (long long)p.E * p.NC;
+__device__ __forceinline__ void reset_drone_xyz(int k, int n_new, R& x, R& y, R& z) {
     x = 0; y = 0; z = 0;
     if (k < n_new) {
         if (n_new <= 4) { x = R(k * 1.75); y = 0; }
@@ -94,6 +92,14 @@ __device__ __forceinline__ void reset_drone(const StepParams<R>& p, long long di
         }
         z = R(kTargetAlt);
     }
+}
+
+// the reset drone's state in the SoA arrays: position, identity attitude, zero velocities; the PID state
+// persists across resets in compat mode (the reference's DSLPIDControl objects are created once,
+// BaseRLAviary.py:80)
+template <class R>
+__device__ __forceinline__ void reset_drone_store(const StepParams<R>& p, long long di, R x, R y, R z) {
+    const long long DS = (long long)p.E * p.NC;
     R* D = p.drone;
     if (p.evald) p.evald[di] = 0;   // episode_drone_distances: (0, 0) -- _housekeeping zeroes self.pos (BaseAviary.py:567, 683-688)
     D[0 * DS + di] = x; D[1 * DS + di] = y; D[2 * DS + di] = z;
@@ -106,13 +112,20 @@ __device__ __forceinline__ void reset_drone(const StepParams<R>& p, long long di
     }
 }
 
-// cow j of a reset env at spawn position (x0, y0) (already looked up in the scenario table)
+// initial pose of constructor drone k, written to the SoA state; returns x, y, z
 template <class R>
-__device__ __forceinline__ void reset_cow_at(const StepParams<R>& p, long long ci, long long env_id, int j, R x0, R y0,
-                                             uint32_t episode, R& x, R& y, R& vx, R& vy) {
-    const long long CS = (long long)p.E * p.M;
-    x = x0; y = y0;
-    if (p.reset_vel) {   // the host's replay of the reference's own draws (ch_reset_with, cattleherd/seeded.py)
+__device__ __forceinline__ void reset_drone(const StepParams<R>& p, long long di, int k, int n_new, R& x, R& y, R& z) {
+    reset_drone_xyz(k, n_new, x, y, z);
+    reset_drone_store(p, di, x, y, z);
+}
+
+// velocity of cow j of a reset env: angle pi(2U-1) (BaseAviary.py:631-632), U from Philox keyed
+// (seed, env id, episode, 1 + j), or the host's replay of the reference's own draws (ch_reset_with,
+// cattleherd/seeded.py)
+template <class R>
+__device__ __forceinline__ void reset_cow_vel(const StepParams<R>& p, long long ci, long long env_id, int j,
+                                              uint32_t episode, R& vx, R& vy) {
+    if (p.reset_vel) {
         vx = R(p.reset_vel[2 * ci]); vy = R(p.reset_vel[2 * ci + 1]);
     } else {
         double u = philox_uniform53(p.k0, p.k1, episode, 1 + j, (uint32_t)env_id);
@@ -121,7 +134,20 @@ __device__ __forceinline__ void reset_cow_at(const StepParams<R>& p, long long c
         sincos_pi(ang, &sa, &ca);   // |ang| <= pi
         vx = R(kMaxVelCattle * ca); vy = R(kMaxVelCattle * sa);
     }
+}
+template <class R>
+__device__ __forceinline__ void reset_cow_store(const StepParams<R>& p, long long ci, R x, R y, R vx, R vy) {
+    const long long CS = (long long)p.E * p.M;
     p.cattle[0 * CS + ci] = x; p.cattle[1 * CS + ci] = y; p.cattle[2 * CS + ci] = vx; p.cattle[3 * CS + ci] = vy;
+}
+
+// cow j of a reset env at spawn position (x0, y0) (already looked up in the scenario table)
+template <class R>
+__device__ __forceinline__ void reset_cow_at(const StepParams<R>& p, long long ci, long long env_id, int j, R x0, R y0,
+                                             uint32_t episode, R& x, R& y, R& vx, R& vy) {
+    x = x0; y = y0;
+    reset_cow_vel(p, ci, env_id, j, episode, vx, vy);
+    reset_cow_store(p, ci, x, y, vx, vy);
 }
 
 // cow j of a reset env: YAML scenario position, yaw/velocity angle pi(2U-1) (BaseAviary.py:600-637),

@@ -109,11 +109,11 @@ struct V2Layout {
         const size_t shared = (sep || 4 * (size_t)G * P > 6 * (size_t)G * M * N) ? 4 * (size_t)G * P : 6 * (size_t)G * M * N;
         size_t o = 0;
         off[CX] = o;     o = al(o + 8 * (size_t)G * M * rb);         // cx cy cvx cvy aux auy spx spy
-        off[DRONE] = o;  o = al(o + 18 * (size_t)G * N * rb);        // dx dy dz pa pb sa sb ca cb scat psp mrew mq meor q[4]
+        off[DRONE] = o;  o = al(o + 21 * (size_t)G * N * rb);        // dx dy dz pa pb sa sb ca cb scat psp mrew mq meor q[4] rd[3]
         off[DCOW] = o;   o = al(o + (size_t)G * N * M * rb);         // cow-drone distances
         off[ENVR] = o;   o = al(o + 4 * (size_t)G * rb);             // prev clock, herd centroid x y
         off[PAIRS] = o;  o = al(o + (W ? (size_t)W * slot : shared) * rb);   // alpha pair table(s), then shepherd terms
-        off[TD] = o;     o = al(o + (sep ? 6 * (size_t)G * M * N * rb + 4 * (size_t)G * M : 0));   // sep: terms, per-cow counts
+        off[TD] = o;     o = al(o + (sep ? 4 * (size_t)G * M * rb + 4 * (size_t)G * M : 0));   // sep: shepherd sums, new velocities, per-cow counts
         off[MET] = o;    o = al(o + (size_t)kMetricRows * G * 8);
         off[IMG] = o;                                                // (observations go straight to HBM)
         off[EI] = o;     o = al(o + ((size_t)kV2EnvInts * G + 2 * G + 2 + kV2Flags) * 4);   // + flock/reset lists

@@ -137,11 +137,12 @@ struct V2Smem {
     R* mrew;                                         // [G*N] MARL per-agent reward scratch
     R *mq, *meor;                                    // [G*N] MARL: reward without the approach term, end-of-episode bonus
     R* dq;                                           // [4][G*N] drone attitude after physics (for the Euler angles)
+    R *rdx, *rdy, *rdz;                              // [G*N] auto-reset: the new episode's drone positions
     R* dcow;                                         // [G*N*M] squared cow-drone distances, (g*N + k)*M + j
     R *prev, *clock, *hcx, *hcy;                     // [G] env reals; herd centroid (cow waves)
     R *tgx, *tgy, *tcx, *tcy;                        // [G*P] alpha pair table
-    R* td;                                           // [6][G*M*N] shepherd/predator terms (the pair table's space unless sep)
-    int* cnt;                                        // sep: [G*M] per-cow arrivals (alpha row 1, shepherd terms N)
+    R* td;                                           // sep: [4][G*M] shepherd sums, new velocities; else [6][G*M*N] shepherd/predator terms (the pair table's space)
+    int* cnt;                                        // sep: [G*M] per-cow arrivals (alpha row, shepherd sum)
     double* met;                                     // [kMetricRows*G]
     int* ei;                                         // [I_COUNT*G] + list [G] + 2 + flags
     int* flags;
@@ -160,12 +161,13 @@ struct V2Smem {
         dx = (R*)(base + L.off[V2Layout::DRONE]); dy = dx + GN; dz = dy + GN;
         pa = dz + GN; pb = pa + GN; sa = pb + GN; sb = sa + GN; ca = sb + GN; cb = ca + GN; scat = cb + GN;
         psp = scat + GN; mrew = psp + GN; mq = mrew + GN; meor = mq + GN; dq = meor + GN;
+        rdx = dq + 4 * GN; rdy = rdx + GN; rdz = rdy + GN;
         dcow = (R*)(base + L.off[V2Layout::DCOW]);
         prev = (R*)(base + L.off[V2Layout::ENVR]); clock = prev + L.G; hcx = clock + L.G; hcy = hcx + L.G;
         pl = (const uint16_t*)(base + L.off[V2Layout::PAIRL]);
         tgx = (R*)(base + L.off[V2Layout::PAIRS]); tgy = tgx + GP; tcx = tgy + GP; tcy = tcx + GP;
         td = L.sep ? (R*)(base + L.off[V2Layout::TD]) : tgx;
-        cnt = (int*)(base + L.off[V2Layout::TD] + 6 * (size_t)L.G * L.M * L.N * sizeof(R));
+        cnt = (int*)(base + L.off[V2Layout::TD] + 4 * (size_t)L.G * L.M * sizeof(R));
         met = (double*)(base + L.off[V2Layout::MET]);
         ei = (int*)(base + L.off[V2Layout::EI]);
         flags = ei + I_COUNT * L.G + 2 * L.G + 2;
@@ -600,9 +602,10 @@ __device__ __forceinline__ void shepherd_sum(const V2Smem<R>& S, int N, int u, i
 
 // gamma term (flockUtils.py:150-160, 340-341) and the velocity update with the speed clip
 // (BaseAviary.py:1384-1400) of cow u from its alpha row (aux, auy) and shepherd sum (ddx, ddy)
+// nv != nullptr: the new velocity goes to LDS (nv[u], nv[GM + u]) for the cow waves' write-back instead of HBM
 template <class R>
 __device__ __forceinline__ void velocity_update(const StepParams<R>& p, const V2Smem<R>& S, int M, int e0, int u, R ddx,
-                                                R ddy) {
+                                                R ddy, R* nv = nullptr, int GM = 0) {
     const long long CS = (long long)p.E * M;
     const R C1G = R(5), C2G = R(0.2 * 2.23606797749979);
     const R qix = S.cx[u], qiy = S.cy[u], pix = S.cvx[u], piy = S.cvy[u];
@@ -612,6 +615,7 @@ __device__ __forceinline__ void velocity_update(const StepParams<R>& p, const V2
     R vx = pix + qx * dt_sqr, vy = piy + qy * dt_sqr;
     R sp = norm2(vx, vy);
     if (sp > R(kMaxVelCattle)) { R f = R(kMaxVelCattle) / sp; vx *= f; vy *= f; }
+    if (nv) { nv[u] = vx; nv[GM + u] = vy; return; }
     const long long ci = (long long)e0 * M + u;
     CH_STS(&p.cattle[2 * CS + ci], vx); CH_STS(&p.cattle[3 * CS + ci], vy);
 }
@@ -1331,7 +1335,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             const int old = __hip_atomic_fetch_add(&S.cnt[u], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (old == 1) {
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-                velocity_update(p, S, M, e0, u, S.td[u], S.td[G * M + u]);
+                velocity_update(p, S, M, e0, u, S.td[u], S.td[G * M + u], S.td + 2 * G * M, G * M);
             }
         };
         auto alpha_step = [&]() -> bool {
@@ -1603,70 +1607,92 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         if (tid == 64) TS(37, (long long)clock64());
         const int nr = ei[NR_AT];
         if (ct == 0) TS(30, (long long)nr);
-        if (nr) {   // uniform across the cow waves
+        if (nr || sep) {   // uniform across the cow waves
             // ---- SB3 auto-reset of the listed envs (BaseAviary.reset, BaseAviary.py:280-331), rebuilt from
             // the pre-step scalars (NUM_DRONES draw, spawn index + 1, episode) while the drone wave still
-            // computes rewards: R1 bodies + own-state rows, R2 neighbour and cattle entries, R3 copy.
+            // computes rewards: the terminal observation (on request), then the bodies and observation rows.
             const int* rl = ei + RS_LIST;
-            if (p.terminal_obs) {   // info["terminal_observation"]: the pre-reset observation, from HBM
+            if (nr && p.terminal_obs) {   // info["terminal_observation"]: the pre-reset observation, from HBM
                 cow_sync(fl + F_X0, W1, true, p.err);   // every cow wave's observation stores of this step are visible
                 for (int q = ct; q < nr * (RW >> 1); q += CW) {
                     const int k = q / (RW >> 1), o = rl[k] * (RW >> 1) + (q - k * (RW >> 1));
                     reinterpret_cast<float2*>(p.terminal_obs + (long long)e0 * RW)[o] = reinterpret_cast<const float2*>(obs_wg)[o];
                 }
             }
-            cow_sync(fl + F_X1, W1, true, p.err);   // terminal observation read; flock stores to the cattle state done
-            // the reset envs' drones on the first cow wave and their cattle on the others, concurrently
+            // The new episode's bodies are computed before the sync (into registers, the new drone positions also
+            // into LDS rd*), so the sync's wait for the slowest cow wave hides that latency; after it only the stores
+            // remain.  The reset envs' drones go to the first cow wave, their cattle to the others (concurrently).
+            // (sep: the flock's new velocities are in LDS; they go to HBM after the sync below, unless the env resets)
             const int dl = W1 >= 2 ? 64 : CW, c0l = W1 >= 2 ? 64 : 0, cl = CW - c0l;
-            if (ct < dl) for (int u = ct; u < nr * N; u += dl) {
-                const int k0 = qdiv(u, N, rN), g = rl[k0], k = u - k0 * N, ud = g * N + k;
+            // drones: one per lane of the first cow wave (nr * N <= G * N <= 64 <= dl)
+            const bool dit = ct < dl && ct < nr * N;
+            R rx = 0, ry = 0, rz = 0;
+            if (dit) {
+                const int k0 = qdiv(ct, N, rN), g = rl[k0], k = ct - k0 * N, ud = g * N + k;
                 const int n = reset_draw_n(p, ei[I_EPISODE * G + g], p.env_off + e0 + g);
                 if (k == 0) ei[I_NEWN * G + g] = n;
-                R x, y, z;
-                reset_drone(p, (long long)e0 * N + ud, k, n, x, y, z);
+                reset_drone_xyz(k, n, rx, ry, rz);
+                S.rdx[ud] = rx; S.rdy[ud] = ry; S.rdz[ud] = rz;
+            }
+            // cattle: the first two per lane in registers (the rest, beyond 2 cl, after the sync)
+            constexpr int RI = 2;
+            R cvx_r[RI], cvy_r[RI];
+#pragma unroll
+            for (int i = 0; i < RI; ++i) {
+                const int u = ct - c0l + i * cl;
+                cvx_r[i] = cvy_r[i] = 0;
+                if (ct >= c0l && u < nr * M) {
+                    const int k0 = qdiv(u, M, rM), g = rl[k0], j = u - k0 * M, uc = g * M + j;
+                    reset_cow_vel(p, (long long)e0 * M + uc, p.env_off + e0 + g, j, (uint32_t)ei[I_EPISODE * G + g],
+                                  cvx_r[i], cvy_r[i]);
+                }
+            }
+            cow_sync(fl + F_X1, W1, true, p.err);   // terminal observation read; this step's stores done; rd* and NEWN seen
+            if (sep) {   // the flocking envs' new velocities (velocity_update), but for the envs that reset
+                const R* nv = S.td + 2 * G * M;
+                for (int u = ct; u < nf * M; u += CW) {
+                    const int f = qdiv(u, M, rM), g = flist[f], j = u - f * M, uc = g * M + j;
+                    if (ei[I_RESET * G + g]) continue;
+                    const long long ci = (long long)e0 * M + uc;
+                    CH_STS(&p.cattle[2 * CS + ci], nv[uc]); CH_STS(&p.cattle[3 * CS + ci], nv[G * M + uc]);
+                }
+            }
+            if (dit) {
+                const int k0 = qdiv(ct, N, rN), g = rl[k0], k = ct - k0 * N, ud = g * N + k;
+                const int n = ei[I_NEWN * G + g];
+                const long long dd = (long long)e0 * N + ud;
+                reset_drone_store(p, dd, rx, ry, rz);
                 if constexpr (PHYS) {   // last_clipped_action, rpy_rates = 0 (_housekeeping, BaseAviary.py:565, 581-582)
 #pragma unroll
-                    for (int c = 0; c < kPhysComps; ++c) CH_STS(&p.phys[c * DS + (long long)e0 * N + ud], R(0));
+                    for (int c = 0; c < kPhysComps; ++c) CH_STS(&p.phys[c * DS + dd], R(0));
                 }
-                {   // identity attitude: Euler angles (+0, -0, +0) for the next step's cache
-                    const long long dd = (long long)e0 * N + ud;
-                    CH_STS(&p.rpy[dd], R(0)); CH_STS(&p.rpy[DS + dd], -R(0)); CH_STS(&p.rpy[2 * DS + dd], R(0));
-                }
-                S.dx[ud] = x; S.dy[ud] = y; S.dz[ud] = z;
-                if (!wobs) continue;
-                float* eb = obs_wg + g * RW;
-                if (k < n) {
-                    // identity quaternion: getEulerFromQuaternion gives atan2(+0, 1), asin(-2 * (+0)), atan2(+0, 1)
-                    // = (+0, -0, +0) (quat_to_euler); zero velocities
-                    const R zero3[3] = {0, 0, 0}, rpy0[3] = {R(0), -R(0), R(0)};
-                    obs_own(eb, k, z, rpy0, zero3, zero3);
-                } else if (k < ei[I_N * G + g]) {
-                    // a row the old episode used and the new one does not (rows >= the old NUM_DRONES are zero)
-                    for (int c = 0; c < 86; c += 2) st2(eb, k * 86 + c, 0.0f, 0.0f);
+                // identity attitude: Euler angles (+0, -0, +0) for the next step's cache
+                CH_STS(&p.rpy[dd], R(0)); CH_STS(&p.rpy[DS + dd], -R(0)); CH_STS(&p.rpy[2 * DS + dd], R(0));
+                if (wobs) {
+                    float* eb = obs_wg + g * RW;
+                    if (k < n) {
+                        // identity quaternion: getEulerFromQuaternion gives atan2(+0, 1), asin(-2 * (+0)), atan2(+0, 1)
+                        // = (+0, -0, +0) (quat_to_euler); zero velocities
+                        const R zero3[3] = {0, 0, 0}, rpy0[3] = {R(0), -R(0), R(0)};
+                        obs_own(eb, k, rz, rpy0, zero3, zero3);
+                        const int nb = nearest_two(S.rdx, S.rdy, g * N, k, n);
+                        obs_nbr(eb, S.rdx, S.rdy, g * N, k, (nb & 0xff) - 1, (nb >> 8) - 1);
+                    } else if (k < ei[I_N * G + g]) {
+                        // a row the old episode used and the new one does not (rows >= the old NUM_DRONES are zero)
+                        for (int c = 0; c < 86; c += 2) st2(eb, k * 86 + c, 0.0f, 0.0f);
+                    }
                 }
             }
-            if (ct >= c0l) for (int u = ct - c0l; u < nr * M; u += cl) {
-                const int k0 = qdiv(u, M, rM), g = rl[k0], j = u - k0 * M, uc = g * M + j;
-                R x, y, vx, vy;
-                reset_cow_at(p, (long long)e0 * M + uc, p.env_off + e0 + g, j, S.spx[uc], S.spy[uc],
-                             (uint32_t)ei[I_EPISODE * G + g], x, y, vx, vy);
-                S.cx[uc] = x; S.cy[uc] = y;
-            }
-            cow_sync(fl + F_X2, W1, false, p.err);
-            if (wobs) {
-                if (ct < dl) for (int u = ct; u < nr * N; u += dl) {
-                    const int k0 = qdiv(u, N, rN), g = rl[k0], i = u - k0 * N;
-                    const int n = ei[I_NEWN * G + g];
-                    if (i >= n) continue;
-                    const int nb = nearest_two(S.dx, S.dy, g * N, i, n);
-                    obs_nbr(obs_wg + g * RW, S.dx, S.dy, g * N, i, (nb & 0xff) - 1, (nb >> 8) - 1);
-                }
-                if (ct >= c0l) for (int u = ct - c0l; u < nr * M; u += cl) {
+            if (ct >= c0l)
+                for (int u = ct - c0l, i = 0; u < nr * M; u += cl, ++i) {
                     const int k0 = qdiv(u, M, rM), g = rl[k0], j = u - k0 * M, uc = g * M + j;
-                    if (j < m_obs)
-                        obs_cattle(obs_wg + g * RW, S.dx, S.dy, g * N, j, ei[I_NEWN * G + g], cat_off, S.cx[uc], S.cy[uc]);
+                    R vx = i == 0 ? cvx_r[0] : cvx_r[1], vy = i == 0 ? cvy_r[0] : cvy_r[1];
+                    if (i >= RI)
+                        reset_cow_vel(p, (long long)e0 * M + uc, p.env_off + e0 + g, j, (uint32_t)ei[I_EPISODE * G + g], vx, vy);
+                    const R x = S.spx[uc], y = S.spy[uc];
+                    reset_cow_store(p, (long long)e0 * M + uc, x, y, vx, vy);
+                    if (wobs && j < m_obs) obs_cattle(obs_wg + g * RW, S.rdx, S.rdy, g * N, j, ei[I_NEWN * G + g], cat_off, x, y);
                 }
-            }
         }
     }
     if (tid == 0) TS(35, (long long)clock64());
