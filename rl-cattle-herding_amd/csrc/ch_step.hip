@@ -141,7 +141,7 @@ struct V2Smem {
     R* dcow;                                         // [G*N*M] squared cow-drone distances, (g*N + k)*M + j
     R *prev, *clock, *hcx, *hcy;                     // [G] env reals; herd centroid (cow waves)
     R *tgx, *tgy, *tcx, *tcy;                        // [G*P] alpha pair table
-    R* td;                                           // sep: [4][G*M] shepherd sums, new velocities; else [6][G*M*N] shepherd/predator terms (the pair table's space)
+    R* td;                                           // sep: [2][G*M] shepherd sums; else [6][G*M*N] shepherd/predator terms (the pair table's space)
     int* cnt;                                        // sep: [G*M] per-cow arrivals (alpha row, shepherd sum)
     double* met;                                     // [kMetricRows*G]
     int* ei;                                         // [I_COUNT*G] + list [G] + 2 + flags
@@ -167,7 +167,7 @@ struct V2Smem {
         pl = (const uint16_t*)(base + L.off[V2Layout::PAIRL]);
         tgx = (R*)(base + L.off[V2Layout::PAIRS]); tgy = tgx + GP; tcx = tgy + GP; tcy = tcx + GP;
         td = L.sep ? (R*)(base + L.off[V2Layout::TD]) : tgx;
-        cnt = (int*)(base + L.off[V2Layout::TD] + 4 * (size_t)L.G * L.M * sizeof(R));
+        cnt = (int*)(base + L.off[V2Layout::TD] + 2 * (size_t)L.G * L.M * sizeof(R));
         met = (double*)(base + L.off[V2Layout::MET]);
         ei = (int*)(base + L.off[V2Layout::EI]);
         flags = ei + I_COUNT * L.G + 2 * L.G + 2;
@@ -602,10 +602,9 @@ __device__ __forceinline__ void shepherd_sum(const V2Smem<R>& S, int N, int u, i
 
 // gamma term (flockUtils.py:150-160, 340-341) and the velocity update with the speed clip
 // (BaseAviary.py:1384-1400) of cow u from its alpha row (aux, auy) and shepherd sum (ddx, ddy)
-// nv != nullptr: the new velocity goes to LDS (nv[u], nv[GM + u]) for the cow waves' write-back instead of HBM
 template <class R>
 __device__ __forceinline__ void velocity_update(const StepParams<R>& p, const V2Smem<R>& S, int M, int e0, int u, R ddx,
-                                                R ddy, R* nv = nullptr, int GM = 0) {
+                                                R ddy) {
     const long long CS = (long long)p.E * M;
     const R C1G = R(5), C2G = R(0.2 * 2.23606797749979);
     const R qix = S.cx[u], qiy = S.cy[u], pix = S.cvx[u], piy = S.cvy[u];
@@ -615,7 +614,6 @@ __device__ __forceinline__ void velocity_update(const StepParams<R>& p, const V2
     R vx = pix + qx * dt_sqr, vy = piy + qy * dt_sqr;
     R sp = norm2(vx, vy);
     if (sp > R(kMaxVelCattle)) { R f = R(kMaxVelCattle) / sp; vx *= f; vy *= f; }
-    if (nv) { nv[u] = vx; nv[GM + u] = vy; return; }
     const long long ci = (long long)e0 * M + u;
     CH_STS(&p.cattle[2 * CS + ci], vx); CH_STS(&p.cattle[3 * CS + ci], vy);
 }
@@ -1335,7 +1333,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             const int old = __hip_atomic_fetch_add(&S.cnt[u], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (old == 1) {
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-                velocity_update(p, S, M, e0, u, S.td[u], S.td[G * M + u], S.td + 2 * G * M, G * M);
+                velocity_update(p, S, M, e0, u, S.td[u], S.td[G * M + u]);
             }
         };
         auto alpha_step = [&]() -> bool {
@@ -1607,7 +1605,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         if (tid == 64) TS(37, (long long)clock64());
         const int nr = ei[NR_AT];
         if (ct == 0) TS(30, (long long)nr);
-        if (nr || sep) {   // uniform across the cow waves
+        if (nr) {   // uniform across the cow waves
             // ---- SB3 auto-reset of the listed envs (BaseAviary.reset, BaseAviary.py:280-331), rebuilt from
             // the pre-step scalars (NUM_DRONES draw, spawn index + 1, episode) while the drone wave still
             // computes rewards: the terminal observation (on request), then the bodies and observation rows.
@@ -1622,7 +1620,6 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             // The new episode's bodies are computed before the sync (into registers, the new drone positions also
             // into LDS rd*), so the sync's wait for the slowest cow wave hides that latency; after it only the stores
             // remain.  The reset envs' drones go to the first cow wave, their cattle to the others (concurrently).
-            // (sep: the flock's new velocities are in LDS; they go to HBM after the sync below, unless the env resets)
             const int dl = W1 >= 2 ? 64 : CW, c0l = W1 >= 2 ? 64 : 0, cl = CW - c0l;
             // drones: one per lane of the first cow wave (nr * N <= G * N <= 64 <= dl)
             const bool dit = ct < dl && ct < nr * N;
@@ -1648,15 +1645,6 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                 }
             }
             cow_sync(fl + F_X1, W1, true, p.err);   // terminal observation read; this step's stores done; rd* and NEWN seen
-            if (sep) {   // the flocking envs' new velocities (velocity_update), but for the envs that reset
-                const R* nv = S.td + 2 * G * M;
-                for (int u = ct; u < nf * M; u += CW) {
-                    const int f = qdiv(u, M, rM), g = flist[f], j = u - f * M, uc = g * M + j;
-                    if (ei[I_RESET * G + g]) continue;
-                    const long long ci = (long long)e0 * M + uc;
-                    CH_STS(&p.cattle[2 * CS + ci], nv[uc]); CH_STS(&p.cattle[3 * CS + ci], nv[G * M + uc]);
-                }
-            }
             if (dit) {
                 const int k0 = qdiv(ct, N, rN), g = rl[k0], k = ct - k0 * N, ud = g * N + k;
                 const int n = ei[I_NEWN * G + g];
