@@ -113,7 +113,7 @@ struct V2Layout {
         off[DCOW] = o;   o = al(o + (size_t)G * N * M * rb);         // cow-drone distances
         off[ENVR] = o;   o = al(o + 4 * (size_t)G * rb);             // prev clock, herd centroid x y
         off[PAIRS] = o;  o = al(o + (W ? (size_t)W * slot : shared) * rb);   // alpha pair table(s), then shepherd terms
-        off[TD] = o;     o = al(o + (sep ? 2 * (size_t)G * M * rb + 4 * (size_t)G * M : 0));   // sep: shepherd sums, per-cow counts
+        off[TD] = o;     o = al(o + (sep ? 4 * (size_t)G * M * rb + 4 * (size_t)G * M : 0));   // sep: shepherd sums, new velocities, per-cow counts
         off[MET] = o;    o = al(o + (size_t)kMetricRows * G * 8);
         off[IMG] = o;                                                // (observations go straight to HBM)
         off[EI] = o;     o = al(o + ((size_t)kV2EnvInts * G + 2 * G + 2 + kV2Flags) * 4);   // + flock/reset lists

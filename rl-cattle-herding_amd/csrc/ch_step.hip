@@ -141,7 +141,7 @@ struct V2Smem {
     R* dcow;                                         // [G*N*M] squared cow-drone distances, (g*N + k)*M + j
     R *prev, *clock, *hcx, *hcy;                     // [G] env reals; herd centroid (cow waves)
     R *tgx, *tgy, *tcx, *tcy;                        // [G*P] alpha pair table
-    R* td;                                           // sep: [2][G*M] shepherd sums; else [6][G*M*N] shepherd/predator terms (the pair table's space)
+    R* td;                                           // sep: [4][G*M] shepherd sums, new velocities; else [6][G*M*N] shepherd/predator terms (the pair table's space)
     int* cnt;                                        // sep: [G*M] per-cow arrivals (alpha row, shepherd sum)
     double* met;                                     // [kMetricRows*G]
     int* ei;                                         // [I_COUNT*G] + list [G] + 2 + flags
@@ -167,7 +167,7 @@ struct V2Smem {
         pl = (const uint16_t*)(base + L.off[V2Layout::PAIRL]);
         tgx = (R*)(base + L.off[V2Layout::PAIRS]); tgy = tgx + GP; tcx = tgy + GP; tcy = tcx + GP;
         td = L.sep ? (R*)(base + L.off[V2Layout::TD]) : tgx;
-        cnt = (int*)(base + L.off[V2Layout::TD] + 2 * (size_t)L.G * L.M * sizeof(R));
+        cnt = (int*)(base + L.off[V2Layout::TD] + 4 * (size_t)L.G * L.M * sizeof(R));
         met = (double*)(base + L.off[V2Layout::MET]);
         ei = (int*)(base + L.off[V2Layout::EI]);
         flags = ei + I_COUNT * L.G + 2 * L.G + 2;
@@ -602,9 +602,10 @@ __device__ __forceinline__ void shepherd_sum(const V2Smem<R>& S, int N, int u, i
 
 // gamma term (flockUtils.py:150-160, 340-341) and the velocity update with the speed clip
 // (BaseAviary.py:1384-1400) of cow u from its alpha row (aux, auy) and shepherd sum (ddx, ddy)
+// nv != nullptr: the new velocity goes to LDS (nv[u], nv[GM + u]) instead of HBM
 template <class R>
 __device__ __forceinline__ void velocity_update(const StepParams<R>& p, const V2Smem<R>& S, int M, int e0, int u, R ddx,
-                                                R ddy) {
+                                                R ddy, R* nv = nullptr, int GM = 0) {
     const long long CS = (long long)p.E * M;
     const R C1G = R(5), C2G = R(0.2 * 2.23606797749979);
     const R qix = S.cx[u], qiy = S.cy[u], pix = S.cvx[u], piy = S.cvy[u];
@@ -614,6 +615,7 @@ __device__ __forceinline__ void velocity_update(const StepParams<R>& p, const V2
     R vx = pix + qx * dt_sqr, vy = piy + qy * dt_sqr;
     R sp = norm2(vx, vy);
     if (sp > R(kMaxVelCattle)) { R f = R(kMaxVelCattle) / sp; vx *= f; vy *= f; }
+    if (nv) { nv[u] = vx; nv[GM + u] = vy; return; }
     const long long ci = (long long)e0 * M + u;
     CH_STS(&p.cattle[2 * CS + ci], vx); CH_STS(&p.cattle[3 * CS + ci], vy);
 }
@@ -826,6 +828,12 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
     if (tid == 0) TS(3, (long long)clock64());
 
     const bool wobs = !(p.phase_mask & 8);
+    // late (shared tables with their own shepherd region): the cattle observation entries and the Euler angles
+    // are written after the reset list is known, and each cow's final velocity by the last of three arrivals
+    // (alpha row, shepherd sum, final pass).  fast (late, no terminal observation requested): the reset envs'
+    // new bodies and observation rows are then written by the lanes that wrote their old values (drones: the
+    // drone wave; cattle state: the phase-0 lane; obs: the single late writer), with no drain or sync.
+    const bool late = sep, fast = late && !p.terminal_obs;
     float* obs_wg = p.obs + (long long)e0 * RW;
     // final per-env scalars, held by the drone wave's env lanes until the write-back
     int f_n = 0, f_sc = 0, f_scA = 0, f_hp = 0, f_level = 0, f_tally = 0, f_spawn = 0, f_active = 0, f_episode = 0;
@@ -1218,6 +1226,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         // publish the reset list: the cow waves rebuild those envs while this wave finishes the reward.
         // This wave's drone-state stores are complete first (the cow waves overwrite reset drones).
         if (envl) ei[I_RESET * G + g] = rs;
+        if (envl && rs) ei[I_NEWN * G + g] = p.reset_n ? p.reset_n[e] : reset_draw_n(p, f_episode, p.env_off + e);
         const unsigned long long rbal = __ballot(rs != 0);
         if (rs) ei[RS_LIST + __popcll(rbal & ((1ull << g) - 1ull))] = g;
         if (tid == 0) ei[NR_AT] = __popcll(rbal);
@@ -1225,6 +1234,42 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         lds_signal(fl + F_R);
         if (tid == 0) TS(15, (long long)clock64());
+        if (fast && ei[NR_AT]) {
+            // SB3 auto-reset, drone side (BaseAviary.reset, BaseAviary.py:280-331): each drone lane of a reset env
+            // writes its new body, Euler cache and observation row itself (it wrote the old ones)
+            wave_sync();   // the reset flags and NUM_DRONES draws of the env lanes
+            const bool rd = dlane && ei[I_RESET * G + dg];
+            const int n_new = rd ? ei[I_NEWN * G + dg] : 0;
+            R x = 0, y = 0, z = 0;
+            if (rd) {
+                reset_drone_xyz(dk, n_new, x, y, z);
+                S.rdx[tid] = x; S.rdy[tid] = y; S.rdz[tid] = z;
+            }
+            wave_sync();   // the env's new drone positions (nearest neighbours)
+            if (rd) {
+                reset_drone_store(p, di, x, y, z);
+                if constexpr (PHYS) {   // last_clipped_action, rpy_rates = 0 (_housekeeping, BaseAviary.py:565, 581-582)
+#pragma unroll
+                    for (int c = 0; c < kPhysComps; ++c) CH_STS(&p.phys[c * DS + di], R(0));
+                }
+                // identity attitude: Euler angles (+0, -0, +0) for the next step's cache
+                CH_STS(&p.rpy[di], R(0)); CH_STS(&p.rpy[DS + di], -R(0)); CH_STS(&p.rpy[2 * DS + di], R(0));
+                if (wobs) {
+                    float* eb = obs_wg + dg * RW;
+                    if (dk < n_new) {
+                        // identity quaternion: getEulerFromQuaternion gives (+0, -0, +0) (quat_to_euler); zero velocities
+                        const R zero3[3] = {0, 0, 0}, rpy0[3] = {R(0), -R(0), R(0)};
+                        obs_own(eb, dk, z, rpy0, zero3, zero3);
+                        const int nb = nearest_two(S.rdx, S.rdy, dg * N, dk, n_new);
+                        obs_nbr(eb, S.rdx, S.rdy, dg * N, dk, (nb & 0xff) - 1, (nb >> 8) - 1);
+                    } else if (dk < ei[I_N * G + dg]) {
+                        // a row the old episode used and the new one does not: own and neighbour entries (the late
+                        // cattle pass zeroes its cattle entries; the rest of the row is constant zero)
+                        for (int c = 0; c < 14; c += 2) st2(eb, dk * 86 + c, 0.0f, 0.0f);
+                    }
+                }
+            }
+        }
         if constexpr (SPLIT) lds_wait(fl + F_S, 2 * Gv * N, p.err);   // spacing and cattle terms (cow waves)
         if (envl && task) {
             const int n = f_n;
@@ -1328,12 +1373,39 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         // (grab is readfirstlane'd, the queue length a ballot count).
         // sep: one of a cow's two inputs to its velocity update is complete -- its alpha row (aux, auy) or its
         // shepherd sum (td[u], td[GM + u]); the second arrival runs the update
+        // late: the second input computes the new velocity into LDS (nv) and marks it ready (+8); the final pass
+        // after the reset list arrives with +4; whichever of the two comes last stores the velocity -- the new
+        // episode's draw for a fast-reset env
+        R* const nv = S.td + 2 * G * M;
+        auto store_final = [&](int u) {
+            const int g = qdiv(u, M, 1.0f / (float)M);
+            const long long ci = (long long)e0 * M + u;
+            R vx = nv[u], vy = nv[G * M + u];
+            if (fast && ei[I_RESET * G + g])
+                reset_cow_vel(p, ci, p.env_off + e0 + g, u - g * M, (uint32_t)ei[I_EPISODE * G + g], vx, vy);
+            CH_STS(&p.cattle[2 * CS + ci], vx); CH_STS(&p.cattle[3 * CS + ci], vy);
+        };
         auto arrive = [&](int u) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
             const int old = __hip_atomic_fetch_add(&S.cnt[u], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (old == 1) {
+            if ((old & 3) == 1) {
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-                velocity_update(p, S, M, e0, u, S.td[u], S.td[G * M + u]);
+                if (!late) {
+                    velocity_update(p, S, M, e0, u, S.td[u], S.td[G * M + u]);
+                } else {
+                    velocity_update(p, S, M, e0, u, S.td[u], S.td[G * M + u], nv, G * M);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                    const int o2 = __hip_atomic_fetch_add(&S.cnt[u], 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (o2 & 4) store_final(u);
+                }
+            }
+        };
+        auto arrive_final = [&](int u) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+            const int old = __hip_atomic_fetch_add(&S.cnt[u], 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (old & 8) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+                store_final(u);
             }
         };
         auto alpha_step = [&]() -> bool {
@@ -1437,7 +1509,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                 }
                 if (wn != 0) atomicAdd(&ei[I_HERD * G + g], 1);
             }
-            if (j < m_obs && wobs) obs_cattle(obs_wg + g * RW, S.dx, S.dy, b0, j, n, cat_off, qix, qiy);
+            if (j < m_obs && wobs && !late) obs_cattle(obs_wg + g * RW, S.dx, S.dy, b0, j, n, cat_off, qix, qiy);
             }
             // H counts finished items, so a wave still busy with an alpha chunk does not hold the drone wave up
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -1466,13 +1538,15 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                 }
             }
         }
-        for (;;) {   // getEulerFromQuaternion of the new attitudes (BaseAviary.py:704-766): the own row's roll,
-                     // pitch, yaw and the next step's PID input (the Euler cache)
+        // getEulerFromQuaternion of the new attitudes (BaseAviary.py:704-766): the own row's roll, pitch, yaw and
+        // the next step's PID input (the Euler cache); late: after the reset list, skipping fast-reset envs
+        auto euler_pass = [&]() {
+          for (;;) {
             const int b = grab(fl + C_EULER, 64, skip_post), u = b + lane;
             if (b >= Gv * N) break;
             if (u < Gv * N) {
                 const int g = qdiv(u, N, rN), k = u - g * N;
-                if (k < ei[I_N * G + g]) {
+                if (k < ei[I_N * G + g] && !(fast && ei[I_RESET * G + g])) {
                     const int GN = G * N;
                     const R qq[4] = {S.dq[u], S.dq[GN + u], S.dq[2 * GN + u], S.dq[3 * GN + u]};
                     R r3[3];
@@ -1483,7 +1557,9 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                     if (wobs) obs_rpy(obs_wg + g * RW, k, r3);
                 }
             }
-        }
+          }
+        };
+        if (!late) euler_pass();
         if constexpr (PW) {
             while (alpha_step()) {   // the rest of the alpha work (the current env first)
             }
@@ -1605,7 +1681,46 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         if (tid == 64) TS(37, (long long)clock64());
         const int nr = ei[NR_AT];
         if (ct == 0) TS(30, (long long)nr);
-        if (nr) {   // uniform across the cow waves
+        if (nr && ct == 0) TS(52, (long long)clock64());
+        if (late) {
+            euler_pass();
+            // final pass, each cow on its phase-0 lane: cattle observation entries (of the new episode for a
+            // fast-reset env, whose new positions and velocities this lane writes too), then the flocking envs'
+            // third arrival
+            for (int u = ct; u < Gv * M; u += CW) {
+                const int g = qdiv(u, M, rM), j = u - g * M;
+                const bool rs_ = fast && ei[I_RESET * G + g];
+                const int n_old = ei[I_N * G + g];
+                const long long ci = (long long)e0 * M + u;
+                if (rs_) {
+                    const R x = S.spx[u], y = S.spy[u];
+                    p.cattle[0 * CS + ci] = x; p.cattle[1 * CS + ci] = y;
+                    if (!ei[I_FLOCK * G + g]) {   // no flock update: the velocity is written here
+                        R vx, vy;
+                        reset_cow_vel(p, ci, p.env_off + e0 + g, j, (uint32_t)ei[I_EPISODE * G + g], vx, vy);
+                        p.cattle[2 * CS + ci] = vx; p.cattle[3 * CS + ci] = vy;
+                    }
+                    if (wobs && j < m_obs) {
+                        const int n_new = ei[I_NEWN * G + g];
+                        float* eb = obs_wg + g * RW;
+                        for (int r = 0; r < N; ++r) {
+                            if (r >= n_new && r >= n_old) break;
+                            if (r < n_new) {
+                                R dx, dy, dz;
+                                reset_drone_xyz(r, n_new, dx, dy, dz);
+                                st2(eb, r * 86 + cat_off + 2 * j, (float)(x - dx), (float)(y - dy));
+                            } else {
+                                st2(eb, r * 86 + cat_off + 2 * j, 0.0f, 0.0f);
+                            }
+                        }
+                    }
+                } else if (wobs && j < m_obs) {
+                    obs_cattle(obs_wg + g * RW, S.dx, S.dy, g * N, j, n_old, cat_off, S.cx[u], S.cy[u]);
+                }
+                if (ei[I_FLOCK * G + g]) arrive_final(u);
+            }
+        }
+        if (nr && !fast) {   // uniform across the cow waves
             // ---- SB3 auto-reset of the listed envs (BaseAviary.reset, BaseAviary.py:280-331), rebuilt from
             // the pre-step scalars (NUM_DRONES draw, spawn index + 1, episode) while the drone wave still
             // computes rewards: the terminal observation (on request), then the bodies and observation rows.
@@ -1644,7 +1759,9 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                                   cvx_r[i], cvy_r[i]);
                 }
             }
+            if (ct == 0) TS(55, (long long)clock64());
             cow_sync(fl + F_X1, W1, true, p.err);   // terminal observation read; this step's stores done; rd* and NEWN seen
+            if (ct == 0) TS(53, (long long)clock64());
             if (dit) {
                 const int k0 = qdiv(ct, N, rN), g = rl[k0], k = ct - k0 * N, ud = g * N + k;
                 const int n = ei[I_NEWN * G + g];
@@ -1681,6 +1798,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                     reset_cow_store(p, (long long)e0 * M + uc, x, y, vx, vy);
                     if (wobs && j < m_obs) obs_cattle(obs_wg + g * RW, S.rdx, S.rdy, g * N, j, ei[I_NEWN * G + g], cat_off, x, y);
                 }
+            if (ct == 0) TS(54, (long long)clock64());
         }
     }
     if (tid == 0) TS(35, (long long)clock64());
