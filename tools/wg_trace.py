@@ -63,6 +63,13 @@ def trace(mode, E, n, m, prec, G=None, B=None, steps=4):
         print(f"   at the last barrier: drone wave {rel(35):.0f} cow wave 1 {rel(36):.0f} (F_R seen {rel(37):.0f})")
         nw = blk.value // 64
         ws = np.where(t[:, 52:52 + nw] > 0, t[:, 52:52 + nw] - t[:, 2:3], 0)
+        rs = t[:, 30] > 0
+        if rs.any():
+            r3 = lambda k: (t[rs, k] - t[rs, 2]).mean()  # noqa: E731
+            print(f"   resetting WGs ({int(rs.sum())}), cow wave 1: reset list seen {r3(52):.0f} bodies computed {r3(55):.0f} "
+                  f"sync passed {r3(53):.0f} stores issued {r3(54):.0f} | drone book {r3(7):.0f} | cow waves done (max per WG) "
+                  f"{(t[rs, 41:41 + blk.value // 64 - 1].max(axis=1) - t[rs, 2]).mean():.0f} vs non-resetting "
+                  f"{(t[~rs, 41:41 + blk.value // 64 - 1].max(axis=1) - t[~rs, 2]).mean():.0f}")
         print(f"   wave start (cycles after wave 0's): mean {' '.join(f'{ws[:, w].mean():.0f}' for w in range(nw))} | "
               f"last wave q50/max {np.percentile(ws.max(axis=1), 50):.0f}/{ws.max():.0f} | first barrier passed {rel(3):.0f}")
         print(f"   alpha passes (cow wave 1): cheap done {rel(38):.0f} all cheap (F_C) {rel(39):.0f} full done {rel(18):.0f}"
