@@ -833,7 +833,9 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
     // (alpha row, shepherd sum, final pass).  fast (late, no terminal observation requested): the reset envs'
     // new bodies and observation rows are then written by the lanes that wrote their old values (drones: the
     // drone wave; cattle state: the phase-0 lane; obs: the single late writer), with no drain or sync.
-    const bool late = sep, fast = late && !p.terminal_obs;
+    // Only the 16-env x 4-drone geometry: at 2 drones x 8 cattle (C2/C3, 3 cow waves) the final pass after the
+    // reset list costs more than the reset sync it saves (C2 16.2 -> 17.2 us, C3 17.1 -> 17.8 us).
+    const bool late = sep && GT == 16 && NT == 4, fast = late && !p.terminal_obs;
     float* obs_wg = p.obs + (long long)e0 * RW;
     // final per-env scalars, held by the drone wave's env lanes until the write-back
     int f_n = 0, f_sc = 0, f_scA = 0, f_hp = 0, f_level = 0, f_tally = 0, f_spawn = 0, f_active = 0, f_episode = 0;
