@@ -44,9 +44,13 @@ def test_configs3_full_size_spot_parity():
     rng = np.random.default_rng(11)
     pick = np.unique(np.concatenate([[0, 1, 15, 16, E - 16, E - 1], rng.choice(E, 58, replace=False)]))
     acts = rng.uniform(-1, 1, (E, n, 4)).astype(np.float32)
-    obs, rew, te, tr = b.step(torch.tensor(acts, device=b.device), autoreset=True)
+    # no terminal observation requested: the workgroups take the sync-free auto-reset path
+    obs, rew, te, tr = b.step(torch.tensor(acts, device=b.device), autoreset=True, terminal_obs=False)
     torch.cuda.synchronize()
     obs, rew, te, tr = obs.cpu().numpy(), rew.cpu().numpy(), te.cpu().numpy(), tr.cpu().numpy()
+    resets = np.nonzero(b.reset_happened.cpu().numpy())[0]
+    assert len(resets) >= 4, "the checked step should auto-reset some envs"
+    pick = np.unique(np.concatenate([pick, resets[:24]]))
     after = b.get_state()
     table = spawn_table(m)
     for e in pick:
@@ -66,6 +70,32 @@ def test_configs3_full_size_spot_parity():
         assert int(after["step_counter"][e]) == int(want["step_counter"]), e
     assert len(pick) >= 60
     b.close()
+
+
+def test_sync_free_reset_path_equals_synced_path():
+    """At configs[3]'s size the step kernel rebuilds auto-reset envs without a cow-wave sync when no terminal
+    observation is requested, and through the drained, synced path when one is: 150 steps of both from the
+    same start give bit-identical observations, rewards, flags and state, step by step."""
+    import torch
+    from cattleherd.env import HerdBatch
+    E, n, m = 4096, 4, 16
+    hs = [HerdBatch(E, n, m), HerdBatch(E, n, m)]
+    for h in hs:
+        h.reset()
+    nres = 0
+    for t in range(150):
+        hs[0].step(random_actions=True, autoreset=True, terminal_obs=True)
+        hs[1].step(random_actions=True, autoreset=True, terminal_obs=False)
+        for x, y in ((hs[0].obs, hs[1].obs), (hs[0].reward, hs[1].reward), (hs[0].terminated, hs[1].terminated),
+                     (hs[0].truncated, hs[1].truncated), (hs[0].reset_happened, hs[1].reset_happened)):
+            assert np.array_equal(x.cpu().numpy(), y.cpu().numpy(), equal_nan=x.dtype.is_floating_point), t
+        nres += int(hs[0].reset_happened.sum())
+    s0, s1 = hs[0].get_state(), hs[1].get_state()
+    for k in s0:
+        assert np.array_equal(np.asarray(s0[k]), np.asarray(s1[k]), equal_nan=np.asarray(s0[k]).dtype.kind == "f"), k
+    assert nres > 500, nres
+    for h in hs:
+        h.close()
 
 
 def test_configs0_one_env_one_drone_lockstep():
