@@ -1567,21 +1567,22 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             }
             cow_sync(fl + F_W, W1, false, p.err);   // every alpha row (aux, auy) is written
             if (ct == 0) TS(21, (long long)clock64());
-            // shepherd / predator terms and the velocity update, one flocking env per wave at a time in its
-            // slot: the env's (cow, drone) items, then each cow's terms in drone order
-            const int MN = M * N;
+            // shepherd / predator sums and the velocity update, one cow per lane with its drones' terms in
+            // registers (shepherd_sum, drone order), 64 / M flocking envs per wave at a time
+            const int per = M <= 64 ? 64 / M : 1;
             for (;;) {
-                const int f = grab(fl + C_DELTA, 1, skip_post);
-                if (f >= nf) break;
+                const int f0 = grab(fl + C_DELTA, per, skip_post);
+                if (f0 >= nf) break;
                 CHUNK_T0;
-                const int g = flist[f], n = ei[I_N * G + g];
-                for (int q = lane; q < MN; q += 64) {
-                    const int j = qdiv(q, N, rN), k = q - j * N;
-                    if (k < n) delta_term(S, N, g * M + j, g, k, tb, tf, q, MN);
+                for (int q = lane; q < per * M; q += 64) {
+                    const int fi = per > 1 ? qdiv(q, M, rM) : 0, j = q - fi * M, f = f0 + fi;
+                    if (f < nf) {
+                        const int g = flist[f], u = g * M + j;
+                        R ddx, ddy;
+                        shepherd_sum<R, NT>(S, N, u, g, ei[I_N * G + g], ddx, ddy);
+                        velocity_update(p, S, M, e0, u, ddx, ddy);
+                    }
                 }
-                wave_sync();
-                for (int j = lane; j < M; j += 64) flock_combine(p, S, N, M, e0, g * M + j, n, tb, tf, j * N, MN);
-                wave_sync();   // the slot is free for the next env
                 CHUNK_T1(3);
             }
             if (ct == 0) TS(16, (long long)clock64());
