@@ -72,14 +72,16 @@ def test_configs3_full_size_spot_parity():
     b.close()
 
 
-def test_sync_free_reset_path_equals_synced_path():
+@pytest.mark.parametrize("physics", ["pyb", "pyb_gnd_drag_dw"])
+def test_sync_free_reset_path_equals_synced_path(physics):
     """At configs[3]'s size the step kernel rebuilds auto-reset envs without a cow-wave sync when no terminal
     observation is requested, and through the drained, synced path when one is: 150 steps of both from the
-    same start give bit-identical observations, rewards, flags and state, step by step."""
+    same start give bit-identical observations, rewards, flags and state, step by step (default physics and
+    the all-effects variant, whose carried rpm / body rates a reset also clears)."""
     import torch
     from cattleherd.env import HerdBatch
     E, n, m = 4096, 4, 16
-    hs = [HerdBatch(E, n, m), HerdBatch(E, n, m)]
+    hs = [HerdBatch(E, n, m, physics=physics), HerdBatch(E, n, m, physics=physics)]
     for h in hs:
         h.reset()
     nres = 0
