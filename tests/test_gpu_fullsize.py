@@ -72,8 +72,8 @@ def test_configs3_full_size_spot_parity():
     b.close()
 
 
-@pytest.mark.parametrize("physics", ["pyb", "pyb_gnd_drag_dw"])
-def test_sync_free_reset_path_equals_synced_path(physics):
+@pytest.mark.parametrize("physics,precision", [("pyb", "f64"), ("pyb_gnd_drag_dw", "f64"), ("pyb", "f32")])
+def test_sync_free_reset_path_equals_synced_path(physics, precision):
     """At configs[3]'s size the step kernel rebuilds auto-reset envs without a cow-wave sync when no terminal
     observation is requested, and through the drained, synced path when one is: 150 steps of both from the
     same start give bit-identical observations, rewards, flags and state, step by step (default physics and
@@ -81,7 +81,7 @@ def test_sync_free_reset_path_equals_synced_path(physics):
     import torch
     from cattleherd.env import HerdBatch
     E, n, m = 4096, 4, 16
-    hs = [HerdBatch(E, n, m, physics=physics), HerdBatch(E, n, m, physics=physics)]
+    hs = [HerdBatch(E, n, m, physics=physics, precision=precision), HerdBatch(E, n, m, physics=physics, precision=precision)]
     for h in hs:
         h.reset()
     nres = 0
