@@ -133,7 +133,9 @@ typedef struct ch_step_io {
     float* reward;             /* device [E][K] (required) */
     uint8_t* terminated;       /* device [E][K] (required) */
     uint8_t* truncated;        /* device [E][K] (required) */
-    float* terminal_obs;       /* optional device [E][R][86]: pre-reset obs of envs that auto-reset */
+    float* terminal_obs;       /* optional device [E][R][86]: pre-reset obs of envs that auto-reset; leave NULL
+                                  when not needed: the 16-env x 4-drone geometry then rebuilds reset envs
+                                  without a workgroup sync (same outputs) */
     uint8_t* agent_active;     /* optional device [E][N]: MARL live-agent mask after this step */
     uint8_t* reset_happened;   /* optional device [E]: 1 where the env auto-reset in this call */
     uint32_t flags;            /* CH_STEP_* */
