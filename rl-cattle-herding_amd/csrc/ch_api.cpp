@@ -365,7 +365,9 @@ int ch_create(const ch_config* c, int64_t n_envs, int32_t device, ch_handle** ou
             V2Layout(16, 4, 16, h->P, c->mode, (int)h->rsize).bytes() <= budget) {
             h->G = 16;
             h->lds = V2Layout(16, 4, 16, h->P, c->mode, (int)h->rsize).bytes();
-            h->block = c->physics == CH_PHYS_PYB ? CH_V2_MAX_BLOCK : CH_V2_MAX_BLOCK_PW;
+            // f32: 512 threads (tools/f32_geom_probe.py: 419 vs 273 M env-steps/s at 262144 envs, 1.5 % slower
+            // at 4096; f64 keeps 768, 230 vs 225 M at 262144 and 1 % faster at 4096)
+            h->block = (c->physics == CH_PHYS_PYB && h->rsize == 8) ? CH_V2_MAX_BLOCK : CH_V2_MAX_BLOCK_PW;
         }
         // measured (tools/ab/marl.py, MI355X, 4096 envs): the dataflow kernel wins for every CTDE size
         // (2x8 19.4 vs 41.1 us, 8x16 39.7 vs 55.8, 12x16 59.9 vs 67.1) and for MARL with up to 16
