@@ -20,12 +20,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "rl-cattle-herding_amd"))
 
 WORKLOADS = {
-    # name: (mode, envs/GPU, drones, cattle, description)
-    "c4": ("ctde", 4096, 4, 16, "BASELINE configs[3]: 4096 envs/GPU x (4 drones, 16 cattle), CTDE obs (12,86), "
-                                "random-action rollout with auto-reset"),
-    "c2": ("ctde", 1024, 2, 8, "BASELINE configs[1]: 1024 envs x (2 drones, 8 cattle), CTDE, random actions"),
-    "c3": ("ctde", 4096, 2, 8, "BASELINE configs[2] env side: 4096 envs x (2 drones, 8 cattle), CTDE"),
-    "c5": ("marl", 4096, 4, 32, "BASELINE configs[4]: 4096 envs x (4 drones, 32 cattle), MARL per-agent obs (4,86)"),
+    # name: (mode, envs/GPU, drones, cattle, compat, description)
+    "c4": ("ctde", 4096, 4, 16, True, "BASELINE configs[3]: 4096 envs/GPU x (4 drones, 16 cattle), CTDE obs (12,86), "
+                                      "random-action rollout with auto-reset"),
+    "c2": ("ctde", 1024, 2, 8, True, "BASELINE configs[1]: 1024 envs x (2 drones, 8 cattle), CTDE, random actions"),
+    # configs[2] is a training run: NaN-safe rewards (compat = 0), else every 2-drone reward is NaN
+    "c3": ("ctde", 4096, 2, 8, False, "BASELINE configs[2]: 4096 envs x (2 drones, 8 cattle), CTDE, NaN-safe rewards "
+                                      "(compat=0, the PPO training configuration)"),
+    "c5": ("marl", 4096, 4, 32, True, "BASELINE configs[4]: 4096 envs x (4 drones, 32 cattle), MARL per-agent obs (4,86)"),
 }
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_F32_PEAK_TFLOPS = 157.3   # f32-input MFMA: 64 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz (dense)
@@ -33,9 +35,14 @@ POLICY_GOLDEN = os.path.join(ROOT, "tests", "golden", "policy_ctde_v16_6.npz")
 PROFILES = os.path.join(ROOT, "profiles")
 
 
-def algorithmic_bytes(mode, n, m, rows, real_bytes):
-    """HBM bytes one env-step must move with this SoA layout (DESIGN.md "Roofline")."""
+def algorithmic_bytes(mode, n, m, rows, real_bytes, eval_metrics=True):
+    """HBM bytes one env-step moves with this SoA layout (DESIGN.md "Roofline"), everything the kernel reads
+    and writes counted once: the carried state, its Euler-angle cache and per-env flags, the evaluation
+    accumulators and the outputs."""
     drone = 22 * real_bytes * 2 * n                   # state read + write
+    euler = 3 * real_bytes * 2 * n                    # Euler angles of the stored attitude, read + written
+    evald = 8 * 2 * n if eval_metrics else 0          # update_evaluation_metrics' per-drone distance, read + written
+    tags = 2 * 2 + 8 * 2                              # stale flags (2 x u8) and the obs-buffer tag, read + written
     actions = 16 * n                                  # drawn actions written to actions_out
     cattle = (4 * real_bytes + 2 * real_bytes + real_bytes) * m   # read pos+vel, write pos, vel every 2nd step
     env = 2 * (9 * 4 + 2 * real_bytes)                # env scalars read + write
@@ -46,7 +53,14 @@ def algorithmic_bytes(mode, n, m, rows, real_bytes):
     obs = n * (10 + 4 + 2 * min(m, 16)) * 4
     k = 1 if mode == "ctde" else n
     flags = 4 * k + 2 * k + n + 1                     # reward, terminated, truncated, agent_active, reset flag
-    return drone + actions + cattle + env + metrics + obs + flags
+    return drone + euler + evald + tags + actions + cattle + env + metrics + obs + flags
+
+
+def survey_bytes(mode, n, m, rows):
+    """SURVEY.md 8(d)'s reference byte model (fp32 SoA, minimal carried state, the full observation block):
+    B_step = 16N (actions) + 176N (drone R/W) + 32M (cattle R/W) + 64 (env scalars R/W) + 344R (obs) + 6K."""
+    k = 1 if mode == "ctde" else n
+    return 16 * n + 176 * n + 32 * m + 64 + 344 * rows + 6 * k
 
 
 def pmc_record(workload, dtype):
@@ -160,6 +174,42 @@ def ppo_rollout(b, d, T=32):
     return out
 
 
+def marl_vec_rollout(n, m, E, steps, warmup, burn_in):
+    """configs[4] through the batched RLlib multi-agent surface (cattleherd.marl_vec_env): random actions,
+    the wrapper semantics and in-launch resets; env-steps/s of the zero-copy tensor path (one launch plus the
+    output views per step, terminal observations requested), and of the dict path (per-env agent dicts built on
+    the host from one copy of the outputs) on a few steps."""
+    import torch
+    from cattleherd.marl_vec_env import CattleHerdMultiAgentVecEnv
+    venv = CattleHerdMultiAgentVecEnv(E, {"num_drones": n, "num_cattle": m, "min_drones": n, "max_drones": n})
+    venv.reset()
+    g = torch.Generator(device=venv.batch.device).manual_seed(0)
+    acts = [torch.rand((E, n, 4), generator=g, device=venv.batch.device) * 2 - 1 for _ in range(8)]
+    for t in range(burn_in + warmup):
+        venv.step_tensors(acts[t % 8])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ended = 0
+    for t in range(steps):
+        out = venv.step_tensors(acts[t % 8])
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ended = int(out["all_done"].sum())
+    nd = min(steps, 10)
+    venv.refresh_agents()
+    host = [a.cpu().numpy() for a in acts]
+    t1 = time.perf_counter()
+    for t in range(nd):
+        venv.step(host[t % 8])
+    dd = time.perf_counter() - t1
+    venv.close()
+    return {"tensor_env_steps_per_s": E * steps / dt, "tensor_ms_per_step": dt / steps * 1e3,
+            "dict_env_steps_per_s": E * nd / dd, "dict_ms_per_step": dd / nd * 1e3, "dict_steps": nd,
+            "ended_last_step": ended,
+            "note": "tensor path: ch_step with terminal observations + the reset/agent-mask views; dict path: "
+                    "RLlibMultiAgentWrapper-style dicts for every env built on the host"}
+
+
 def cpu_baseline(mode, n, m, seconds=12.0):
     """The CPU oracle (scalar fp64 C port, OpenMP one env per thread) on a bounded sample, on every
     core this process may use: OMP_NUM_THREADS when the pool sets it (16 per GPU on the MI355X
@@ -221,6 +271,12 @@ def main():
     ap.add_argument("--graph", type=int, default=0,
                     help="steps per captured HIP graph in the timed loop (0 = one host launch per step)")
     ap.add_argument("--backend", default="nccl", help="process-group backend (nccl = RCCL over xGMI)")
+    ap.add_argument("--burn-in", type=int, default=1200,
+                    help="untimed random-action steps before the warmup, so the timed steps start from the "
+                         "steady-state spread of episode phases (auto-resets at their long-run rate); 1200 = the "
+                         "level-7 CTDE episode cap (80 s at 15 steps/s)")
+    ap.add_argument("--marl-vec", action="store_true",
+                    help="MARL workloads: also time the batched multi-agent surface (tensor and dict paths)")
     ap.add_argument("--launch-check", action="store_true",
                     help="run only the multi-rank plumbing (process group, env ranges, all-reduce); no GPU")
     args = ap.parse_args()
@@ -246,11 +302,11 @@ def main():
         print(f"bench: --gpus {args.gpus} but the process group has {world} ranks", file=sys.stderr)
         sys.exit(3)
 
-    mode, E, n, m, desc = WORKLOADS[args.workload]
+    mode, E, n, m, compat, desc = WORKLOADS[args.workload]
     if args.envs:
         E = args.envs
     b = HerdBatch(E, n, m, mode=mode, precision=args.precision, env_id_offset=D.env_offset(rank, E),
-                  physics=args.physics)
+                  physics=args.physics, compat=compat)
     print(f"bench: rank {rank}/{world} device {torch.cuda.current_device()} envs "
           f"[{D.env_offset(rank, E)}, {D.env_offset(rank, E) + E})", file=sys.stderr, flush=True)
     stream = torch.cuda.current_stream()
@@ -270,6 +326,10 @@ def main():
         return mhost.numpy().copy()
 
     b.reset()
+    # burn-in (untimed, before the warmup): the envs leave the common starting point, so the timed steps see
+    # episode phases -- and auto-resets -- at their steady-state spread rather than K steps of fresh episodes
+    for _ in range(args.burn_in):
+        b.step(random_actions=True, autoreset=True, terminal_obs=False)
     for _ in range(args.warmup):
         b.step(random_actions=True, autoreset=True, terminal_obs=False)
     # the timed loop: K steps as whole graph replays of `chunk` steps (plus single launches for the rest)
@@ -318,9 +378,11 @@ def main():
     kern_us = s_ev.elapsed_time(e_ev) / nk * 1000.0
     rb = 8 if args.precision == "f64" else 4
     bytes_step = algorithmic_bytes(mode, n, m, b.obs_rows, rb)
+    survey_step = survey_bytes(mode, n, m, b.obs_rows)
     if args.physics != "pyb":
         bytes_step += 2 * 7 * rb * n   # carried last_clipped_action + rpy_rates, read and written
     achieved = bytes_step * E / (kern_us * 1e-6) / 1e9
+    achieved_survey = survey_step * E / (kern_us * 1e-6) / 1e9
     traffic, traffic_src = (pmc_traffic(args.workload, args.precision)
                             if E == WORKLOADS[args.workload][1] and args.physics == "pyb" else (None, None))
     kname = kernel_name(b)
@@ -333,7 +395,9 @@ def main():
             "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1000.0, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": args.precision, "agent_steps_per_s": value * n,
-            "data": "synthetic: Philox4x32 random VEL actions in-kernel, spawn table from config/cattle_positions.yaml",
+            "data": "synthetic: Philox4x32 random VEL actions in-kernel, spawn table from config/cattle_positions.yaml; "
+                    f"envs burnt in for {args.burn_in} untimed steps before the warmup (steady-state episode phases, "
+                    "auto-resets inside the timed steps at their long-run rate)",
             "launch": f"HIP graph of {chunk} steps per replay" if graph is not None else "one host launch per step",
             "rollout_end_us": rollout_end_us,
             "config": {"workload": desc, "envs_per_gpu": E, "num_drones": n, "num_cattle": m, "mode": mode,
@@ -342,7 +406,13 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_src, "algorithmic_bytes_per_launch": bytes_step * E,
-                         "kernel": kname, "kernel_us": kern_us, "bytes_per_env_step": bytes_step},
+                         "kernel": kname, "kernel_us": kern_us, "bytes_per_env_step": bytes_step,
+                         "byte_model": "this layout: f64 state, Euler cache, eval accumulators, flags, the obs "
+                                       "entries a step changes (bench.py algorithmic_bytes)"},
+            "roofline_survey": {"bound": "hbm", "achieved": achieved_survey, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": achieved_survey / HBM_PEAK_GBS, "bytes_per_env_step": survey_step,
+                                "algorithmic_bytes_per_launch": survey_step * E, "kernel_us": kern_us,
+                                "byte_model": "SURVEY.md 8(d): fp32 SoA, minimal carried state, full obs block"},
             "valu": (valu_issue(args.workload, args.precision, kern_us)
                      if E == WORKLOADS[args.workload][1] and args.physics == "pyb" else None),
             "rollout_metrics": {"episodes": mv[1], "mean_return": (mv[2] / mv[1]) if mv[1] else None,
@@ -350,6 +420,9 @@ def main():
         }
         if args.policy and mode == "ctde":
             out["policy_rollout"] = policy_rollout(b, n, args.steps, args.warmup)
+        if args.marl_vec and mode == "marl":
+            b.close()
+            out["marl_vec_env"] = marl_vec_rollout(n, m, E, args.steps, args.warmup, args.burn_in)
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(mode, n, m, args.cpu_seconds)
         elif world == 1:

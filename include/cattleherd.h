@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CH_ABI_VERSION 3
+#define CH_ABI_VERSION 4
 
 enum {
     CH_OK = 0,
@@ -140,6 +140,9 @@ typedef struct ch_step_io {
     uint8_t* reset_happened;   /* optional device [E]: 1 where the env auto-reset in this call */
     uint32_t flags;            /* CH_STEP_* */
     uint32_t _pad;
+    double* episode_stats;     /* optional device [E][2]: where an episode ends in this call, its return (the sum of
+                                  the float64 rewards the reference returns) and length in steps -- SB3 Monitor's
+                                  info["episode"] "r" and "l" (CTDECattleHerder.py:91-99); other rows untouched */
 } ch_step_io;
 
 /* Replaces: BaseAviary.step (sb3_envs/BaseAviary.py:335-465) for every env at once — VEL action →

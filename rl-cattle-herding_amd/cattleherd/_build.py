@@ -35,14 +35,18 @@ def build(force=False, verbose=False, extra_flags=(), out=None):
     if not force and out is None and not _stale():
         return LIB
     os.makedirs(BUILD, exist_ok=True)
-    objs = []
+    objs, procs = [], []
+    # the translation units compile in parallel (ch_step.hip's instantiations dominate the build)
     for src in SOURCES:
         obj = os.path.join(BUILD, src + ("".join(extra_flags).replace("-", "_") if extra_flags else "") + ".o")
         cmd = [HIPCC, *FLAGS, *extra_flags, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
-        subprocess.run(cmd, check=True)
+        procs.append((cmd, subprocess.Popen(cmd)))
         objs.append(obj)
+    failed = [cmd for cmd, p in procs if p.wait() != 0]
+    if failed:
+        raise subprocess.CalledProcessError(1, failed[0])
     tmp = lib_out + ".tmp"
     cmd = [HIPCC, *FLAGS, "-shared", *objs, "-o", tmp]
     if verbose:

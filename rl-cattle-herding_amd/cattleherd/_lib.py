@@ -15,7 +15,7 @@ CH_PREC_F64, CH_PREC_F32 = 0, 1
 CH_STEP_AUTORESET, CH_STEP_RANDOM_ACTIONS = 0x1, 0x2
 METRIC_NAMES = ("steps", "episodes", "return_sum", "length_sum", "terminated", "truncated", "nan_rewards",
                 "effectiveness_sum")
-ABI_VERSION = 3
+ABI_VERSION = 4
 # Physics enum (utils/enums.py:13-21, include/cattleherd.h CH_PHYS_*)
 PHYSICS = {"pyb": 0, "dyn": 1, "pyb_gnd": 2, "pyb_drag": 3, "pyb_dw": 4, "pyb_gnd_drag_dw": 5, "dyn_rk4": 6}
 
@@ -43,7 +43,8 @@ class ChStepIO(ctypes.Structure):
     _fields_ = [("actions", ctypes.c_void_p), ("actions_out", ctypes.c_void_p), ("obs", ctypes.c_void_p),
                 ("reward", ctypes.c_void_p), ("terminated", ctypes.c_void_p), ("truncated", ctypes.c_void_p),
                 ("terminal_obs", ctypes.c_void_p), ("agent_active", ctypes.c_void_p),
-                ("reset_happened", ctypes.c_void_p), ("flags", ctypes.c_uint32), ("_pad", ctypes.c_uint32)]
+                ("reset_happened", ctypes.c_void_p), ("flags", ctypes.c_uint32), ("_pad", ctypes.c_uint32),
+                ("episode_stats", ctypes.c_void_p)]
 
 
 class ChMlp(ctypes.Structure):

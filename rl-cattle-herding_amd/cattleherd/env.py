@@ -76,6 +76,8 @@ class HerdBatch:
         self.agent_active = torch.zeros((self.n_envs, num_drones), dtype=torch.uint8, **z)
         self.reset_happened = torch.zeros(self.n_envs, dtype=torch.uint8, **z)
         self.actions = torch.zeros((self.n_envs, num_drones, 4), dtype=torch.float32, **z)
+        # per env: return and length of the last episode that ended (rows rewritten only where one ends)
+        self.episode_stats = torch.zeros((self.n_envs, 2), dtype=torch.float64, **z)
         # the step io block: output pointers are fixed for the life of the batch, so a step only
         # rewrites the action pointers and flags (keeps the per-step host cost to one ctypes call)
         self._io = L.ChStepIO()
@@ -85,6 +87,7 @@ class HerdBatch:
         self._io.truncated = self.truncated.data_ptr()
         self._io.agent_active = self.agent_active.data_ptr()
         self._io.reset_happened = self.reset_happened.data_ptr()
+        self._io.episode_stats = self.episode_stats.data_ptr()
         self._io_ref = ctypes.byref(self._io)
         self._ch_step = L.lib().ch_step
         self._raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
@@ -120,14 +123,27 @@ class HerdBatch:
                                       None if cv is None else cv.ctypes.data, obs, self._stream()), self.handle)
         return self.obs
 
-    def step(self, actions=None, autoreset=True, random_actions=False, terminal_obs=True, step_io=None):
+    def step(self, actions=None, autoreset=True, random_actions=False, terminal_obs=True, obs_out=None):
         """BaseAviary.step for every env.  ``actions``: float32 [E, num_drones, 4] device tensor.
 
         ``self.obs`` is overwritten in place and is read-only to the caller: the step kernel stores only
         the entries that change (own state, neighbours, cattle), the constant-zero bytes of each block
         (rows >= NUM_DRONES, the action-buffer block) stay from the last full write.  After writing
-        into ``self.obs``, call ``invalidate_obs()`` so the next step rewrites every block in full."""
+        into ``self.obs``, call ``invalidate_obs()`` so the next step rewrites every block in full.
+        ``obs_out`` (float32 [E, obs_rows, 86] device tensor, 16-byte aligned): write this step's
+        observations there instead of ``self.obs`` (a switch of buffers makes the next step write every
+        block in full, ch_api.cpp note_obs_buffer)."""
         io = self._io
+        if obs_out is not None:
+            if (obs_out.dtype != self.torch.float32 or obs_out.device != self.device or not obs_out.is_contiguous()
+                    or tuple(obs_out.shape) != tuple(self.obs.shape)):
+                raise ValueError(f"obs_out must be a contiguous float32 {tuple(self.obs.shape)} tensor on {self.device}")
+            io.obs = obs_out.data_ptr()
+            try:
+                _, rew, te, tr = self.step(actions, autoreset, random_actions, terminal_obs)
+            finally:
+                io.obs = self.obs.data_ptr()
+            return obs_out, rew, te, tr
         flags = (L.CH_STEP_AUTORESET if autoreset else 0) | (L.CH_STEP_RANDOM_ACTIONS if random_actions else 0)
         if random_actions:
             io.actions = None
@@ -163,8 +179,9 @@ class HerdBatch:
         """Capture ``steps`` random-action steps into a HIP graph (torch.cuda.CUDAGraph); ``replay()``
         then runs them with one launch from the host.  Every launch parameter is constant across steps
         (the Philox counter lives in the env state) and the state-dependent switches (Euler cache,
-        observation bytes) are device words the kernel reads at run time, so a replay is exactly
-        ``steps`` calls of ``step(random_actions=True)``, also after reset()/set_state()/invalidate_obs().
+        observation bytes) are per-env device flags the kernel reads at run time, so a replay is exactly
+        ``steps`` calls of ``step(random_actions=True)``, also after reset()/set_state()/invalidate_obs()
+        and after steps into another observation buffer (``obs_out``: the switch raises the flags).
         Nothing runs at capture time."""
         torch = self.torch
         side = torch.cuda.Stream(device=self.device)

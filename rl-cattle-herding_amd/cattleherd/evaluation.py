@@ -44,6 +44,26 @@ def herding_effectiveness(cattle_xy, drone_xy):
     return np.count_nonzero(wn) / len(c) * 100
 
 
+def failure_truncation(state, e, n, target_alt=0.45, max_alt_error=0.27, collision=0.2, max_formation=8.0,
+                       mission_boundary=15.0):
+    """Conditions 1-4 of CattleAviary._computeTruncated (CattleAviary.py:513-542) on env ``e`` of a state
+    dict (``HerdBatch.get_state``) with ``n`` live drones: altitude loss, a drone pair closer than the
+    collision threshold, a drone isolated from all others, the formation too far from the herd."""
+    pos = np.asarray(state["drone_pos"][e, :n], np.float64)
+    if np.any(np.abs(pos[:, 2] - target_alt) > max_alt_error):
+        return True
+    xy = pos[:, :2]
+    d = np.linalg.norm(xy[:, None, :] - xy[None, :, :], axis=-1)
+    iu = np.triu_indices(n, 1)
+    if np.any(d[iu] < collision):
+        return True
+    np.fill_diagonal(d, np.inf)
+    if np.any(np.all(d > max_formation, axis=1)):
+        return True
+    herd = np.asarray(state["cow_pos"][e], np.float64).mean(axis=0)
+    return bool(np.linalg.norm(xy.mean(axis=0) - herd) > mission_boundary)
+
+
 class Evaluator:
     """utils/evaluation.py:5-94 (``evaluator``): episode-level and per-step lists."""
 
@@ -139,7 +159,9 @@ class EvalTracker:
         drone_poses, cattle_poses = self._poses(state, n, m)
         ep_time = step_counter_before / ctrl_freq
         eff = herding_effectiveness(cattle_poses, drone_poses)
-        if ep_time > episode_len_sec:
+        # _computeTruncated returns at the first failure condition (CattleAviary.py:513-542); the time-out
+        # branch with its trigger (545-548) is reached only when none of them holds
+        if ep_time > episode_len_sec and not failure_truncation(state, self.e, n):
             for _ in range(2):   # evaluation_episode_trigger (BaseAviary.py:1439-1450)
                 self.evaluator.append_episode_data(self.episode_drone_distances, n, ep_time, eff)
         drone_vel = np.array(state["drone_vel"][self.e, :n, :2], np.float64)

@@ -51,6 +51,12 @@ ObservationType = Enum("ObservationType", [("KIN", "kin"), ("RGB", "rgb"), ("COK
 OBS_WIDTH = 86           # 10 + 4*2 + 16*2 + 9*4 (BaseRLAviary.py:262)
 GLOBAL_MAX_NUM_DRONES = 12
 
+# curriculum_learning.py:10-194: (min_num_drones, max_num_drones, episode_length seconds) per level -- the one
+# host copy of the table the adapters read (the kernels carry the full level table, ch_device.h kLevels)
+CURRICULUM = {0: (3, 3, 40), 1: (4, 4, 40), 2: (4, 4, 40), 3: (4, 4, 40), 4: (4, 4, 80), 5: (4, 4, 40),
+              6: (4, 12, 80), 7: (4, 12, 80)}
+DEFAULT_LEVEL = {"ctde": 7, "marl": 0}   # CattleAviary.py:62 / MARLCattleAviary.py:62
+
 
 def ctde_action_space(n):
     return Box(low=-np.ones((n, 4)), high=np.ones((n, 4)), dtype=np.float32)

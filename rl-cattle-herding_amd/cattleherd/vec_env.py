@@ -3,16 +3,20 @@
 Drop-in for ``make_vec_env(CattleAviary, n_envs=..., vec_env_cls=SubprocVecEnv)``
 (simulator/CTDECattleHerder.py:91-97): ``CattleHerdVecEnv(n_envs, num_drones=..., num_cattle=...)``
 returns numpy observations ``(E, 12, 86)``, rewards ``(E,)``, dones ``(E,)`` and per-env infos with
-SB3's ``terminal_observation`` / ``TimeLimit.truncated`` keys, auto-resetting finished envs inside
-the step launch.  ``step_tensors`` is the zero-copy path for on-device policies.
+SB3's ``terminal_observation`` / ``TimeLimit.truncated`` keys and, as the Monitor that ``make_vec_env``
+wraps around every env (CTDECattleHerder.py:91-99) adds, ``episode = {"r", "l", "t"}`` for each episode that
+ends, auto-resetting finished envs inside the step launch.  ``step_tensors`` is the zero-copy path for
+on-device policies.
 
 If stable_baselines3 is importable the class derives from its VecEnv; otherwise it implements the
 same methods (duck-typed).
 """
+import time
+
 import numpy as np
 
 from .env import HerdBatch
-from .spaces import check_supported, ctde_action_space, ctde_observation_space
+from .spaces import CURRICULUM, DEFAULT_LEVEL, check_supported, ctde_action_space, ctde_observation_space
 
 try:  # pragma: no cover
     from stable_baselines3.common.vec_env.base_vec_env import VecEnv as _VecEnvBase
@@ -35,13 +39,13 @@ class CattleHerdVecEnv(_VecEnvBase):
         self._attrs = {"EPISODE_LEN_SEC": self._episode_len(), "CTRL_FREQ": self.batch.cfg.ctrl_freq,
                        "CTRL_TIMESTEP": 1.0 / self.batch.cfg.ctrl_freq, "NUM_DRONES": num_drones,
                        "is_evaluating": False}
+        self._t_start = time.time()
         if _VecEnvBase is not object:  # SB3 bookkeeping
             _VecEnvBase.__init__(self, n_envs, self.observation_space, self.action_space)
 
     def _episode_len(self):
         lvl = self.batch.cfg.curriculum_level
-        lvl = 7 if lvl < 0 else lvl
-        return (40, 40, 40, 40, 80, 40, 80, 80)[lvl]
+        return CURRICULUM[DEFAULT_LEVEL["ctde"] if lvl < 0 else lvl][2]
 
     # ---- VecEnv API --------------------------------------------------------------------------
     def reset(self):
@@ -66,9 +70,14 @@ class CattleHerdVecEnv(_VecEnvBase):
         idx = np.nonzero(dones)[0]
         if len(idx):
             term_obs = self.batch.terminal_obs[idx].cpu().numpy()
+            # Monitor.step: the episode's summed float64 reward and length, kept on the device by the step
+            # kernel (ch_step_io.episode_stats), and the wall time since the Monitor started
+            stats = self.batch.episode_stats[idx].cpu().numpy()
+            t = round(time.time() - self._t_start, 6)
             for k, e in enumerate(idx):
                 infos[e]["terminal_observation"] = term_obs[k]
                 infos[e]["TimeLimit.truncated"] = bool(tr_np[e] and not te_np[e])
+                infos[e]["episode"] = {"r": round(float(stats[k, 0]), 6), "l": int(stats[k, 1]), "t": t}
         return obs_np, rew_np, dones, infos
 
     def step(self, actions):

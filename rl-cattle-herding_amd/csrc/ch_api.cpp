@@ -32,6 +32,7 @@ struct ch_handle {
     // recomputing atan2/asin/atan2; any other writer of the state clears rpy_valid.
     void* rpy = nullptr;
     uint8_t* stale = nullptr;   // device [2][E]: StepParams::stale (Euler cache stale, obs bytes unknown, per env)
+    unsigned long long* obs_tag = nullptr;   // device [E]: StepParams::obs_tag (the buffer holding env e's constant obs bytes)
     void* cattle = nullptr;
     void* phys = nullptr;   // [kPhysComps][E][NC]: last_clipped_action, DYN rpy_rates
     void* envr = nullptr;
@@ -159,7 +160,7 @@ static StepParams<R> params(ch_handle* h) {
     p.k0 = (uint32_t)c.seed; p.k1 = (uint32_t)(c.seed >> 32);
     p.env_off = c.env_id_offset;
     p.cs_cc = cattle_spacing_cc();
-    p.drone = (R*)h->drone; p.rpy = (R*)h->rpy; p.stale = h->stale; p.cattle = (R*)h->cattle; p.envr = (R*)h->envr; p.envi = h->envi;
+    p.drone = (R*)h->drone; p.rpy = (R*)h->rpy; p.stale = h->stale; p.obs_tag = h->obs_tag; p.cattle = (R*)h->cattle; p.envr = (R*)h->envr; p.envi = h->envi;
     p.metrics = h->metrics; p.spawn = h->spawn; p.n_scen = h->n_scen; p.n_cows = h->n_cows;
     p.debug = h->debug;
     p.phase_mask = h->phase_mask;
@@ -226,7 +227,7 @@ const char* ch_last_error(const ch_handle* h) { return h ? h->err.c_str() : g_cr
 
 static void free_all(ch_handle* h) {
     void* ptrs[] = {h->drone, h->rpy, h->cattle, h->phys, h->envr, h->envi, h->metrics, h->spawn, h->pairs,
-                    h->errw, h->mdev, h->stale, h->evald, h->rdn, h->rdv};
+                    h->errw, h->mdev, h->stale, h->obs_tag, h->evald, h->rdn, h->rdv};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (h->mhost) (void)hipHostFree(h->mhost);
@@ -320,6 +321,8 @@ int ch_create(const ch_config* c, int64_t n_envs, int32_t device, ch_handle** ou
     {
         CTRY(hipMalloc(&h->stale, 2 * (size_t)E));
         CTRY(hipMemset(h->stale, 1, 2 * (size_t)E));   // no Euler cache yet; obs bytes unknown
+        CTRY(hipMalloc(&h->obs_tag, sizeof(unsigned long long) * (size_t)E));
+        CTRY(hipMemset(h->obs_tag, 0, sizeof(unsigned long long) * (size_t)E));   // no buffer holds them
     }
     if (c->eval_metrics) {
         CTRY(hipMalloc(&h->evald, sizeof(double) * E * h->NC));
@@ -471,6 +474,9 @@ int ch_reset(ch_handle* h, const uint8_t* mask_dev, float* obs_dev, void* stream
     if (e != hipSuccess) return fail(h, CH_ERR_DEVICE, std::string("ch_reset launch: ") + hipGetErrorString(e));
     if (!mask_dev) h->obs_zero_ptr = obs_dev;                    // every block written in full
     else if (h->obs_zero_ptr != obs_dev) h->obs_zero_ptr = nullptr;   // some blocks of obs_dev unknown
+    // a full reset rebuilds every env: the results a failed hand-off spoiled are gone, so the sticky device
+    // error word is cleared (the failure was reported by every ch_sync / ch_metrics / ch_get_state before it)
+    if (!mask_dev) HIP_TRY(h, hipMemsetAsync(h->errw, 0, sizeof(int), st));
     return CH_OK;
 }
 
@@ -507,6 +513,7 @@ int ch_reset_with(ch_handle* h, const uint8_t* mask_dev, const int32_t* num_dron
         e = launch_reset(p, h->team, st);
     }
     if (e != hipSuccess) return fail(h, CH_ERR_DEVICE, std::string("ch_reset_with launch: ") + hipGetErrorString(e));
+    if (!mask_dev) HIP_TRY(h, hipMemsetAsync(h->errw, 0, sizeof(int), st));   // as ch_reset
     HIP_TRY(h, hipStreamSynchronize(st));   // the host arrays may be reused as soon as this returns
     if (!mask_dev) h->obs_zero_ptr = obs_dev;
     else if (h->obs_zero_ptr != obs_dev) h->obs_zero_ptr = nullptr;
@@ -532,6 +539,7 @@ int ch_step(ch_handle* h, const ch_step_io* io, void* stream) {
         p.actions = io->actions; p.actions_out = io->actions_out; p.obs = io->obs; p.reward = io->reward;
         p.term = io->terminated; p.trunc = io->truncated; p.terminal_obs = io->terminal_obs;
         p.agent_active = io->agent_active; p.reset_happened = io->reset_happened; p.flags = io->flags;
+        p.episode_stats = io->episode_stats;
         p.obs_full = io->obs != h->obs_zero_ptr;
     };
     if (h->rsize == sizeof(double)) {
@@ -545,6 +553,10 @@ int ch_step(ch_handle* h, const ch_step_io* io, void* stream) {
     }
     if (e != hipSuccess) return fail(h, CH_ERR_DEVICE, std::string("ch_step launch: ") + hipGetErrorString(e));
     h->obs_zero_ptr = (h->phase_mask & 8) ? nullptr : io->obs;
+    // The per-env "constant obs bytes unknown" flags (stale row 1) describe one buffer: the one the last step
+    // wrote.  A step into a different buffer than the previous step's leaves the other buffer's blocks behind
+    // (rows a reset episode no longer uses), so the flags are raised again: whatever the next step writes --
+    // this buffer, or the first one from a HIP graph captured earlier -- it writes every block in full.
     return CH_OK;
 }
 
@@ -752,11 +764,14 @@ static int rollout_args(ch_handle* h, const ch_rollout* rb, RolloutArgs& a, cons
     if (!rb) return fail(h, CH_ERR_INVALID, std::string(who) + ": NULL rollout buffer");
     if (h->cfg.mode != CH_MODE_CTDE)
         return fail(h, CH_ERR_UNSUPPORTED, std::string(who) + ": the SB3 rollout buffer is for CTDE handles");
-    if (rb->n_steps < 1 || rb->act_dim < 1 || rb->act_dim > 256)
-        return fail(h, CH_ERR_INVALID, std::string(who) + ": n_steps >= 1 and 1 <= act_dim <= 256 required");
+    // the env reads a (num_drones, 4) action per env (ch_step: float4 [e * num_drones + k]), so the policy must
+    // produce at least num_drones * 4 outputs (SB3: Box((NUM_DRONES, 4)) or the reference's (12, 4))
+    if (rb->n_steps < 1 || rb->act_dim < h->NC * 4 || rb->act_dim > 256)
+        return fail(h, CH_ERR_INVALID, std::string(who) + ": n_steps >= 1 and num_drones * 4 = " +
+                                           std::to_string(h->NC * 4) + " <= act_dim <= 256 required");
     std::memset(&a, 0, sizeof(a));
     a.T = rb->n_steps; a.rows = h->E; a.obs_dim = h->rows * 86; a.act_dim = rb->act_dim;
-    a.env_act_dim = std::min(rb->act_dim, h->NC * 4);
+    a.env_act_dim = h->NC * 4;
     a.obs = rb->obs; a.actions = rb->actions; a.rewards = rb->rewards; a.episode_starts = rb->episode_starts;
     a.values = rb->values; a.log_probs = rb->log_probs; a.advantages = rb->advantages; a.returns = rb->returns;
     a.last_episode_starts = rb->last_episode_starts;

@@ -28,11 +28,14 @@ struct StepParams {
     double cs_cc;   // CattleSpacingRewardFunction continuation constant (host-evaluated)
     R* drone;       // [22][E][NC]
     R* rpy;         // v2: [3][E][NC] Euler angles of the stored quaternion (valid unless stale[e])
-    // device control words of the handle, read by the v2 step at its start (so a captured HIP graph
-    // sees state changes made after capture): [0] the Euler cache is stale, [1] the constant-zero
-    // observation bytes are unknown, [2] v2 workgroups finished (the last one clears [0] and [1])
-    uint8_t* stale; // [2][E] per env: row 0 the Euler cache is stale, row 1 the obs block's constant bytes are
-                    // unknown; set by every other writer (v1, ch_reset, ch_set_state, invalidate), cleared by the v2 step
+    // per-env device flags, read by the v2 step with its env's state (so a captured HIP graph sees state changes
+    // made after capture) and cleared at its write-back: row 0 the Euler cache is stale, row 1 the obs block's
+    // constant bytes are unknown; set by every other writer (v1, ch_reset, ch_set_state, invalidate)
+    uint8_t* stale; // [2][E]
+    // [E] the address of the obs buffer whose block of env e holds the env's constant-zero bytes (0: none): set
+    // by every full-block writer (v1 step / reset, v2 step) to the buffer it wrote.  A v2 step into any other
+    // buffer -- e.g. a graph captured on buffer A replayed after steps into B -- writes the env's block in full.
+    unsigned long long* obs_tag;
     R* cattle;      // [4][E][M]
     R* envr;        // [2][E]
     int* envi;      // [10][E]
@@ -48,6 +51,7 @@ struct StepParams {
     float* terminal_obs;
     uint8_t* agent_active;
     uint8_t* reset_happened;
+    double* episode_stats;    // optional [E][2]: return and length of the episode that ended in this step
     const uint8_t* reset_mask;
     uint32_t flags;
     double* debug;  // optional [E][NC][16] per-drone intermediates (diagnostics only)

@@ -489,6 +489,7 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
             mt[kMetricCurReturn] += ret;
             mt[kMetricCurLen] += 1;
             if (done) {
+                if (p.episode_stats) { p.episode_stats[2 * e] = mt[kMetricCurReturn]; p.episode_stats[2 * e + 1] = mt[kMetricCurLen]; }
                 mt[CH_METRIC_EPISODES] += 1;
                 mt[CH_METRIC_RETURN_SUM] += mt[kMetricCurReturn];
                 mt[CH_METRIC_LENGTH_SUM] += mt[kMetricCurLen];
@@ -547,6 +548,8 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
     if (write && !(p.phase_mask & 8)) write_obs(p.obs + (long long)e * p.rows * 86, p.rows, S, t, m_obs, cat_off);
     if (write && t == 0) {
         if (p.stale) p.stale[e] = 1;   // this kernel does not keep the v2 step's Euler-angle cache
+        // every block this kernel writes is written in full
+        if (p.obs_tag) p.obs_tag[e] = (p.phase_mask & 8) ? 0ull : (unsigned long long)(uintptr_t)p.obs;
         p.envi[0 * E + e] = n; p.envi[1 * E + e] = sc; p.envi[2 * E + e] = scA; p.envi[3 * E + e] = has_prev;
         p.envi[4 * E + e] = level; p.envi[5 * E + e] = tally; p.envi[6 * E + e] = spawn; p.envi[7 * E + e] = active;
         p.envi[8 * E + e] = episode;

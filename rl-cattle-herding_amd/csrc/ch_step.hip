@@ -706,7 +706,8 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             const int e = e0 + ct;
 #pragma unroll
             for (int r = 0; r < 9; ++r) ei0[r] = p.envi[r * E + e];
-            ei0[9] = p.stale[E + e];
+            // constant obs bytes unknown: flagged, or this buffer is not the one that holds them
+            ei0[9] = p.stale[E + e] | (p.obs_tag[e] != (unsigned long long)(uintptr_t)p.obs ? 1 : 0);
             er0[0] = p.envr[e]; er0[1] = p.envr[E + e];
 #pragma unroll
             for (int r = 0; r < kMetricRows; ++r) met0[r] = p.metrics[r * E + e];
@@ -1322,6 +1323,11 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             o[kMetricCurReturn] += ret;
             o[kMetricCurLen] += 1;
             if (done) {
+                // SB3 Monitor's episode record (its reward sum and length) for the env that ends here
+                if (p.episode_stats) {
+                    CH_ST(&p.episode_stats[2 * (long long)e], o[kMetricCurReturn]);
+                    CH_ST(&p.episode_stats[2 * (long long)e + 1], o[kMetricCurLen]);
+                }
                 o[CH_METRIC_EPISODES] += 1;
                 o[CH_METRIC_RETURN_SUM] += o[kMetricCurReturn];
                 o[CH_METRIC_LENGTH_SUM] += o[kMetricCurLen];
@@ -1351,6 +1357,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             // this step wrote the env's Euler cache and, unless obs were masked off, its whole obs block
             p.stale[e] = 0;
             if (wobs) p.stale[E + e] = 0;
+            p.obs_tag[e] = wobs ? (unsigned long long)(uintptr_t)p.obs : 0ull;
         }
     } else {
         // ============ cow waves ================================================================

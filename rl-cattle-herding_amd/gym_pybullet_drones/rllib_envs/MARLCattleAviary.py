@@ -9,11 +9,8 @@ rllib_envs/BaseAviary.py:425-431 (ch_config.marl_wrapper = 0).  RLlib drivers us
 import numpy as np
 
 from cattleherd.env import HerdBatch
-from cattleherd.spaces import (ActionType, DroneModel, ObservationType, Physics, agent_action_space,
+from cattleherd.spaces import (CURRICULUM, ActionType, DroneModel, ObservationType, Physics, agent_action_space,
                                agent_observation_space, check_supported)
-
-_LEVEL = {0: (3, 3, 40), 1: (4, 4, 40), 2: (4, 4, 40), 3: (4, 4, 40), 4: (4, 4, 80), 5: (4, 4, 40), 6: (4, 12, 80),
-          7: (4, 12, 80)}
 
 
 class MARLCattleAviary:
@@ -26,7 +23,7 @@ class MARLCattleAviary:
         check_supported(drone_model, physics, obs, act)
         if pyb_freq % ctrl_freq != 0:
             raise ValueError("[ERROR] in BaseAviary.__init__(), pyb_freq is not divisible by env_freq.")
-        lo, hi, ep = _LEVEL[curriculum_level]
+        lo, hi, ep = CURRICULUM[curriculum_level]
         self.MIN_NUM_DRONES = min(lo, num_drones) if min_drones is None else int(min_drones)
         self.MAX_NUM_DRONES = min(hi, num_drones) if max_drones is None else int(max_drones)
         self.CTRL_FREQ, self.PYB_FREQ = ctrl_freq, pyb_freq

@@ -13,7 +13,7 @@ import numpy as np
 from cattleherd.evaluation import EvalTracker, Evaluator
 from cattleherd.seeded import ReferenceResetRNG
 from cattleherd.env import HerdBatch
-from cattleherd.spaces import (ActionType, DroneModel, ObservationType, Physics, check_supported,
+from cattleherd.spaces import (CURRICULUM, ActionType, DroneModel, ObservationType, Physics, check_supported,
                                ctde_action_space, ctde_observation_space)
 
 try:  # pragma: no cover
@@ -21,10 +21,6 @@ try:  # pragma: no cover
     _EnvBase = _gym.Env
 except Exception:  # noqa: BLE001
     _EnvBase = object
-
-# curriculum_learning.py: (min_drones, max_drones, episode_length) per level
-_LEVEL = {0: (3, 3, 40), 1: (4, 4, 40), 2: (4, 4, 40), 3: (4, 4, 40), 4: (4, 4, 80), 5: (4, 4, 40), 6: (4, 12, 80),
-          7: (4, 12, 80)}
 
 
 class CattleAviary(_EnvBase):
@@ -40,7 +36,7 @@ class CattleAviary(_EnvBase):
         check_supported(drone_model, physics, obs, act)
         if pyb_freq % ctrl_freq != 0:
             raise ValueError("[ERROR] in BaseAviary.__init__(), pyb_freq is not divisible by env_freq.")
-        lo, hi, ep = _LEVEL[curriculum_level]
+        lo, hi, ep = CURRICULUM[curriculum_level]
         # the reference draws NUM_DRONES in the curriculum's [min, max] but sizes its controllers by
         # num_drones (BaseRLAviary.py:80); clip the range so every draw is runnable
         self.MIN_NUM_DRONES = min(lo, num_drones) if min_drones is None else int(min_drones)

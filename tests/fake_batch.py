@@ -44,6 +44,9 @@ class FakeBatch:
         self.truncated = torch.zeros((E, K), dtype=torch.uint8)
         self.agent_active = torch.zeros((E, num_drones), dtype=torch.uint8)
         self.actions = torch.zeros((E, num_drones, 4))
+        self.reset_happened = torch.zeros(E, dtype=torch.uint8)
+        self.episode_stats = torch.zeros((E, 2), dtype=torch.float64)   # as ch_step_io.episode_stats
+        self._ret, self._len = np.zeros(E), np.zeros(E)
         self.step_index = 0
 
     def reset(self, mask=None):
@@ -62,6 +65,12 @@ class FakeBatch:
             self.terminated[e] = torch.from_numpy(te)
             self.truncated[e] = torch.from_numpy(tr)
             self.agent_active[e] = torch.from_numpy(env.get_state()["active"][:self.num_drones])
+            self._ret[e] += float(np.sum(r[np.isfinite(r)])) if self.mode else float(r[0])
+            self._len[e] += 1
+            if done:
+                self.episode_stats[e, 0], self.episode_stats[e, 1] = self._ret[e], self._len[e]
+                self._ret[e], self._len[e] = 0.0, 0.0
+            self.reset_happened[e] = int(done and autoreset)
             if done and autoreset:
                 self.terminal_obs[e] = torch.from_numpy(tobs)
         self.step_index += 1
@@ -78,7 +87,10 @@ class FakeBatch:
 
     def env_ints(self):
         s = stack([env.get_state() for env in self.envs])
-        return {k: np.asarray(s[k], np.int64) for k in ("n", "step_counter", "step_counter_A")}
+        out = {k: np.asarray(s[k], np.int64) for k in ("n", "step_counter", "step_counter_A")}
+        act = np.asarray(s["active"], np.int64)[:, :self.num_drones]
+        out["active_mask"] = (act << np.arange(self.num_drones)[None, :]).sum(1)
+        return out
 
     def eval_distances(self):
         return np.stack([env.get_state()["eval_dist"][:self.num_drones] for env in self.envs])

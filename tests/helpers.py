@@ -29,6 +29,23 @@ def stack(states):
     return {k: np.stack([np.asarray(s[k]) for s in states]) for k in states[0]}
 
 
+def oracle_view(g, e, nmax):
+    """Env ``e`` of a HerdBatch.get_state() dict as an oracle Env.set_state() dict: per-drone arrays padded to
+    the oracle's ``nmax`` drones (identity quaternions, inactive) -- the device state before a step."""
+    out = {}
+    for k, v in g.items():
+        x = np.asarray(v[e])
+        if k in ("drone_pos", "drone_quat", "drone_vel", "drone_angv", "pid_last_rpy", "pid_int_pos", "pid_int_rpy",
+                 "last_rpm", "rpy_rates", "active"):
+            pad = np.zeros((nmax,) + x.shape[1:], x.dtype)
+            pad[:x.shape[0]] = x
+            if k == "drone_quat":
+                pad[x.shape[0]:, 3] = 1
+            x = pad
+        out[k] = x
+    return out
+
+
 def close(a, b, rtol, atol):
     a = np.asarray(a, np.float64)
     b = np.asarray(b, np.float64)

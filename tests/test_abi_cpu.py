@@ -29,7 +29,7 @@ def test_default_config_and_struct_layout():
     c = _lib.default_config(_lib.CH_MODE_CTDE, 12, 16)
     assert c.abi_version == _lib.ABI_VERSION and c.ctrl_freq == 60 and c.pyb_freq == 240
     assert c.compat == 1 and c.damping == 0.04 and c.min_drones == -1
-    assert ctypes.sizeof(_lib.ChStepIO) == 9 * 8 + 8
+    assert ctypes.sizeof(_lib.ChStepIO) == 9 * 8 + 8 + 8
 
 
 def test_builtin_spawn_table_is_the_reference_yaml(spawn16):

@@ -53,3 +53,32 @@ def test_cattle_aviary_evaluation_data_matches_reference(patched, tmp_path):
     path = tmp_path / "evaluation_data.pkl"
     env.evaluation_save(str(path))
     assert path.stat().st_size > 0
+
+
+def _tracker_state(drone_xyz, cow_xy):
+    drone = np.asarray(drone_xyz, np.float64)[None]
+    cows = np.asarray(cow_xy, np.float64)[None]
+    return {"drone_pos": drone, "drone_vel": np.zeros_like(drone), "cow_pos": cows, "cow_vel": np.zeros_like(cows)}
+
+
+@pytest.mark.parametrize("case,drones,want", [
+    ("clean time-out", [[0, 0, 0.45], [1.75, 0, 0.45], [3.5, 0, 0.45]], 2),
+    ("altitude loss", [[0, 0, 0.80], [1.75, 0, 0.45], [3.5, 0, 0.45]], 0),
+    ("collision", [[0, 0, 0.45], [0.1, 0, 0.45], [3.5, 0, 0.45]], 0),
+    ("isolated drone", [[0, 0, 0.45], [1.75, 0, 0.45], [30, 0, 0.45]], 0),
+    ("mission boundary", [[40, 0, 0.45], [41.75, 0, 0.45], [43.5, 0, 0.45]], 0),
+])
+def test_time_out_trigger_only_when_no_failure_truncation(case, drones, want):
+    """_computeTruncated returns at its first failure condition (CattleAviary.py:513-542), so the time-out
+    branch and its evaluation_episode_trigger (545-548) run only when none holds: a failure on the
+    time-out step logs no episode entry."""
+    from cattleherd.evaluation import EvalTracker, Evaluator, failure_truncation
+    cows = [[2.0, 8.0], [3.0, 9.0], [1.0, 9.5], [2.5, 10.0]]
+    s = _tracker_state(drones, cows)
+    assert failure_truncation(s, 0, 3) == (want == 0), case
+    ev = Evaluator()
+    tr = EvalTracker(ev)
+    tr.on_reset(s, 3)
+    tr.after_step(s, np.zeros(3), 3, 4, step_counter_before=4804, ctrl_freq=60, episode_len_sec=80)
+    assert len(ev.total_time_taken) == want, case
+    assert len(ev.curr_time) == 1   # the step itself is logged either way (update_evaluation_metrics)

@@ -120,3 +120,35 @@ def test_vec_env_random_rollout_infos_on_gpu():
     assert saw > 0
     assert venv.get_attr("EPISODE_LEN_SEC") == [80] * 64 and venv.env_is_wrapped(object) == [False] * 64
     venv.close()
+
+
+@pytest.mark.parametrize("n,m,compat", [(4, 16, True), (2, 8, False)])
+def test_vec_env_monitor_episode_info_on_gpu(n, m, compat):
+    """SB3 Monitor's info["episode"] (make_vec_env wraps every env in one, CTDECattleHerder.py:91-99) from the
+    batched VecEnv: for every env that ends an episode, "l" is the number of steps since its last reset and "r"
+    the sum of the rewards it returned (the device sums the float64 rewards, the host here the float32 ones it
+    received: rtol 1e-6), "t" the seconds since the env started, non-decreasing."""
+    from cattleherd.vec_env import CattleHerdVecEnv
+    E = 256
+    venv = CattleHerdVecEnv(E, num_drones=n, num_cattle=m, compat=compat)
+    venv.reset()
+    rng = np.random.default_rng(1)
+    ret, length = np.zeros(E), np.zeros(E, np.int64)
+    seen, last_t = 0, 0.0
+    for _ in range(400):
+        obs, rew, dones, infos = venv.step(rng.uniform(-1, 1, (E, n, 4)).astype(np.float32))
+        ret += rew.astype(np.float64)
+        length += 1
+        for e in range(E):
+            if dones[e]:
+                ep = infos[e]["episode"]
+                assert set(ep) == {"r", "l", "t"} and ep["l"] == length[e], (e, ep, length[e])
+                assert np.isclose(ep["r"], ret[e], rtol=1e-6, atol=1e-5), (e, ep["r"], ret[e])
+                assert ep["t"] >= last_t
+                last_t = ep["t"]
+                ret[e], length[e] = 0.0, 0
+                seen += 1
+            else:
+                assert "episode" not in infos[e]
+    assert seen > 50, seen
+    venv.close()

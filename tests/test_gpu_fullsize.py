@@ -6,36 +6,25 @@ rtol 1e-6 / atol 1e-7 (the f32 output cast), reward rtol 1e-6, state 1e-9, flags
 import numpy as np
 import pytest
 
-from helpers import close, stack
+from helpers import close, oracle_view as _oracle_view
 
 pytestmark = pytest.mark.gpu
 
 
-def _oracle_view(g, e, nmax):
-    out = {}
-    for k, v in g.items():
-        x = np.asarray(v[e])
-        if k in ("drone_pos", "drone_quat", "drone_vel", "drone_angv", "pid_last_rpy", "pid_int_pos", "pid_int_rpy",
-                 "last_rpm", "rpy_rates", "active"):
-            pad = np.zeros((nmax,) + x.shape[1:], x.dtype)
-            pad[:x.shape[0]] = x
-            if k == "drone_quat":
-                pad[x.shape[0]:, 3] = 1
-            x = pad
-        out[k] = x
-    return out
-
-
-def test_configs3_full_size_spot_parity():
+@pytest.mark.parametrize("n,m,compat", [(4, 16, True), (2, 8, True), (2, 8, False)],
+                         ids=["configs3", "configs2_compat", "configs2_training"])
+def test_full_size_spot_parity(n, m, compat):
     """4096 envs, 300 device-drawn random steps with auto-reset, then one step with host actions; 64 envs
     (a fixed random sample, incl. the first and last workgroup) re-run that step on the oracle from the
-    device state before it."""
+    device state before it.  configs[3]'s (4, 16) and configs[2]'s (2, 8) -- the latter with the reference's
+    quirks (compat: the 2-drone CTDE reward is NaN on every step, CattleAviary.py:234-246) and NaN-safe as its
+    PPO training leg runs it (compat = 0: finite rewards)."""
     import torch
     import oracle as O
     from cattleherd._lib import spawn_table
     from cattleherd.env import HerdBatch
-    E, n, m = 4096, 4, 16
-    b = HerdBatch(E, n, m)
+    E = 4096
+    b = HerdBatch(E, n, m, compat=compat)
     b.reset()
     for _ in range(300):
         b.step(random_actions=True, autoreset=True)
@@ -53,8 +42,12 @@ def test_configs3_full_size_spot_parity():
     pick = np.unique(np.concatenate([pick, resets[:24]]))
     after = b.get_state()
     table = spawn_table(m)
+    if compat and n == 2:
+        assert np.isnan(rew).all()
+    else:
+        assert np.isfinite(rew).all()
     for e in pick:
-        env = O.Env(0, n, m, table, env_id=int(e))
+        env = O.Env(0, n, m, table, env_id=int(e), compat=compat)
         env.set_state(_oracle_view(g, e, O.NMAX))
         env.st.episode = int(g["episode"][e])   # (set_state leaves the reset counter to the env's own resets)
         o, r, t1, t2, done, _ = env.step(acts[e], autoreset=True)

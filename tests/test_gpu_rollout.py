@@ -28,17 +28,22 @@ def _gae_numpy(rewards, values, episode_starts, last_values, dones, gamma, lam):
     return adv, adv + values
 
 
-def test_rollout_buffer_matches_sb3_semantics():
+@pytest.mark.parametrize("E,n,m,compat,level", [(512, 4, 16, True, 2), (4096, 2, 8, False, 7)],
+                         ids=["4x16_level2", "configs2_training"])
+def test_rollout_buffer_matches_sb3_semantics(E, n, m, compat, level):
+    """configs[2]'s training leg is the second case: 4096 envs x (2 drones, 8 cattle), NaN-safe rewards
+    (compat = 0; with the reference's quirk every 2-drone CTDE reward is NaN, CattleAviary.py:234-246), the
+    driver's default curriculum level 7 (80 s episodes, CTDECattleHerder.py:91-127)."""
     import torch
     from cattleherd.env import HerdBatch
     from cattleherd.policy import DevicePolicy
     from cattleherd.rollout import DeviceRolloutBuffer
-    E, T, n, m = 512, 40, 4, 16
+    T = 40
     A = 4 * n                        # the CTDE action space is Box((NUM_DRONES, 4)), flattened by SB3
     sc = 4800 - 30 + (np.arange(E) % 60)   # half the envs reach the 80 s time limit inside the rollout
 
     def make():
-        bb = HerdBatch(E, n, m, mode="ctde", curriculum_level=2)
+        bb = HerdBatch(E, n, m, mode="ctde", curriculum_level=level, compat=compat)
         bb.reset()
         bb.set_state({"step_counter": sc})
         return bb
@@ -76,6 +81,8 @@ def test_rollout_buffer_matches_sb3_semantics():
         rr[tr & ~te] += 0.99 * tv[tr & ~te]
         rew.append(rr.cpu().numpy()); dn.append((te | tr).cpu().numpy()); tl.append((tr & ~te).cpu().numpy())
     rew, dn = np.array(rew), np.array(dn)
+    if not compat:
+        assert np.isfinite(rb.rewards.cpu().numpy()).all()
     assert np.allclose(rb.rewards.cpu().numpy(), rew, rtol=1e-5, atol=1e-5)   # V(terminal) MFMA vs torch
     assert np.array_equal(es[1:], dn[:-1].astype(np.float32))
     assert dn.any() and np.array(tl).any()

@@ -67,6 +67,60 @@ def test_graph_replay_equals_eager_across_state_changes(mode, n, m, E):
         h.close()
 
 
+def test_graph_replay_after_steps_into_another_obs_buffer():
+    """Steps into a second observation buffer between replays of a graph captured on the first: envs that
+    reset there (NUM_DRONES redrawn in [2, 6]) leave rows in the graph's buffer that the new episode no
+    longer uses.  The buffer switch raises the per-env "constant bytes unknown" flags, so the next replay
+    rewrites every block and the graph's buffer equals an eager twin stepped into one buffer only."""
+    import torch
+    E, n, m, K = 1024, 6, 16, 5
+    eager, gr = _pair("ctde", n, m, E, min_drones=2, max_drones=n)
+    for h in (eager, gr):
+        h.reset()
+    graph = gr.capture_rollout(K, terminal_obs=False)
+    other = torch.full_like(gr.obs, 3.0)
+    nres = 0
+    for rnd in range(8):
+        graph.replay()
+        for _ in range(K):
+            eager.step(random_actions=True, autoreset=True, terminal_obs=False)
+        torch.cuda.synchronize()
+        assert _same(_outs(eager), _outs(gr)), rnd
+        for _ in range(30):   # eager twin: the same steps into its own buffer
+            gr.step(random_actions=True, autoreset=True, terminal_obs=False, obs_out=other)
+            eager.step(random_actions=True, autoreset=True, terminal_obs=False)
+            nres += int(gr.reset_happened.sum())
+        torch.cuda.synchronize()
+        assert torch.equal(other, eager.obs), rnd
+    assert nres > 50, nres
+    for h in (eager, gr):
+        h.close()
+
+
+def test_full_reset_clears_the_device_error_word():
+    """After a failed hand-off the handle reports CH_ERR_DEVICE until a full reset() rebuilds every env;
+    then it steps and reports normally again (a masked reset does not clear it)."""
+    import torch
+    from cattleherd import _lib
+    from cattleherd.env import HerdBatch
+    b = HerdBatch(256, 4, 16, mode="ctde")
+    b.reset()
+    assert _lib.lib().ch__set_phase_mask(b.handle, ctypes.c_int32(64)) == 0
+    b.step(random_actions=True)
+    with pytest.raises(_lib.ChError):
+        b.sync()
+    assert _lib.lib().ch__set_phase_mask(b.handle, ctypes.c_int32(0)) == 0
+    b.reset(mask=torch.ones(256, dtype=torch.uint8, device=b.device))
+    with pytest.raises(_lib.ChError):
+        b.sync()
+    b.reset()
+    b.sync()
+    b.step(random_actions=True)
+    b.sync()
+    b.get_state()
+    b.close()
+
+
 def test_device_metrics_equal_host_sum_of_rows():
     """ch_metrics (device reduction + pinned copy) and ch_metrics_device agree with each other and
     with the metric rows summed on the host; reset_after zeroes the summed rows only."""
