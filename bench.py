@@ -146,29 +146,36 @@ def policy_rollout(b, n, steps, warmup):
            "roofline": {"bound": "mfma", "achieved": tf, "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
                         "frac": tf / MFMA_F32_PEAK_TFLOPS, "flops_per_forward": flops}}
     out["ppo_rollout"] = ppo_rollout(b, d)
+    # the packed actor-critic reads the observation once, but each workgroup still streams both heads' weights
+    # for its 16 rows, which is what the forward waits on: measured slower, reported beside it
+    out["ppo_rollout_fused_nets"] = ppo_rollout(b, d, fused=True)
     return out
 
 
-def ppo_rollout(b, d, T=32):
-    """SB3 collect_rollouts on the device (cattleherd.rollout): per step actor + critic forward,
-    Gaussian sample / log-prob / buffer store, env step with auto-reset and terminal obs, V(terminal obs)
-    bootstrap; then GAE.  env-steps/s of one whole T-step collection (after one untimed collection)."""
+def ppo_rollout(b, d, T=32, fused=False):
+    """SB3 collect_rollouts on the device (cattleherd.rollout): per step the actor and critic forwards (fused=True:
+    one launch of the two heads packed as one net, DevicePolicy.sb3_actor_critic, bit-identical to the separate
+    nets), Gaussian sample / log-prob / buffer store (with the previous step's reward bootstrap), env step with
+    auto-reset and terminal obs, V(terminal obs); then GAE.  env-steps/s of one whole T-step collection (after
+    one untimed collection)."""
     import torch
     from cattleherd.policy import DevicePolicy
     from cattleherd.rollout import DeviceRolloutBuffer
     sd = {k.replace("__", "."): torch.tensor(d[k]) for k in d.files if "__" in k}
     actor = DevicePolicy.sb3_actor(sd, clip=False)
     critic = DevicePolicy.sb3_critic(sd)
+    nets = (DevicePolicy.sb3_actor_critic(sd), None) if fused else (actor, critic)
     log_std = torch.full((actor.dims[-1],), -1.0, device=b.device)   # log_std_init (CTDECattleHerder.py:122)
     rb = DeviceRolloutBuffer(b, T, act_dim=actor.dims[-1])
     b.reset()
-    rb.collect(actor, critic, log_std, seed=1)
+    rb.collect(*nets, log_std, seed=1)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    rb.collect(actor, critic, log_std, seed=2)
+    rb.collect(*nets, log_std, seed=2)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     out = {"env_steps_per_s": b.n_envs * T / dt, "ms_per_step": dt / T * 1000.0, "n_steps": T,
+           "policy": "actor + critic fused (one forward per step)" if fused else "actor and critic separately",
            "buffer_GB": sum(t.numel() * 4 for t in (rb.obs, rb.actions)) / 1e9}
     del rb
     return out

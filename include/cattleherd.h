@@ -277,13 +277,18 @@ int ch_rollout_gae(ch_handle* h, const ch_rollout* rb, const float* last_value, 
  * for t < n_steps, on `stream`: actor and critic forwards on step->obs (ch_policy_forward), ch_rollout_store,
  * ch_step with auto-reset and terminal observations, the critic on the terminal observations of the envs that
  * reset (ch_mlp_forward_masked; skipped with bootstrap_truncated = 0), ch_rollout_post; then the critic on the
- * last observations and ch_rollout_gae.  Device scratch (caller-owned): */
+ * last observations and ch_rollout_gae.
+ * critic == NULL: `actor` is a fused actor-critic whose output is act_dim + 1 wide (the action mean, then the
+ * value; e.g. SB3's two MLPs packed as one: layer 1 stacked, layers 2-3 block-diagonal, which leaves every output
+ * bit-identical to the separate nets): one forward per step reads the observation once.  `mean` and
+ * `terminal_value` are then [rows][act_dim + 1] (both heads); `value` is not used.
+ * Device scratch (caller-owned): */
 typedef struct ch_rollout_io {
     const ch_step_io* step;    /* the env's step buffers; obs, reward, terminated, truncated, terminal_obs and
                                   reset_happened are required (actions are env_actions below) */
-    float* mean;               /* [rows][act_dim] */
+    float* mean;               /* [rows][act_dim] ([rows][act_dim + 1] with a fused actor-critic) */
     float* value;              /* [rows] */
-    float* terminal_value;     /* [rows] */
+    float* terminal_value;     /* [rows] ([rows][act_dim + 1] with a fused actor-critic) */
     float* env_actions;        /* [rows][num_drones][4] */
 } ch_rollout_io;
 int ch_rollout_collect(ch_handle* h, const ch_rollout* rb, const ch_rollout_io* io, const ch_mlp* actor,

@@ -84,6 +84,40 @@ class DevicePolicy:
                   (sd["value_net.weight"], sd["value_net.bias"])]
         return cls(layers, "tanh", None, device)
 
+    @classmethod
+    def sb3_actor_critic(cls, state_dict, device=None):
+        """SB3 ActorCriticPolicy's two MLPs as one net with both heads (output [mean (A), value]): layer 1
+        stacked (policy_net.0 over value_net.0: the observation is read once), layers 2 and 3 block-diagonal.
+        Every output is the same f32 MFMA fma chain as the separate nets' (the other head's blocks add +-0),
+        so the mean and the value are bit-identical to sb3_actor(clip=False) and sb3_critic."""
+        import torch
+        sd = {k: torch.as_tensor(v, dtype=torch.float32) for k, v in state_dict.items()}
+        aw = [sd["mlp_extractor.policy_net.0.weight"], sd["mlp_extractor.policy_net.2.weight"], sd["action_net.weight"]]
+        ab = [sd["mlp_extractor.policy_net.0.bias"], sd["mlp_extractor.policy_net.2.bias"], sd["action_net.bias"]]
+        cw = [sd["mlp_extractor.value_net.0.weight"], sd["mlp_extractor.value_net.2.weight"], sd["value_net.weight"]]
+        cb = [sd["mlp_extractor.value_net.0.bias"], sd["mlp_extractor.value_net.2.bias"], sd["value_net.bias"]]
+        layers = [(torch.cat([aw[0], cw[0]], 0), torch.cat([ab[0], cb[0]], 0))]
+        for i in (1, 2):
+            layers.append((torch.block_diag(aw[i], cw[i]), torch.cat([ab[i], cb[i]], 0)))
+        net = cls(layers, "tanh", None, device)
+        net.heads = (int(aw[2].shape[0]), int(cw[2].shape[0]))
+        return net
+
+    @classmethod
+    def fuse(cls, actor, critic):
+        """The same packing from two DevicePolicy MLPs of equal depth (e.g. random-initialised ones)."""
+        import torch
+        if len(actor.weights) != len(critic.weights) or actor.hidden_act != critic.hidden_act:
+            raise ValueError("actor and critic must have the same depth and activation")
+        layers = []
+        for i, (aw, ab, cw, cb) in enumerate(zip(actor.weights, actor.biases, critic.weights, critic.biases)):
+            w = torch.cat([aw, cw], 0) if i == 0 else torch.block_diag(aw, cw)
+            z = lambda w_, b_: b_ if b_ is not None else torch.zeros(w_.shape[0], device=w_.device)  # noqa: E731
+            layers.append((w, torch.cat([z(aw, ab), z(cw, cb)], 0)))
+        net = cls(layers, actor.hidden_act, None, actor.device)
+        net.heads = (actor.dims[-1], critic.dims[-1])
+        return net
+
     @staticmethod
     def random_layers(dims, seed=0):
         """nn.Linear default initialisation (uniform +-1/sqrt(fan_in)) for the given widths."""

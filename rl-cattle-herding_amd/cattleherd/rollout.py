@@ -60,6 +60,7 @@ class DeviceRolloutBuffer:
         self.env_actions = torch.zeros((E, batch.num_drones, 4), **z)
         self.value = torch.zeros((E, 1), **z)
         self.mean = torch.zeros((E, self.act_dim), **z)
+        self.mean_fused = None   # [E, act_dim + 1]: a fused actor-critic's output (collect(critic=None))
         self.terminal_value = torch.zeros((E, 1), **z)
         rb = ChRollout()
         rb.n_steps, rb.act_dim = self.T, self.act_dim
@@ -73,20 +74,31 @@ class DeviceRolloutBuffer:
         """SB3 collect_rollouts for n_steps steps of every env, on the device, in one native call
         (ch_rollout_collect: the loop of collect_steps below runs in C++).  ``actor``: DevicePolicy of the
         action mean (no clip: SB3's action_net output), ``critic``: DevicePolicy of V, ``log_std``:
-        float32 [act_dim] device tensor."""
+        float32 [act_dim] device tensor.  ``critic=None``: ``actor`` is a fused actor-critic
+        (DevicePolicy.sb3_actor_critic / fuse, output [mean, value]) and one forward per step serves both."""
         b, lib = self.batch, self._lib
         torch = b.torch
         log_std = log_std.to(device=b.device, dtype=torch.float32).contiguous()
         io = ChRolloutIO()
         io.step = ctypes.pointer(b._io)
-        io.mean, io.value = self.mean.data_ptr(), self.value.data_ptr()
-        io.terminal_value, io.env_actions = self.terminal_value.data_ptr(), self.env_actions.data_ptr()
+        if critic is None:
+            if actor.dims[-1] != self.act_dim + 1:
+                raise ValueError(f"a fused actor-critic must output act_dim + 1 = {self.act_dim + 1} columns")
+            if self.mean_fused is None:
+                self.mean_fused = torch.zeros((b.n_envs, self.act_dim + 1), dtype=torch.float32, device=b.device)
+                self.terminal_fused = torch.zeros((b.n_envs, self.act_dim + 1), dtype=torch.float32, device=b.device)
+            io.mean, io.terminal_value = self.mean_fused.data_ptr(), self.terminal_fused.data_ptr()
+        else:
+            io.mean, io.value = self.mean.data_ptr(), self.value.data_ptr()
+            io.terminal_value = self.terminal_value.data_ptr()
+        io.env_actions = self.env_actions.data_ptr()
         keep = b._io.terminal_obs
         b._io.terminal_obs = b.terminal_obs.data_ptr()
         try:
             L.check(lib.ch_rollout_collect(b.handle, ctypes.byref(self._rb), ctypes.byref(io), ctypes.byref(actor._net),
-                                           ctypes.byref(critic._net), log_std.data_ptr(), int(seed), self.gamma,
-                                           self.gae_lambda, int(bool(bootstrap_truncated)), b._stream()), b.handle)
+                                           None if critic is None else ctypes.byref(critic._net), log_std.data_ptr(),
+                                           int(seed), self.gamma, self.gae_lambda, int(bool(bootstrap_truncated)),
+                                           b._stream()), b.handle)
         finally:
             b._io.terminal_obs = keep
         return self

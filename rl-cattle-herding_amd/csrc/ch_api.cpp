@@ -772,6 +772,7 @@ static int rollout_args(ch_handle* h, const ch_rollout* rb, RolloutArgs& a, cons
     std::memset(&a, 0, sizeof(a));
     a.T = rb->n_steps; a.rows = h->E; a.obs_dim = h->rows * 86; a.act_dim = rb->act_dim;
     a.env_act_dim = h->NC * 4;
+    a.mean_ld = rb->act_dim; a.value_ld = 1; a.tv_ld = 1; a.post_prev = 0;
     a.obs = rb->obs; a.actions = rb->actions; a.rewards = rb->rewards; a.episode_starts = rb->episode_starts;
     a.values = rb->values; a.log_probs = rb->log_probs; a.advantages = rb->advantages; a.returns = rb->returns;
     a.last_episode_starts = rb->last_episode_starts;
@@ -831,37 +832,60 @@ int ch_rollout_collect(ch_handle* h, const ch_rollout* rb, const ch_rollout_io* 
     RolloutArgs ra;
     int rc = rollout_args(h, rb, ra, "ch_rollout_collect");
     if (rc) return rc;
-    if (!io || !io->step || !io->mean || !io->value || !io->env_actions || !log_std || !actor || !critic)
+    if (!io || !io->step || !io->mean || !io->env_actions || !log_std || !actor || (critic && !io->value))
         return fail(h, CH_ERR_INVALID, "ch_rollout_collect: NULL argument");
     const ch_step_io* sio = io->step;
     if (!sio->obs || !sio->reward || !sio->terminated || !sio->truncated || !sio->terminal_obs || !sio->reset_happened ||
         (bootstrap_truncated && !io->terminal_value))
         return fail(h, CH_ERR_INVALID, "ch_rollout_collect: the step buffers (obs, reward, terminated, truncated, "
                                        "terminal_obs, reset_happened) and terminal_value are required");
-    if (actor->dims[actor->n_layers] != rb->act_dim || critic->dims[critic->n_layers] != 1)
-        return fail(h, CH_ERR_INVALID, "ch_rollout_collect: actor output must be act_dim wide, critic output 1");
+    if (!rb->obs || !rb->actions || !rb->rewards || !rb->episode_starts || !rb->values || !rb->log_probs ||
+        !rb->advantages || !rb->returns || !rb->last_episode_starts)
+        return fail(h, CH_ERR_INVALID, "ch_rollout_collect: NULL rollout buffer array");
+    if ((reinterpret_cast<uintptr_t>(sio->obs) | reinterpret_cast<uintptr_t>(rb->obs)) & 15)
+        return fail(h, CH_ERR_INVALID, "ch_rollout_collect: obs buffers must be 16-byte aligned");
+    // critic == NULL: `actor` is a fused actor-critic (both heads in one net, output act_dim + 1 wide: the action
+    // mean, then the value); one forward per step reads the observation once.  io->mean is then its
+    // [rows][act_dim + 1] output and io->terminal_value a [rows][act_dim + 1] one for the terminal observations.
+    const bool fused = critic == nullptr;
+    const int out_w = fused ? rb->act_dim + 1 : rb->act_dim;
+    if (actor->dims[actor->n_layers] != out_w || (!fused && critic->dims[critic->n_layers] != 1))
+        return fail(h, CH_ERR_INVALID, fused ? "ch_rollout_collect: a fused actor-critic's output must be act_dim + 1 wide"
+                                             : "ch_rollout_collect: actor output must be act_dim wide, critic output 1");
     hipStream_t st = (hipStream_t)stream;
     ch_step_io s = *sio;
     s.actions = io->env_actions; s.actions_out = nullptr;
     s.flags = (s.flags & ~CH_STEP_RANDOM_ACTIONS) | CH_STEP_AUTORESET;
+    const ch_mlp* vnet = fused ? actor : critic;
+    float* value = fused ? io->mean + rb->act_dim : io->value;
+    float* tv_out = io->terminal_value;
+    const float* tval = fused ? io->terminal_value + rb->act_dim : io->terminal_value;
+    RolloutArgs a = ra;
+    a.mean_ld = out_w; a.value_ld = fused ? out_w : 1; a.tv_ld = fused ? out_w : 1;
+    // each step's post (reward + gamma V(terminal obs), next episode start) runs in the next step's store, the
+    // last one in the GAE kernel: the step outputs and terminal values it reads are still that step's then
+    a.post_prev = 1;
+    a.reward = sio->reward; a.terminated = sio->terminated; a.truncated = sio->truncated;
+    a.terminal_value = bootstrap_truncated ? tval : nullptr; a.gamma = gamma;
+    a.obs_now = sio->obs; a.mean = io->mean; a.value = value; a.log_std = log_std; a.seed = seed;
+    a.env_actions = io->env_actions;
+    HIP_TRY(h, hipSetDevice(h->device));
     for (int32_t t = 0; t < rb->n_steps; ++t) {
         // SB3 collect_rollouts, one step of every env: policy(obs) -> sample, log-prob, value -> env.step ->
         // bootstrap truncated rewards with V(terminal obs) -> buffer (OnPolicyAlgorithm.collect_rollouts)
         if ((rc = ch_policy_forward(h, actor, sio->obs, io->mean, stream))) return rc;
-        if ((rc = ch_policy_forward(h, critic, sio->obs, io->value, stream))) return rc;
-        if ((rc = ch_rollout_store(h, rb, t, sio->obs, io->mean, io->value, log_std, seed, io->env_actions, stream)))
-            return rc;
+        if (!fused && (rc = ch_policy_forward(h, critic, sio->obs, io->value, stream))) return rc;
+        a.t = t;
+        HIP_TRY(h, launch_rollout(a, 0, st));
         if ((rc = ch_step(h, &s, stream))) return rc;
         if (bootstrap_truncated &&
-            (rc = ch_mlp_forward_masked(critic, sio->terminal_obs, h->E, sio->reset_happened, io->terminal_value, stream)))
+            (rc = ch_mlp_forward_masked(vnet, sio->terminal_obs, h->E, sio->reset_happened, tv_out, stream)))
             return fail(h, rc, "ch_rollout_collect: " + std::string(ch_last_error(nullptr)));
-        if ((rc = ch_rollout_post(h, rb, t, sio->reward, sio->terminated, sio->truncated,
-                                  bootstrap_truncated ? io->terminal_value : nullptr, gamma, stream)))
-            return rc;
     }
-    if ((rc = ch_policy_forward(h, critic, sio->obs, io->value, stream))) return rc;
-    (void)st;
-    return ch_rollout_gae(h, rb, io->value, gamma, gae_lambda, stream);
+    if ((rc = ch_policy_forward(h, vnet, sio->obs, fused ? io->mean : io->value, stream))) return rc;
+    a.gamma_lambda = (float)((double)gamma * (double)gae_lambda);   // SB3: float32(self.gamma * self.gae_lambda)
+    HIP_TRY(h, launch_rollout(a, 2, st));
+    return CH_OK;
 }
 
 int ch_metrics(ch_handle* h, double* out, int32_t reset_after, void* stream) {

@@ -65,13 +65,25 @@ __device__ __forceinline__ void philox_k(uint32_t c[4], uint32_t k0, uint32_t k1
 constexpr int kRollThreads = 256;
 }  // namespace
 
+// after the env step t: reward (+ gamma V(terminal obs) for truncations) into the buffer, next episode start
+__device__ __forceinline__ void rollout_post_env(const RolloutArgs& a, int t, long long e) {
+    const long long row = (long long)t * a.rows + e;
+    const bool te = a.terminated[e] != 0, tr = a.truncated[e] != 0;
+    float r = a.reward[e];
+    if (tr && !te && a.terminal_value) r += a.gamma * a.terminal_value[e * a.tv_ld];   // rewards[idx] += gamma * terminal_value
+    a.rewards[row] = r;
+    a.last_episode_starts[e] = (te || tr) ? 1.0f : 0.0f;
+}
+
 // one workgroup per env: the observation row into the buffer, the Gaussian sample, its log-probability
-// (summed in action order by one lane), the clipped env action, value and episode start
+// (summed in action order by one lane), the clipped env action, value and episode start; with post_prev, the
+// previous step's post first (one launch per step less in ch_rollout_collect)
 __global__ __launch_bounds__(kRollThreads) void k_rollout_store(RolloutArgs a) {
     __shared__ float lp[kRollThreads];
     const long long e = blockIdx.x;
     const int tid = threadIdx.x;
     const long long row = (long long)a.t * a.rows + e;
+    if (a.post_prev && a.t > 0 && tid == 0) rollout_post_env(a, a.t - 1, e);
     const float4* src = reinterpret_cast<const float4*>(a.obs_now + e * a.obs_dim);
     float4* dst = reinterpret_cast<float4*>(a.obs + row * a.obs_dim);
     for (int k = tid; k < a.obs_dim / 4; k += kRollThreads) dst[k] = src[k];
@@ -82,7 +94,7 @@ __global__ __launch_bounds__(kRollThreads) void k_rollout_store(RolloutArgs a) {
         const float u1 = ((float)(c[0] >> 8) + 1.0f) * (1.0f / 16777216.0f);   // (0, 1]
         const float u2 = (float)(c[1] >> 8) * (1.0f / 16777216.0f);
         const float eps = sqrtf(-2.0f * logf(u1)) * cosf(6.2831853071795865f * u2);
-        const float mu = a.mean[e * a.act_dim + k], ls = a.log_std[k], sd = expf(ls);
+        const float mu = a.mean[e * a.mean_ld + k], ls = a.log_std[k], sd = expf(ls);
         const float act = mu + sd * eps;
         a.actions[row * a.act_dim + k] = act;
         // torch.distributions.Normal.log_prob: -((x - mu)^2) / (2 var) - log(std) - log(sqrt(2 pi))
@@ -95,7 +107,7 @@ __global__ __launch_bounds__(kRollThreads) void k_rollout_store(RolloutArgs a) {
         float s = 0.0f;
         for (int k = 0; k < a.act_dim; ++k) s += lp[k];
         a.log_probs[row] = s;
-        a.values[row] = a.value[e];
+        a.values[row] = a.value[e * a.value_ld];
         a.episode_starts[row] = a.last_episode_starts[e];
     }
 }
@@ -104,24 +116,20 @@ __global__ __launch_bounds__(kRollThreads) void k_rollout_store(RolloutArgs a) {
 __global__ void k_rollout_post(RolloutArgs a) {
     const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= a.rows) return;
-    const long long row = (long long)a.t * a.rows + e;
-    const bool te = a.terminated[e] != 0, tr = a.truncated[e] != 0;
-    float r = a.reward[e];
-    if (tr && !te && a.terminal_value) r += a.gamma * a.terminal_value[e];   // rewards[idx] += gamma * terminal_value
-    a.rewards[row] = r;
-    a.last_episode_starts[e] = (te || tr) ? 1.0f : 0.0f;
+    rollout_post_env(a, a.t, e);
 }
 
 // RolloutBuffer.compute_returns_and_advantage, one env per thread, backwards over the buffer in float32
 __global__ void k_rollout_gae(RolloutArgs a) {
     const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= a.rows) return;
+    if (a.post_prev) rollout_post_env(a, a.T - 1, e);   // the last step's post (ch_rollout_collect)
     const float g = a.gamma, gl = a.gamma_lambda;
     float last = 0.0f;
     for (int s = a.T - 1; s >= 0; --s) {
         const long long row = (long long)s * a.rows + e;
         float nnt, nv;
-        if (s == a.T - 1) { nnt = 1.0f - a.last_episode_starts[e]; nv = a.value[e]; }
+        if (s == a.T - 1) { nnt = 1.0f - a.last_episode_starts[e]; nv = a.value[e * a.value_ld]; }
         else { nnt = 1.0f - a.episode_starts[row + a.rows]; nv = a.values[row + a.rows]; }
         const float delta = (a.rewards[row] + (g * nv) * nnt) - a.values[row];
         last = delta + (gl * nnt) * last;

@@ -93,14 +93,14 @@ struct Level {
 #define CH_V2_MAX_BLOCK_PW 512   // per-wave-table and physics-variant kernels: 8 waves (their register use allows 2 per SIMD)
 #endif
 constexpr int kV2EnvInts = 14;
-constexpr int kV2Flags = 24;         // LDS hand-off counters between the drone wave and the cow waves + work counters
+constexpr int kV2Flags = 32;         // LDS hand-off counters between the drone wave and the cow waves + work counters
 // W = 0: one alpha pair table for the whole workgroup (4 reals per pair, G*P pairs), reused for the
 // shepherd terms.  W > 0 ("per-wave env tables", large herds): each of the W cow waves owns a slot for
 // ONE env at a time -- 3 reals per pair (gradient x, y and the bump; the consensus term is recomputed
 // from the velocities when the rows are summed), reused for that env's shepherd terms -- so the LDS
 // no longer grows with G*P and a whole CU's envs fit in one workgroup.
 struct V2Layout {
-    enum { CX = 0, DRONE, DCOW, ENVR, PAIRS, TD, MET, IMG, EI, LEVELS, PAIRL, BYTES, NOFF };
+    enum { CX = 0, DRONE, DCOW, ENVR, PAIRS, TD, MET, IMG, EI, LEVELS, PAIRL, OROW, BYTES, NOFF };
     int G, N, M, P, rows, W;
     bool sep;      // shared tables: the shepherd terms in a region of their own (not reusing the pair table)
     size_t slot;   // W > 0: reals per wave slot
@@ -123,6 +123,10 @@ struct V2Layout {
         off[EI] = o;     o = al(o + ((size_t)kV2EnvInts * G + 2 * G + 2 + kV2Flags) * 4);   // + flock/reset lists
         off[LEVELS] = o; o = al(o + 8 * sizeof(Level));              // curriculum table
         off[PAIRL] = o;  o = al(o + 2 * (size_t)P);                  // unordered cow pairs (i | j << 8)
+        // late (the 16-env x 4-drone CTDE geometry, ch_step.hip): the new attitudes' Euler angles er[3][G*N] (R) and
+        // columns 0..13 of each drone's obs row (f32)
+        const bool late = W == 0 && sep && G == 16 && N == 4 && mode == CH_MODE_CTDE;
+        off[OROW] = o;   o = al(o + (late ? 3 * (size_t)G * N * rb + 14 * 4 * (size_t)G * N : 0));
         const size_t tabs = W ? (size_t)W : (size_t)G;               // pair flags and term flags: per slot / per env
         // per-cow neighbour masks (u64) and "has a neighbour in sensing range" bytes, then the queue of pairs
         // inside the bump's support (u16; one per slot for W > 0, one for the workgroup otherwise)
@@ -160,6 +164,9 @@ hipError_t launch_metrics_reduce(double* metrics, long long E, double* out, cons
 // ch_aux.hip: the on-device PPO rollout buffer (ch_rollout_*)
 struct RolloutArgs {
     int T, t, obs_dim, act_dim, env_act_dim;
+    int mean_ld, value_ld, tv_ld;   // row strides of mean / value / terminal_value (a fused actor-critic's output
+                                    // holds both heads in one [rows][act_dim + 1] buffer)
+    int post_prev;                  // store (t) / gae: first run step t - 1's (T - 1's) post (ch_rollout_collect)
     long long rows;
     unsigned long long seed;
     float gamma, gamma_lambda;

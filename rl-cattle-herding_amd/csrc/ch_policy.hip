@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <cstdlib>
 
 #include "ch_internal.h"
 
@@ -176,15 +177,19 @@ __device__ __forceinline__ void mlp_layer(const MlpArgs& a, int li, const float*
 }
 
 
-// WIDE: some layer is wider than 128 (the RLlib 256-wide model): 16-column tiles up to 4 per wave, one
-// chunk in flight; otherwise (the SB3 actor / critic, 128 wide) up to 2 tiles per wave and two chunks in
-// flight.  Separate kernels keep the narrow one's register ring from spilling.  (Tried and reverted: a
-// split-K layer with each wave loading its K chunks straight from global memory into the MFMA operand
-// layout, no LDS staging: 85 us for one 16-row tile of the 1032-wide forward vs 35 us, the 16-row x
-// 64-byte operand loads being far slower than the coalesced staging loads.)
-template <bool WIDE>
-__global__ __launch_bounds__(WIDE ? 256 : 512) void k_mlp(MlpArgs a) {
-    constexpr int NW = WIDE ? 4 : 8;   // waves: the narrow kernel gives every wave one 16-column tile
+// NW waves per workgroup, up to TWMAX 16-column tiles per wave, DEPTH K-chunks in flight:
+//   <8, 1, 2> the SB3 actor / critic (128 wide): every wave one tile, two chunks in flight;
+//   <8, 2, 2> layers up to 256 wide (the fused actor-critic, the RLlib model): two tiles per wave, still eight
+//             waves and two chunks in flight;
+//   <4, 4, 1> the previous 256-wide kernel (four waves of up to four tiles, one chunk in flight), kept for
+//             A/B (CH_MLP_WIDE4=1): at 4096 rows it ran the fused 1032-256-256-49 forward in 41.9 us, twice the
+//             128-wide forward's 20.3 us (profiles/r03/c/policy_kernel_stats.csv).
+// Separate instantiations keep the narrow one's register ring from spilling.  (Tried and reverted: a split-K
+// layer with each wave loading its K chunks straight from global memory into the MFMA operand layout, no LDS
+// staging: 85 us for one 16-row tile of the 1032-wide forward vs 35 us, the 16-row x 64-byte operand loads
+// being far slower than the coalesced staging loads.)
+template <int NW, int TWMAX, int DEPTH>
+__global__ __launch_bounds__(64 * NW) void k_mlp(MlpArgs a) {
     extern __shared__ __align__(16) float sm[];
     float* xs = sm;                                  // [16][kKS]
     float* ws = xs + kTM * kKS;                      // [kWMax][kKS]
@@ -217,27 +222,23 @@ __global__ __launch_bounds__(WIDE ? 256 : 512) void k_mlp(MlpArgs a) {
     for (int li = 0; li < a.layers; ++li) {
         const bool last = li == a.layers - 1;
         const int nt = (a.dims[li + 1] + 15) >> 4;
-        if constexpr (WIDE) {
-            if (li == 0) {
-                if (nt <= 4) mlp_layer<true, 1, 1, NW>(a, 0, a.x, a.dims[0], nullptr, 0, a.dims[0], kloop0, xs, ws, cur, ldh, last);
-                else if (nt > 8) mlp_layer<true, 4, 1, NW>(a, 0, a.x, a.dims[0], nullptr, 0, a.dims[0], kloop0, xs, ws, cur, ldh, last);
-                else mlp_layer<true, 2, 1, NW>(a, 0, a.x, a.dims[0], nullptr, 0, a.dims[0], kloop0, xs, ws, cur, ldh, last);
-            } else {
-                const int K = a.dims[li];
-                if (nt <= 4) mlp_layer<false, 1, 1, NW>(a, li, nullptr, 0, cur, ldh, K, K, xs, ws, nxt, ldh, last);
-                else if (nt > 8) mlp_layer<false, 4, 1, NW>(a, li, nullptr, 0, cur, ldh, K, K, xs, ws, nxt, ldh, last);
-                else mlp_layer<false, 2, 1, NW>(a, li, nullptr, 0, cur, ldh, K, K, xs, ws, nxt, ldh, last);
-                float* t = cur; cur = nxt; nxt = t;
-            }
-        } else {   // 8 waves, one tile each; two chunks in flight (3 measured no faster)
-            if (li == 0) {
-                mlp_layer<true, 1, 2, NW>(a, 0, a.x, a.dims[0], nullptr, 0, a.dims[0], kloop0, xs, ws, cur, ldh, last);
-            } else {
-                const int K = a.dims[li];
-                mlp_layer<false, 1, 2, NW>(a, li, nullptr, 0, cur, ldh, K, K, xs, ws, nxt, ldh, last);
-                float* t = cur; cur = nxt; nxt = t;
-            }
+        const int tw = nt <= NW ? 1 : (nt <= 2 * NW ? 2 : 4);   // tiles per wave this layer needs
+        const bool ag = li == 0;
+        const int K = ag ? a.dims[0] : a.dims[li];
+        const int kl = ag ? kloop0 : K;
+        float* out = ag ? cur : nxt;
+#define CH_MLP_LAYER(TW)                                                                                            \
+        if (ag) mlp_layer<true, TW, DEPTH, NW>(a, 0, a.x, a.dims[0], nullptr, 0, K, kl, xs, ws, out, ldh, last);     \
+        else mlp_layer<false, TW, DEPTH, NW>(a, li, nullptr, 0, cur, ldh, K, kl, xs, ws, out, ldh, last)
+        if constexpr (TWMAX >= 4) {
+            if (tw >= 4) { CH_MLP_LAYER(4); } else if (tw == 2) { CH_MLP_LAYER(2); } else { CH_MLP_LAYER(1); }
+        } else if constexpr (TWMAX >= 2) {
+            if (tw >= 2) { CH_MLP_LAYER(2); } else { CH_MLP_LAYER(1); }
+        } else {
+            CH_MLP_LAYER(1);
         }
+#undef CH_MLP_LAYER
+        if (!ag) { float* t = cur; cur = nxt; nxt = t; }
     }
 }
 
@@ -248,12 +249,14 @@ size_t mlp_lds_bytes() { return sizeof(float) * (kTM * kKS + kWMax * kKS + 2 * k
 hipError_t launch_mlp(const MlpArgs& a, hipStream_t st) {
     // the dynamic-LDS opt-in, once per device (the attribute is per device context)
     static std::atomic<unsigned long long> attr_set{0};
+    static const bool wide4 = [] { const char* v = getenv("CH_MLP_WIDE4"); return v && v[0] == '1'; }();
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     const unsigned long long bit = 1ull << (dev & 63);
     if (!(attr_set.load(std::memory_order_relaxed) & bit)) {
-        for (const void* f : {reinterpret_cast<const void*>(&k_mlp<false>), reinterpret_cast<const void*>(&k_mlp<true>)}) {
+        for (const void* f : {reinterpret_cast<const void*>(&k_mlp<8, 1, 2>), reinterpret_cast<const void*>(&k_mlp<8, 2, 2>),
+                              reinterpret_cast<const void*>(&k_mlp<4, 4, 1>)}) {
             e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp_lds_bytes());
             if (e != hipSuccess) return e;
         }
@@ -261,10 +264,11 @@ hipError_t launch_mlp(const MlpArgs& a, hipStream_t st) {
     }
     const long long grid = (a.rows + kTM - 1) / kTM;
     if (grid == 0) return hipSuccess;
-    bool wide = false;
-    for (int i = 1; i <= a.layers; ++i) wide |= a.dims[i] > 128;
-    if (wide) hipLaunchKernelGGL(k_mlp<true>, dim3((unsigned)grid), dim3(256), mlp_lds_bytes(), st, a);
-    else hipLaunchKernelGGL(k_mlp<false>, dim3((unsigned)grid), dim3(512), mlp_lds_bytes(), st, a);
+    int maxw = 0;
+    for (int i = 1; i <= a.layers; ++i) maxw = a.dims[i] > maxw ? a.dims[i] : maxw;
+    if (maxw <= 128) hipLaunchKernelGGL((k_mlp<8, 1, 2>), dim3((unsigned)grid), dim3(512), mlp_lds_bytes(), st, a);
+    else if (wide4) hipLaunchKernelGGL((k_mlp<4, 4, 1>), dim3((unsigned)grid), dim3(256), mlp_lds_bytes(), st, a);
+    else hipLaunchKernelGGL((k_mlp<8, 2, 2>), dim3((unsigned)grid), dim3(512), mlp_lds_bytes(), st, a);
     return hipGetLastError();
 }
 

@@ -41,6 +41,8 @@ enum { F_D = 0, F_T, F_H, F_A, F_E, F_R, F_X0, F_X1, F_X2,     // hand-off count
        C_EULER,                                                   // Euler angles of the new attitudes (cow waves)
        V_DSIMD,                                                   // 1 + the SIMD the drone wave runs on
        F_S, C_SPC, C_SCAT,                                        // split: drone reward terms done on the cow waves
+       F_HC,                                                      // herd centroids done (first cow wave)
+       F_EU,                                                      // late: Euler angles in orow (the wave that took them)
        FLAG_COUNT };
 static_assert(FLAG_COUNT <= kV2Flags, "LDS flag words");
 // after the per-env rows: flocking-env list [G], reset-env list [G], their counts, then the counters
@@ -126,6 +128,8 @@ __device__ __forceinline__ void cow_sync(int* f, int waves, bool global, int* er
 #define TS(slot, val) do { if (p.tstamp) p.tstamp[(long long)blockIdx.x * 128 + (slot)] = (val); } while (0)
 // diagnostics: per cow wave 1..6, chunks taken and cycles spent in each dynamic loop (slots 64 + 10 (w - 1) + 2 loop)
 #define CHUNK_T0 const long long ck0_ = p.tstamp ? (long long)clock64() : 0
+// diagnostics: the latest of the cow waves at a point (per-workgroup max of the shader clock in slot `slot`)
+#define TS_MAX(slot) do { if (p.tstamp && (threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned long long*>(p.tstamp + (long long)blockIdx.x * 128 + (slot)), (unsigned long long)clock64()); } while (0)
 #define CHUNK_T1(loop) do { if (p.tstamp && (threadIdx.x & 63) == 0 && (threadIdx.x >> 6) <= 6) { long long* q_ = p.tstamp + (long long)blockIdx.x * 128 + 64 + 10 * ((threadIdx.x >> 6) - 1) + 2 * (loop); q_[0] += 1; q_[1] += (long long)clock64() - ck0_; } } while (0)
 
 template <class R>
@@ -138,6 +142,8 @@ struct V2Smem {
     R *mq, *meor;                                    // [G*N] MARL: reward without the approach term, end-of-episode bonus
     R* dq;                                           // [4][G*N] drone attitude after physics (for the Euler angles)
     R *rdx, *rdy, *rdz;                              // [G*N] auto-reset: the new episode's drone positions
+    R* er;                                           // [3][G*N] late: Euler angles of the new attitudes (to store)
+    float* orow;                                     // [G*N][14] late: columns 0..13 of each drone's obs row
     R* dcow;                                         // [G*N*M] squared cow-drone distances, (g*N + k)*M + j
     R *prev, *clock, *hcx, *hcy;                     // [G] env reals; herd centroid (cow waves)
     R *tgx, *tgy, *tcx, *tcy;                        // [G*P] alpha pair table
@@ -163,6 +169,8 @@ struct V2Smem {
         psp = scat + GN; mrew = psp + GN; mq = mrew + GN; meor = mq + GN; dq = meor + GN;
         rdx = dq + 4 * GN; rdy = rdx + GN; rdz = rdy + GN;
         dcow = (R*)(base + L.off[V2Layout::DCOW]);
+        er = (R*)(base + L.off[V2Layout::OROW]);   // (late geometry only; see V2Layout)
+        orow = (float*)(er + 3 * GN);
         prev = (R*)(base + L.off[V2Layout::ENVR]); clock = prev + L.G; hcx = clock + L.G; hcy = hcx + L.G;
         pl = (const uint16_t*)(base + L.off[V2Layout::PAIRL]);
         tgx = (R*)(base + L.off[V2Layout::PAIRS]); tgy = tgx + GP; tcx = tgy + GP; tcy = tcx + GP;
@@ -801,15 +809,14 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         if (ct == 0) TS(11, (long long)clock64());
         if (ct < 64) {
             // herd centroid (CattleAviary.py: HerdCentroid, np.mean over the cattle): needs only the integrated
-            // cows, so it is done before the drone hand-off; it counts Gv items of hand-off H
+            // cows, so it is done before the drone hand-off (signal HC)
             const int g = ct;
             if (g < Gv) {
                 R sx = 0, sy = 0;
                 CH_UNROLL for (int j = 0; j < M; ++j) { sx += S.cx[g * M + j]; sy += S.cy[g * M + j]; }
                 S.hcx[g] = sx / R(M); S.hcy[g] = sy / R(M);
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-            if (ct == 0) __hip_atomic_fetch_add(fl + F_H, Gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            lds_signal(fl + F_HC);
         }
         // spawn positions of the episode an auto-reset would start: scenario index + 1 (BaseAviary.py:600-606).
         // Loaded into registers here and parked in LDS after the pair loop, so the load latency hides
@@ -896,7 +903,17 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         wave_sync();
         lds_signal(fl + F_D);   // positions published: the cow waves' distance work starts now
         // the own-state row but its Euler angles, which a cow wave computes from S.dq (obs_euler)
-        if (live && wobs) obs_own_nrpy(obs_wg + dg * RW, dk, pos[2], v, w);
+        // late: into LDS, and the row's columns 0..13 go out later as one 56-byte segment (euler_store)
+        if (live && wobs) {
+            if (late) {
+                float* o = S.orow + tid * 14;
+                o[0] = (float)pos[2];
+                o[4] = (float)v[0]; o[5] = (float)v[1]; o[6] = (float)v[2];
+                o[7] = (float)w[0]; o[8] = (float)w[1]; o[9] = (float)w[2];
+            } else {
+                obs_own_nrpy(obs_wg + dg * RW, dk, pos[2], v, w);
+            }
+        }
         if (tid == 0) TS(4, (long long)clock64());
         lds_wait(fl + F_E, W1, p.err);   // env scalars and the curriculum table (staged by the cow waves)
         if (p.evald && live) CH_STS(&p.evald[di], eval_distance_step(ev_acc, ei[I_SC * G + dg] == 0, px0, py0, pos[0], pos[1]));
@@ -924,14 +941,42 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             if (fabs(pos[2] - R(kTargetAlt)) > R(kTargetAlt * 0.6)) f |= 1;
             S.pa[tid] = m1; S.pb[tid] = m2; S.dflags[tid] = f;
             if constexpr (!SPLIT) spacing_terms(S, LT[ei[I_LEVEL * G + dg]], p.compat != 0, tid, m1, m2);
-            if (wobs) obs_nbr(obs_wg + dg * RW, S.dx, S.dy, b0, i, i1, i2);
+            if (wobs && late) {   // the same entries as obs_nbr, into the row's LDS segment
+                float* o = S.orow + tid * 14 + 10;
+                o[0] = i1 >= 0 ? (float)(S.dx[b0 + i1] - xi) : 0.0f; o[1] = i1 >= 0 ? (float)(S.dy[b0 + i1] - yi) : 0.0f;
+                o[2] = i2 >= 0 ? (float)(S.dx[b0 + i2] - xi) : 0.0f; o[3] = i2 >= 0 ? (float)(S.dy[b0 + i2] - yi) : 0.0f;
+            } else if (wobs) {
+                obs_nbr(obs_wg + dg * RW, S.dx, S.dy, b0, i, i1, i2);
+            }
         }
         lds_signal(fl + F_T);
         if (tid == 0) TS(5, (long long)clock64());
-        // every cow item (distances, winding, cattle obs) and herd centroid done
-        lds_wait(fl + F_H, Gv * M + Gv + ((p.phase_mask & CH_PHASE_FORCE_TIMEOUT) ? 1 : 0), p.err);
+        const int force = (p.phase_mask & CH_PHASE_FORCE_TIMEOUT) ? 1 : 0;
+        lds_wait(fl + F_HC, 1, p.err);   // herd centroids
+        // EARLY (CTDE, opt-in CH_EARLY_RESET): the auto-reset decision comes before the cow items (hand-off H:
+        // cow-drone distances, winding numbers).  CattleAviary's _computeTerminated reads the herding effectiveness
+        // only at curriculum levels 4-6 (CattleAviary.py:465-474; a success at level 3 can move its second call to
+        // level 4) and _computeTruncated never does (497-552): a workgroup without such an env publishes its reset
+        // list from the drone terms and the centroids alone, and waits for H only for the reward.  Measured (same box,
+        // profiles/r03/b/ab.log): no gain -- H completes at ~27.0k cycles, before the drone wave would wait for it,
+        // and the reset decision itself takes ~3k cycles after the drone terms; the reset list moved from 31.4k to
+        // 30.5k cycles but the drone wave's end moved from 37.0k to 38.4k (the cow waves' final pass now competes
+        // with its reward), 197.4 vs 196.8 M env-steps/s.
+#ifdef CH_EARLY_RESET
+        constexpr bool EARLY = !marl && !SPLIT;
+#else
+        constexpr bool EARLY = false;
+#endif
+        const int g = tid;
+        const bool envl = g < Gv;
+        bool h_done = !EARLY;
+        if constexpr (EARLY) {
+            const int lv0 = envl ? ei[I_LEVEL * G + g] : 0;
+            h_done = __ballot(envl && task && lv0 >= 3 && lv0 <= 6) != 0;
+        }
+        if (h_done) lds_wait(fl + F_H, Gv * M + force, p.err);   // every cow item
         if (tid == 0) TS(6, (long long)clock64());
-        if (live && task && !SPLIT) {
+        if (live && task && !SPLIT && h_done) {
             S.scat[tid] = cattle_term(S, tid, M, R(p.cs_cc));
             if constexpr (marl) {
                 // MARLCattleAviary._computeReward's per-agent part at the step's starting level
@@ -976,8 +1021,6 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
 
         // per-env bookkeeping, one env per lane, in the reference's call order; the final scalars stay in
         // this lane's registers and go to HBM after the last barrier
-        const int g = tid;
-        const bool envl = g < Gv;
         const int e = e0 + g, b0 = g * N;
         if (envl) {
             f_n = ei[I_N * G + g]; f_sc = ei[I_SC * G + g]; f_scA = ei[I_SCA * G + g]; f_hp = ei[I_HASPREV * G + g];
@@ -993,7 +1036,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         if (envl && task) {
             const int n = f_n;
             R sdx = 0, sdy = 0;
-            const int herded = ei[I_HERD * G + g];   // counted by the cow waves (winding number)
+            const int herded = h_done ? ei[I_HERD * G + g] : 0;   // counted by the cow waves (winding number)
             scx = S.hcx[g]; scy = S.hcy[g];          // herd centroid, summed by the cow waves
             // per-drone sums without per-lane branches: a drone beyond NUM_DRONES adds +0, which leaves a sum
             // that starts at +0 unchanged (x + +0 = x unless x = -0, and such a sum is never -0)
@@ -1005,7 +1048,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             sdx = divc(sdx, R(n)); sdy = divc(sdy, R(n));
             R ex = sdx - scx, ey = sdy - scy;
             cent = sqrt(ex * ex + ey * ey + R(0) * R(0));   // HerdCentroid/DroneCentroid, z = 0.95 both
-            eff = R((double)herded / M * 100);
+            eff = h_done ? R((double)herded / M * 100) : R(0);   // (not read by this step's terminated calls)
             bool anynan = false;
             uint8_t any = 0;
             CH_UNROLL for (int i = 0; i < N; ++i) {
@@ -1273,6 +1316,15 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                 }
             }
         }
+        if constexpr (EARLY) {
+            if (!h_done) {   // the reward's inputs from the cow items: closest cows, the effectiveness
+                lds_wait(fl + F_H, Gv * M + force, p.err);
+                if (tid == 0) TS(6, (long long)clock64());
+                if (live && task) S.scat[tid] = cattle_term(S, tid, M, R(p.cs_cc));
+                wave_sync();
+                if (envl && task) eff = R((double)ei[I_HERD * G + g] / M * 100);
+            }
+        }
         if constexpr (SPLIT) lds_wait(fl + F_S, 2 * Gv * N, p.err);   // spacing and cattle terms (cow waves)
         if (envl && task) {
             const int n = f_n;
@@ -1533,7 +1585,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                 for (;;) {
                     const int b = grab(fl + (pass ? C_SCAT : C_SPC), 64, skip_post), u = b + lane;
                     if (b >= Gv * N) break;
-                    if (pass) lds_wait(fl + F_H, Gv * M + Gv, p.err);
+                    if (pass) lds_wait(fl + F_H, Gv * M, p.err);
                     else lds_wait(fl + F_T, 1, p.err);
                     if (u < Gv * N && task) {
                         const int g = qdiv(u, N, rN), k = u - g * N;
@@ -1548,7 +1600,66 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             }
         }
         // getEulerFromQuaternion of the new attitudes (BaseAviary.py:704-766): the own row's roll, pitch, yaw and
-        // the next step's PID input (the Euler cache); late: after the reset list, skipping fast-reset envs
+        // the next step's PID input (the Euler cache).  late: the angles are computed here too, into LDS (er), by
+        // the wave that takes the chunk, and that wave stores them after the reset list, skipping fast-reset envs
+        // (whose Euler cache and own row the drone wave rewrites) -- so the transcendental chain no longer sits
+        // between the reset list and the end of the workgroup.
+        int euler_b = -1;   // late: the chunk of drones whose angles this wave holds in er (wave-uniform)
+        auto euler_math = [&]() {
+          for (;;) {
+            const int b = grab(fl + C_EULER, 64, skip_post), u = b + lane;
+            if (b >= Gv * N) break;
+            euler_b = b;
+            if (u < Gv * N) {
+                const int g = qdiv(u, N, rN), k = u - g * N;
+                if (k < ei[I_N * G + g]) {
+                    const int GN = G * N;
+                    const R qq[4] = {S.dq[u], S.dq[GN + u], S.dq[2 * GN + u], S.dq[3 * GN + u]};
+                    R r3[3];
+                    quat_to_euler(qq, r3);
+                    S.er[u] = r3[0]; S.er[GN + u] = r3[1]; S.er[2 * GN + u] = r3[2];
+                    float* o = S.orow + u * 14 + 1;
+                    o[0] = (float)r3[0]; o[1] = (float)r3[1]; o[2] = (float)r3[2];
+                }
+            }
+          }
+          if (euler_b >= 0) {
+              if (lane == 0) TS(62, (long long)clock64());
+              lds_signal(fl + F_EU);   // orow's Euler columns, for the segment writers of the final pass
+          }
+        };
+        // late, after the reset list: this wave's chunk of the Euler cache (from er)
+        auto euler_store = [&]() {
+            if (euler_b < 0) return;
+            const int u = euler_b + lane;
+            if (u < Gv * N) {
+                const int g = qdiv(u, N, rN), k = u - g * N;
+                if (k < ei[I_N * G + g] && !(fast && ei[I_RESET * G + g])) {
+                    const int GN = G * N;
+                    const long long dd = (long long)e0 * N + u;
+                    CH_STS(&p.rpy[dd], S.er[u]); CH_STS(&p.rpy[DS + dd], S.er[GN + u]);
+                    CH_STS(&p.rpy[2 * DS + dd], S.er[2 * GN + u]);
+                }
+            }
+        };
+        // late, after the reset list: columns 0..13 of every live drone row -- own state, Euler angles, the two nearest
+        // drones, collected in orow by the drone wave and the Euler wave -- as 56-byte segments, seven consecutive
+        // lanes per row and one float2 each, so a row's columns go out in one coalesced piece instead of eight
+        // scattered write-through stores.  Done by the lanes the final cattle pass leaves idle.
+        auto obs_segments = [&]() {
+            if (!wobs) return;
+            const int free0 = Gv * M, nfree = CW - free0, items = Gv * N * 7;
+            const int q0 = nfree > 0 ? ct - free0 : ct, qs = nfree > 0 ? nfree : CW;
+            if (q0 < 0 || q0 >= items) return;
+            lds_wait(fl + F_EU, 1, p.err);   // (long done: the Euler math runs before the flock's tail)
+            const float r7 = 1.0f / 7.0f;
+            for (int q = q0; q < items; q += qs) {
+                const int uq = qdiv(q, 7, r7), c = q - 7 * uq;
+                const int g = qdiv(uq, N, rN), k = uq - g * N;
+                if (k < ei[I_N * G + g] && !(fast && ei[I_RESET * G + g]))
+                    st2(obs_wg + g * RW, k * 86 + 2 * c, S.orow[uq * 14 + 2 * c], S.orow[uq * 14 + 2 * c + 1]);
+            }
+        };
         auto euler_pass = [&]() {
           for (;;) {
             const int b = grab(fl + C_EULER, 64, skip_post), u = b + lane;
@@ -1569,6 +1680,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
           }
         };
         if (!late) euler_pass();
+        else euler_math();
         if constexpr (PW) {
             while (alpha_step()) {   // the rest of the alpha work (the current env first)
             }
@@ -1686,14 +1798,18 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             }
         }
         if (lane == 0) TS(40 + (tid >> 6), (long long)clock64());   // this cow wave's flock work done
+        TS_MAX(57);
         if (ct == 0) TS(31, (long long)nf);
         lds_wait(fl + F_R, 1, p.err);    // the reset list
         if (tid == 64) TS(37, (long long)clock64());
         const int nr = ei[NR_AT];
         if (ct == 0) TS(30, (long long)nr);
         if (nr && ct == 0) TS(52, (long long)clock64());
+        TS_MAX(56);
         if (late) {
-            euler_pass();
+            euler_store();
+            obs_segments();
+            TS_MAX(58);
             // final pass, each cow on its phase-0 lane: cattle observation entries (of the new episode for a
             // fast-reset env, whose new positions and velocities this lane writes too), then the flocking envs'
             // third arrival
@@ -1729,6 +1845,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                 }
                 if (ei[I_FLOCK * G + g]) arrive_final(u);
             }
+            TS_MAX(60);
         }
         if (nr && !fast) {   // uniform across the cow waves
             // ---- SB3 auto-reset of the listed envs (BaseAviary.reset, BaseAviary.py:280-331), rebuilt from
@@ -1813,6 +1930,8 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
     }
     if (tid == 0) TS(35, (long long)clock64());
     if (tid == 64) TS(36, (long long)clock64());
+    // diagnostics: the last cow wave's end (slot 63)
+    if (tid >= 64) TS_MAX(63);
     // No closing barrier: every wave leaves when its own work is done (the LDS lives until the last one
     // has).  With timestamps on, one barrier marks the workgroup's end for the trace.
     if (p.tstamp) {

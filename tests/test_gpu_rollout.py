@@ -122,3 +122,42 @@ def test_native_collect_equals_python_loop():
         b.close()
     for k in bufs[0]:
         assert torch.equal(bufs[0][k], bufs[1][k]), k
+
+
+def test_fused_actor_critic_is_bit_identical():
+    """The SB3 actor and critic packed as one net (layer 1 stacked, layers 2-3 block-diagonal; one forward per
+    step reads the observation once): its two heads equal the separate nets' forwards bit for bit -- the
+    reference's trained model-v16-6 on oracle observations and random nets on a batch -- and a native collection
+    with it fills the same buffers as with the separate nets."""
+    import torch
+    from cattleherd.env import HerdBatch
+    from cattleherd.policy import DevicePolicy
+    from cattleherd.rollout import DeviceRolloutBuffer
+    from helpers import load
+    d = load("policy_ctde_v16_6.npz")
+    sd = {k.replace("__", "."): torch.tensor(d[k]) for k in d.files if "__" in k}
+    actor, critic = DevicePolicy.sb3_actor(sd, clip=False), DevicePolicy.sb3_critic(sd)
+    fused = DevicePolicy.sb3_actor_critic(sd)
+    x = torch.tensor(d["obs"], device=fused.device).reshape(len(d["obs"]), -1)
+    y = fused.forward(x)
+    assert torch.equal(y[:, :48], actor.forward(x)) and torch.equal(y[:, 48:], critic.forward(x))
+    E, T, n, m = 1024, 24, 4, 16
+    sc = 4800 - 12 + (np.arange(E) % 24)
+    bufs = []
+    for use_fused in (False, True):
+        b = HerdBatch(E, n, m, mode="ctde", curriculum_level=7)
+        b.reset()
+        b.set_state({"step_counter": sc})
+        rb = DeviceRolloutBuffer(b, T, act_dim=48)
+        log_std = torch.full((48,), -1.0, device=b.device)
+        if use_fused:
+            rb.collect(fused, None, log_std, seed=4)
+        else:
+            rb.collect(actor, critic, log_std, seed=4)
+        torch.cuda.synchronize()
+        bufs.append({k: getattr(rb, k).cpu() for k in ("obs", "actions", "rewards", "episode_starts", "values",
+                                                        "log_probs", "advantages", "returns")})
+        assert rb.episode_starts[1:].sum() > 0
+        b.close()
+    for k in bufs[0]:
+        assert torch.equal(bufs[0][k], bufs[1][k]), k

@@ -51,6 +51,11 @@ def trace(mode, E, n, m, prec, G=None, B=None, steps=4):
         print(f"   drone wave (cycles from start): B0 {rel(3):.0f} chain {rel(4):.0f} terms {rel(5):.0f} "
               f"H {rel(6):.0f} resets-published {rel(15):.0f} book {rel(7):.0f} | cow waves: alpha {rel(8):.0f} D {rel(9):.0f} flock {rel(10):.0f} "
               f"copy {rel(11):.0f} | B1 {rel(13):.0f} end {rel(14):.0f}")
+        print(f"   drone wave end {rel(35):.0f} | cow waves: final pass start (wave 1) {rel(37):.0f}, Euler math done "
+              f"{(t[t[:, 62] > 0, 62] - t[t[:, 62] > 0, 2]).mean() if (t[:, 62] > 0).any() else float('nan'):.0f}, "
+              f"last cow wave end {rel(63):.0f}")
+        print(f"   cow waves (latest of the workgroup's waves): flock done {rel(57):.0f}, reset list seen {rel(56):.0f}, "
+              f"Euler stores done {rel(58):.0f}, final pass done {rel(60):.0f}, end {rel(63):.0f}")
         nfv = t[:, 31]
         for sel, name in ((nfv >= 0, "all"), (nfv <= 2, "nf<=2"), (nfv >= 7, "nf>=7")):
             if not sel.any():
