@@ -100,7 +100,7 @@ constexpr int kV2Flags = 32;         // LDS hand-off counters between the drone 
 // from the velocities when the rows are summed), reused for that env's shepherd terms -- so the LDS
 // no longer grows with G*P and a whole CU's envs fit in one workgroup.
 struct V2Layout {
-    enum { CX = 0, DRONE, DCOW, ENVR, PAIRS, TD, MET, IMG, EI, LEVELS, PAIRL, OROW, BYTES, NOFF };
+    enum { CX = 0, DRONE, DCOW, ENVR, PAIRS, TD, MET, IMG, EI, LEVELS, PAIRL, BYTES, NOFF };
     int G, N, M, P, rows, W;
     bool sep;      // shared tables: the shepherd terms in a region of their own (not reusing the pair table)
     size_t slot;   // W > 0: reals per wave slot
@@ -123,10 +123,6 @@ struct V2Layout {
         off[EI] = o;     o = al(o + ((size_t)kV2EnvInts * G + 2 * G + 2 + kV2Flags) * 4);   // + flock/reset lists
         off[LEVELS] = o; o = al(o + 8 * sizeof(Level));              // curriculum table
         off[PAIRL] = o;  o = al(o + 2 * (size_t)P);                  // unordered cow pairs (i | j << 8)
-        // late (the 16-env x 4-drone CTDE geometry, ch_step.hip): the new attitudes' Euler angles er[3][G*N] (R) and
-        // columns 0..13 of each drone's obs row (f32)
-        const bool late = W == 0 && sep && G == 16 && N == 4 && mode == CH_MODE_CTDE;
-        off[OROW] = o;   o = al(o + (late ? 3 * (size_t)G * N * rb + 14 * 4 * (size_t)G * N : 0));
         const size_t tabs = W ? (size_t)W : (size_t)G;               // pair flags and term flags: per slot / per env
         // per-cow neighbour masks (u64) and "has a neighbour in sensing range" bytes, then the queue of pairs
         // inside the bump's support (u16; one per slot for W > 0, one for the workgroup otherwise)

@@ -42,7 +42,6 @@ enum { F_D = 0, F_T, F_H, F_A, F_E, F_R, F_X0, F_X1, F_X2,     // hand-off count
        V_DSIMD,                                                   // 1 + the SIMD the drone wave runs on
        F_S, C_SPC, C_SCAT,                                        // split: drone reward terms done on the cow waves
        F_HC,                                                      // herd centroids done (first cow wave)
-       F_EU,                                                      // late: Euler angles in orow (the wave that took them)
        FLAG_COUNT };
 static_assert(FLAG_COUNT <= kV2Flags, "LDS flag words");
 // after the per-env rows: flocking-env list [G], reset-env list [G], their counts, then the counters
@@ -142,8 +141,6 @@ struct V2Smem {
     R *mq, *meor;                                    // [G*N] MARL: reward without the approach term, end-of-episode bonus
     R* dq;                                           // [4][G*N] drone attitude after physics (for the Euler angles)
     R *rdx, *rdy, *rdz;                              // [G*N] auto-reset: the new episode's drone positions
-    R* er;                                           // [3][G*N] late: Euler angles of the new attitudes (to store)
-    float* orow;                                     // [G*N][14] late: columns 0..13 of each drone's obs row
     R* dcow;                                         // [G*N*M] squared cow-drone distances, (g*N + k)*M + j
     R *prev, *clock, *hcx, *hcy;                     // [G] env reals; herd centroid (cow waves)
     R *tgx, *tgy, *tcx, *tcy;                        // [G*P] alpha pair table
@@ -169,8 +166,6 @@ struct V2Smem {
         psp = scat + GN; mrew = psp + GN; mq = mrew + GN; meor = mq + GN; dq = meor + GN;
         rdx = dq + 4 * GN; rdy = rdx + GN; rdz = rdy + GN;
         dcow = (R*)(base + L.off[V2Layout::DCOW]);
-        er = (R*)(base + L.off[V2Layout::OROW]);   // (late geometry only; see V2Layout)
-        orow = (float*)(er + 3 * GN);
         prev = (R*)(base + L.off[V2Layout::ENVR]); clock = prev + L.G; hcx = clock + L.G; hcy = hcx + L.G;
         pl = (const uint16_t*)(base + L.off[V2Layout::PAIRL]);
         tgx = (R*)(base + L.off[V2Layout::PAIRS]); tgy = tgx + GP; tcx = tgy + GP; tcy = tcx + GP;
@@ -903,17 +898,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         wave_sync();
         lds_signal(fl + F_D);   // positions published: the cow waves' distance work starts now
         // the own-state row but its Euler angles, which a cow wave computes from S.dq (obs_euler)
-        // late: into LDS, and the row's columns 0..13 go out later as one 56-byte segment (euler_store)
-        if (live && wobs) {
-            if (late) {
-                float* o = S.orow + tid * 14;
-                o[0] = (float)pos[2];
-                o[4] = (float)v[0]; o[5] = (float)v[1]; o[6] = (float)v[2];
-                o[7] = (float)w[0]; o[8] = (float)w[1]; o[9] = (float)w[2];
-            } else {
-                obs_own_nrpy(obs_wg + dg * RW, dk, pos[2], v, w);
-            }
-        }
+        if (live && wobs) obs_own_nrpy(obs_wg + dg * RW, dk, pos[2], v, w);
         if (tid == 0) TS(4, (long long)clock64());
         lds_wait(fl + F_E, W1, p.err);   // env scalars and the curriculum table (staged by the cow waves)
         if (p.evald && live) CH_STS(&p.evald[di], eval_distance_step(ev_acc, ei[I_SC * G + dg] == 0, px0, py0, pos[0], pos[1]));
@@ -941,13 +926,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             if (fabs(pos[2] - R(kTargetAlt)) > R(kTargetAlt * 0.6)) f |= 1;
             S.pa[tid] = m1; S.pb[tid] = m2; S.dflags[tid] = f;
             if constexpr (!SPLIT) spacing_terms(S, LT[ei[I_LEVEL * G + dg]], p.compat != 0, tid, m1, m2);
-            if (wobs && late) {   // the same entries as obs_nbr, into the row's LDS segment
-                float* o = S.orow + tid * 14 + 10;
-                o[0] = i1 >= 0 ? (float)(S.dx[b0 + i1] - xi) : 0.0f; o[1] = i1 >= 0 ? (float)(S.dy[b0 + i1] - yi) : 0.0f;
-                o[2] = i2 >= 0 ? (float)(S.dx[b0 + i2] - xi) : 0.0f; o[3] = i2 >= 0 ? (float)(S.dy[b0 + i2] - yi) : 0.0f;
-            } else if (wobs) {
-                obs_nbr(obs_wg + dg * RW, S.dx, S.dy, b0, i, i1, i2);
-            }
+            if (wobs) obs_nbr(obs_wg + dg * RW, S.dx, S.dy, b0, i, i1, i2);
         }
         lds_signal(fl + F_T);
         if (tid == 0) TS(5, (long long)clock64());
@@ -1600,66 +1579,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             }
         }
         // getEulerFromQuaternion of the new attitudes (BaseAviary.py:704-766): the own row's roll, pitch, yaw and
-        // the next step's PID input (the Euler cache).  late: the angles are computed here too, into LDS (er), by
-        // the wave that takes the chunk, and that wave stores them after the reset list, skipping fast-reset envs
-        // (whose Euler cache and own row the drone wave rewrites) -- so the transcendental chain no longer sits
-        // between the reset list and the end of the workgroup.
-        int euler_b = -1;   // late: the chunk of drones whose angles this wave holds in er (wave-uniform)
-        auto euler_math = [&]() {
-          for (;;) {
-            const int b = grab(fl + C_EULER, 64, skip_post), u = b + lane;
-            if (b >= Gv * N) break;
-            euler_b = b;
-            if (u < Gv * N) {
-                const int g = qdiv(u, N, rN), k = u - g * N;
-                if (k < ei[I_N * G + g]) {
-                    const int GN = G * N;
-                    const R qq[4] = {S.dq[u], S.dq[GN + u], S.dq[2 * GN + u], S.dq[3 * GN + u]};
-                    R r3[3];
-                    quat_to_euler(qq, r3);
-                    S.er[u] = r3[0]; S.er[GN + u] = r3[1]; S.er[2 * GN + u] = r3[2];
-                    float* o = S.orow + u * 14 + 1;
-                    o[0] = (float)r3[0]; o[1] = (float)r3[1]; o[2] = (float)r3[2];
-                }
-            }
-          }
-          if (euler_b >= 0) {
-              if (lane == 0) TS(62, (long long)clock64());
-              lds_signal(fl + F_EU);   // orow's Euler columns, for the segment writers of the final pass
-          }
-        };
-        // late, after the reset list: this wave's chunk of the Euler cache (from er)
-        auto euler_store = [&]() {
-            if (euler_b < 0) return;
-            const int u = euler_b + lane;
-            if (u < Gv * N) {
-                const int g = qdiv(u, N, rN), k = u - g * N;
-                if (k < ei[I_N * G + g] && !(fast && ei[I_RESET * G + g])) {
-                    const int GN = G * N;
-                    const long long dd = (long long)e0 * N + u;
-                    CH_STS(&p.rpy[dd], S.er[u]); CH_STS(&p.rpy[DS + dd], S.er[GN + u]);
-                    CH_STS(&p.rpy[2 * DS + dd], S.er[2 * GN + u]);
-                }
-            }
-        };
-        // late, after the reset list: columns 0..13 of every live drone row -- own state, Euler angles, the two nearest
-        // drones, collected in orow by the drone wave and the Euler wave -- as 56-byte segments, seven consecutive
-        // lanes per row and one float2 each, so a row's columns go out in one coalesced piece instead of eight
-        // scattered write-through stores.  Done by the lanes the final cattle pass leaves idle.
-        auto obs_segments = [&]() {
-            if (!wobs) return;
-            const int free0 = Gv * M, nfree = CW - free0, items = Gv * N * 7;
-            const int q0 = nfree > 0 ? ct - free0 : ct, qs = nfree > 0 ? nfree : CW;
-            if (q0 < 0 || q0 >= items) return;
-            lds_wait(fl + F_EU, 1, p.err);   // (long done: the Euler math runs before the flock's tail)
-            const float r7 = 1.0f / 7.0f;
-            for (int q = q0; q < items; q += qs) {
-                const int uq = qdiv(q, 7, r7), c = q - 7 * uq;
-                const int g = qdiv(uq, N, rN), k = uq - g * N;
-                if (k < ei[I_N * G + g] && !(fast && ei[I_RESET * G + g]))
-                    st2(obs_wg + g * RW, k * 86 + 2 * c, S.orow[uq * 14 + 2 * c], S.orow[uq * 14 + 2 * c + 1]);
-            }
-        };
+        // the next step's PID input (the Euler cache); late: after the reset list, skipping fast-reset envs
         auto euler_pass = [&]() {
           for (;;) {
             const int b = grab(fl + C_EULER, 64, skip_post), u = b + lane;
@@ -1680,7 +1600,6 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
           }
         };
         if (!late) euler_pass();
-        else euler_math();
         if constexpr (PW) {
             while (alpha_step()) {   // the rest of the alpha work (the current env first)
             }
@@ -1807,8 +1726,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         if (nr && ct == 0) TS(52, (long long)clock64());
         TS_MAX(56);
         if (late) {
-            euler_store();
-            obs_segments();
+            euler_pass();
             TS_MAX(58);
             // final pass, each cow on its phase-0 lane: cattle observation entries (of the new episode for a
             // fast-reset env, whose new positions and velocities this lane writes too), then the flocking envs'
@@ -1930,8 +1848,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
     }
     if (tid == 0) TS(35, (long long)clock64());
     if (tid == 64) TS(36, (long long)clock64());
-    // diagnostics: the last cow wave's end (slot 63)
-    if (tid >= 64) TS_MAX(63);
+    if (tid >= 64) TS_MAX(63);   // diagnostics: the last cow wave's end
     // No closing barrier: every wave leaves when its own work is done (the LDS lives until the last one
     // has).  With timestamps on, one barrier marks the workgroup's end for the trace.
     if (p.tstamp) {
