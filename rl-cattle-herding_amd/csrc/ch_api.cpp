@@ -36,6 +36,11 @@ struct ch_handle {
     void* cattle = nullptr;
     void* phys = nullptr;   // [kPhysComps][E][NC]: last_clipped_action, DYN rpy_rates
     void* envr = nullptr;
+    // f32 mode only: the f64 copies of the positions and prev_cent_dists the step integrates and measures
+    // centroids on (StepParams::pos64 / cpos64 / prev64); the f32 arrays above keep their rounded values
+    double* pos64 = nullptr;    // [3][E][NC]
+    double* cpos64 = nullptr;   // [2][E][M]
+    double* prev64 = nullptr;   // [E]
     int* envi = nullptr;
     double* metrics = nullptr;
     double* spawn = nullptr;
@@ -161,6 +166,7 @@ static StepParams<R> params(ch_handle* h) {
     p.env_off = c.env_id_offset;
     p.cs_cc = cattle_spacing_cc();
     p.drone = (R*)h->drone; p.rpy = (R*)h->rpy; p.stale = h->stale; p.obs_tag = h->obs_tag; p.cattle = (R*)h->cattle; p.envr = (R*)h->envr; p.envi = h->envi;
+    p.pos64 = h->pos64; p.cpos64 = h->cpos64; p.prev64 = h->prev64;
     p.metrics = h->metrics; p.spawn = h->spawn; p.n_scen = h->n_scen; p.n_cows = h->n_cows;
     p.debug = h->debug;
     p.phase_mask = h->phase_mask;
@@ -227,7 +233,7 @@ const char* ch_last_error(const ch_handle* h) { return h ? h->err.c_str() : g_cr
 
 static void free_all(ch_handle* h) {
     void* ptrs[] = {h->drone, h->rpy, h->cattle, h->phys, h->envr, h->envi, h->metrics, h->spawn, h->pairs,
-                    h->errw, h->mdev, h->stale, h->obs_tag, h->evald, h->rdn, h->rdv};
+                    h->errw, h->mdev, h->stale, h->obs_tag, h->evald, h->rdn, h->rdv, h->pos64, h->cpos64, h->prev64};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (h->mhost) (void)hipHostFree(h->mhost);
@@ -316,6 +322,11 @@ int ch_create(const ch_config* c, int64_t n_envs, int32_t device, ch_handle** ou
     CTRY(hipMalloc(&h->phys, h->rsize * kPhysComps * E * h->NC));
     CTRY(hipMemset(h->phys, 0, h->rsize * kPhysComps * E * h->NC));
     CTRY(hipMalloc(&h->envr, h->rsize * kEnvReal * E));
+    if (h->rsize == sizeof(float)) {
+        CTRY(hipMalloc(&h->pos64, sizeof(double) * 3 * E * h->NC));
+        CTRY(hipMalloc(&h->cpos64, sizeof(double) * 2 * E * h->M));
+        CTRY(hipMalloc(&h->prev64, sizeof(double) * E));
+    }
     CTRY(hipMalloc(&h->envi, sizeof(int) * kEnvInt * E));
     CTRY(hipMalloc(&h->metrics, sizeof(double) * kMetricRows * E));
     {
@@ -428,6 +439,9 @@ int ch_create(const ch_config* c, int64_t n_envs, int32_t device, ch_handle** ou
             CTRY(hipMemcpy(h->drone, f.data(), f.size() * 4, hipMemcpyHostToDevice));
             CTRY(hipMemcpy(h->cattle, fc.data(), fc.size() * 4, hipMemcpyHostToDevice));
             CTRY(hipMemcpy(h->envr, fr.data(), fr.size() * 4, hipMemcpyHostToDevice));
+            CTRY(hipMemcpy(h->pos64, dz.data(), sizeof(double) * 3 * E * h->NC, hipMemcpyHostToDevice));
+            CTRY(hipMemcpy(h->cpos64, cz.data(), sizeof(double) * 2 * E * h->M, hipMemcpyHostToDevice));
+            CTRY(hipMemcpy(h->prev64, rz.data(), sizeof(double) * E, hipMemcpyHostToDevice));
         }
         CTRY(hipMemcpy(h->envi, ei.data(), ei.size() * sizeof(int), hipMemcpyHostToDevice));
         CTRY(hipMemset(h->metrics, 0, sizeof(double) * kMetricRows * E));
@@ -589,6 +603,10 @@ int ch_get_state(ch_handle* h, double* hd, int32_t* hi, void* stream) {
             HIP_TRY(h, hipMemcpy(f.data() + nd + nc, h->envr, nr * 4, hipMemcpyDeviceToHost));
             HIP_TRY(h, hipMemcpy(f.data() + nd + nc + nr, h->phys, np_ * 4, hipMemcpyDeviceToHost));
             for (size_t i = 0; i < f.size(); ++i) hd[i] = f[i];
+            // the positions and prev_cent_dists as the step holds them (f64)
+            HIP_TRY(h, hipMemcpy(hd, h->pos64, sizeof(double) * 3 * h->E * h->NC, hipMemcpyDeviceToHost));
+            HIP_TRY(h, hipMemcpy(hd + nd, h->cpos64, sizeof(double) * 2 * h->E * h->M, hipMemcpyDeviceToHost));
+            HIP_TRY(h, hipMemcpy(hd + nd + nc, h->prev64, sizeof(double) * h->E, hipMemcpyDeviceToHost));
         }
     }
     if (hi) HIP_TRY(h, hipMemcpy(hi, h->envi, sizeof(int) * kEnvInt * h->E, hipMemcpyDeviceToHost));
@@ -619,6 +637,9 @@ int ch_set_state(ch_handle* h, const double* hd, const int32_t* hi, void* stream
             HIP_TRY(h, hipMemcpy(h->cattle, f.data() + nd, nc * 4, hipMemcpyHostToDevice));
             HIP_TRY(h, hipMemcpy(h->envr, f.data() + nd + nc, nr * 4, hipMemcpyHostToDevice));
             HIP_TRY(h, hipMemcpy(h->phys, f.data() + nd + nc + nr, np_ * 4, hipMemcpyHostToDevice));
+            HIP_TRY(h, hipMemcpy(h->pos64, hd, sizeof(double) * 3 * h->E * h->NC, hipMemcpyHostToDevice));
+            HIP_TRY(h, hipMemcpy(h->cpos64, hd + nd, sizeof(double) * 2 * h->E * h->M, hipMemcpyHostToDevice));
+            HIP_TRY(h, hipMemcpy(h->prev64, hd + nd + nc, sizeof(double) * h->E, hipMemcpyHostToDevice));
         }
     }
     if (hi) HIP_TRY(h, hipMemcpy(h->envi, hi, sizeof(int) * kEnvInt * h->E, hipMemcpyHostToDevice));

@@ -66,9 +66,9 @@ __device__ __forceinline__ int reset_draw_n(const StepParams<R>& p, int episode,
 
 // env-scalar part of a reset: NUM_DRONES draw (BaseAviary.py:307), counters (306, 557), spawn index
 // advanced before use (600-606); prev_cent_dists / spacing clock persist in compat mode (CattleAviary.py:89)
-template <class R>
+template <class R, class PR>
 __device__ __forceinline__ void reset_scalars(const StepParams<R>& p, int e, int& n, int& sc, int& scA, int& spawn,
-                                              int& episode, int& active, int& has_prev, R& prev, R& clock) {
+                                              int& episode, int& active, int& has_prev, PR& prev, R& clock) {
     const int nn = p.reset_n ? p.reset_n[e] : reset_draw_n(p, episode, p.env_off + e);
     n = nn;
     sc = 0; scA = 0;
@@ -80,7 +80,7 @@ __device__ __forceinline__ void reset_scalars(const StepParams<R>& p, int e, int
 }
 
 // initial position of constructor drone k of an episode with n_new drones (initialize_drone_positions,
-// BaseAviary.py:251-277)
+// BaseAviary.py:251-277); R = double also in f32 mode (the f64 position state)
 template <class R>
 __device__ __forceinline__ void reset_drone_xyz(int k, int n_new, R& x, R& y, R& z) {
     x = 0; y = 0; z = 0;
@@ -98,11 +98,12 @@ __device__ __forceinline__ void reset_drone_xyz(int k, int n_new, R& x, R& y, R&
 // persists across resets in compat mode (the reference's DSLPIDControl objects are created once,
 // BaseRLAviary.py:80)
 template <class R>
-__device__ __forceinline__ void reset_drone_store(const StepParams<R>& p, long long di, R x, R y, R z) {
+__device__ __forceinline__ void reset_drone_store(const StepParams<R>& p, long long di, double x, double y, double z) {
     const long long DS = (long long)p.E * p.NC;
     R* D = p.drone;
     if (p.evald) p.evald[di] = 0;   // episode_drone_distances: (0, 0) -- _housekeeping zeroes self.pos (BaseAviary.py:567, 683-688)
-    D[0 * DS + di] = x; D[1 * DS + di] = y; D[2 * DS + di] = z;
+    D[0 * DS + di] = R(x); D[1 * DS + di] = R(y); D[2 * DS + di] = R(z);
+    if (p.pos64) { p.pos64[0 * DS + di] = x; p.pos64[1 * DS + di] = y; p.pos64[2 * DS + di] = z; }
     D[3 * DS + di] = 0; D[4 * DS + di] = 0; D[5 * DS + di] = 0; D[6 * DS + di] = 1;
 #pragma unroll
     for (int c = 7; c < 13; ++c) D[c * DS + di] = 0;
@@ -115,8 +116,10 @@ __device__ __forceinline__ void reset_drone_store(const StepParams<R>& p, long l
 // initial pose of constructor drone k, written to the SoA state; returns x, y, z
 template <class R>
 __device__ __forceinline__ void reset_drone(const StepParams<R>& p, long long di, int k, int n_new, R& x, R& y, R& z) {
-    reset_drone_xyz(k, n_new, x, y, z);
-    reset_drone_store(p, di, x, y, z);
+    double xd, yd, zd;
+    reset_drone_xyz(k, n_new, xd, yd, zd);
+    reset_drone_store(p, di, xd, yd, zd);
+    x = R(xd); y = R(yd); z = R(zd);
 }
 
 // velocity of cow j of a reset env: angle pi(2U-1) (BaseAviary.py:631-632), U from Philox keyed
@@ -136,18 +139,19 @@ __device__ __forceinline__ void reset_cow_vel(const StepParams<R>& p, long long 
     }
 }
 template <class R>
-__device__ __forceinline__ void reset_cow_store(const StepParams<R>& p, long long ci, R x, R y, R vx, R vy) {
+__device__ __forceinline__ void reset_cow_store(const StepParams<R>& p, long long ci, double x, double y, R vx, R vy) {
     const long long CS = (long long)p.E * p.M;
-    p.cattle[0 * CS + ci] = x; p.cattle[1 * CS + ci] = y; p.cattle[2 * CS + ci] = vx; p.cattle[3 * CS + ci] = vy;
+    p.cattle[0 * CS + ci] = R(x); p.cattle[1 * CS + ci] = R(y); p.cattle[2 * CS + ci] = vx; p.cattle[3 * CS + ci] = vy;
+    if (p.cpos64) { p.cpos64[0 * CS + ci] = x; p.cpos64[1 * CS + ci] = y; }
 }
 
 // cow j of a reset env at spawn position (x0, y0) (already looked up in the scenario table)
 template <class R>
-__device__ __forceinline__ void reset_cow_at(const StepParams<R>& p, long long ci, long long env_id, int j, R x0, R y0,
-                                             uint32_t episode, R& x, R& y, R& vx, R& vy) {
-    x = x0; y = y0;
+__device__ __forceinline__ void reset_cow_at(const StepParams<R>& p, long long ci, long long env_id, int j, double x0,
+                                             double y0, uint32_t episode, R& x, R& y, R& vx, R& vy) {
+    x = R(x0); y = R(y0);
     reset_cow_vel(p, ci, env_id, j, episode, vx, vy);
-    reset_cow_store(p, ci, x, y, vx, vy);
+    reset_cow_store(p, ci, x0, y0, vx, vy);
 }
 
 // cow j of a reset env: YAML scenario position, yaw/velocity angle pi(2U-1) (BaseAviary.py:600-637),
@@ -156,7 +160,7 @@ template <class R>
 __device__ __forceinline__ void reset_cow(const StepParams<R>& p, long long ci, long long env_id, int j, int spawn,
                                           uint32_t episode, R& x, R& y, R& vx, R& vy) {
     const double* tab = p.spawn + ((long long)spawn * p.n_cows + j) * 2;
-    reset_cow_at(p, ci, env_id, j, R(tab[0]), R(tab[1]), episode, x, y, vx, vy);
+    reset_cow_at(p, ci, env_id, j, tab[0], tab[1], episode, x, y, vx, vy);
 }
 
 

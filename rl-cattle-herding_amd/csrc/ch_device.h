@@ -229,9 +229,15 @@ struct NoExtraForces {
 };
 // `extra(M, F, Tw)` adds the physics-variant link forces (BaseAviary.py:424-445) after the motor
 // model and before gravity, in the reference's applyExternalForce order.
+// pacc (f32 mode): the position accumulates in f64 -- p + (v dt), f32 increment and f64 sum -- and p is its rounded copy
+template <class R> __device__ __forceinline__ void pos_add(R p[3], double* pacc, int i, R d) {
+    if (pacc) { pacc[i] = pacc[i] + (double)d; p[i] = R(pacc[i]); }
+    else p[i] = p[i] + d;
+}
 template <class R, class X = NoExtraForces>
 __device__ __forceinline__ void drone_substep(R p[3], R q[4], R v[3], R w[3], const R rpm[4], R dt, R damping,
-                                              bool torque_world, bool gyro, const X& extra = X()) {
+                                              bool torque_world, bool gyro, const X& extra = X(),
+                                              double* pacc = nullptr) {
     const R PX[4] = {R(0.028), R(-0.028), R(-0.028), R(0.028)}, PY[4] = {R(-0.028), R(-0.028), R(0.028), R(0.028)};
     R M[9];
     quat_to_mat(q, M);
@@ -299,7 +305,7 @@ __device__ __forceinline__ void drone_substep(R p[3], R q[4], R v[3], R w[3], co
         w[i] = w[i] + aw * dt;
     }
 #pragma unroll
-    for (int i = 0; i < 3; ++i) p[i] = p[i] + v[i] * dt;
+    for (int i = 0; i < 3; ++i) pos_add(p, pacc, i, v[i] * dt);
     // btMultiBody::stepPositionsMultiDof exponential-map quaternion update (base body)
     R fang = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
     if (fang * dt > R(0.5 * (0.5 * kPi))) fang = R(0.5 * (0.5 * kPi)) / dt;
@@ -395,7 +401,8 @@ __device__ __forceinline__ void downwash_term(const R me[3], const R o[3], const
 // Physics.DYN: _dynamics (1043-1102) + _integrateQ (1104-1118).  Explicit Euler on the body rates rr
 // (persistent rpy_rates); the stored angular velocity is rotation(old quat) @ rr.
 template <class R>
-__device__ __forceinline__ void dyn_substep(R p[3], R q[4], R v[3], R w[3], R rr[3], const R rpm[4], R dt) {
+__device__ __forceinline__ void dyn_substep(R p[3], R q[4], R v[3], R w[3], R rr[3], const R rpm[4], R dt,
+                                            double* pacc = nullptr) {
     R M[9];
     quat_to_mat(q, M);
     R f[4], z[4];
@@ -416,7 +423,7 @@ __device__ __forceinline__ void dyn_substep(R p[3], R q[4], R v[3], R w[3], R rr
         rr[i] = rr[i] + dt * ((R(1) / J[i]) * tq[i]);
     }
 #pragma unroll
-    for (int i = 0; i < 3; ++i) p[i] = p[i] + dt * v[i];
+    for (int i = 0; i < 3; ++i) pos_add(p, pacc, i, dt * v[i]);
     const R on = sqrt(rr[0] * rr[0] + rr[1] * rr[1] + rr[2] * rr[2]);
     if (!(fabs(on) <= R(1e-8))) {   // np.isclose(omega_norm, 0): atol 1e-8
         R si, co;
@@ -468,7 +475,8 @@ __device__ __forceinline__ void dyn_deriv(const R q[4], const R v[3], const R rr
     for (int i = 0; i < 4; ++i) dq[i] = R(0.5) * (L[i][0] * q[0] + L[i][1] * q[1] + L[i][2] * q[2] + L[i][3] * q[3]);
 }
 template <class R>
-__device__ __forceinline__ void rk4_substep(R p[3], R q[4], R v[3], R w[3], R rr[3], const R rpm[4], R dt) {
+__device__ __forceinline__ void rk4_substep(R p[3], R q[4], R v[3], R w[3], R rr[3], const R rpm[4], R dt,
+                                            double* pacc = nullptr) {
     R kp[4][3], kv[4][3], kq[4][4], kr[4][3];
     const R a[4] = {R(0), R(0.5) * dt, R(0.5) * dt, dt};
 #pragma unroll
@@ -486,7 +494,7 @@ __device__ __forceinline__ void rk4_substep(R p[3], R q[4], R v[3], R w[3], R rr
     const R h6 = dt / R(6.0);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-        p[i] = p[i] + h6 * (((kp[0][i] + R(2) * kp[1][i]) + R(2) * kp[2][i]) + kp[3][i]);
+        pos_add(p, pacc, i, h6 * (((kp[0][i] + R(2) * kp[1][i]) + R(2) * kp[2][i]) + kp[3][i]));
         v[i] = v[i] + h6 * (((kv[0][i] + R(2) * kv[1][i]) + R(2) * kv[2][i]) + kv[3][i]);
         rr[i] = rr[i] + h6 * (((kr[0][i] + R(2) * kr[1][i]) + R(2) * kr[2][i]) + kr[3][i]);
     }
@@ -508,7 +516,8 @@ __device__ __forceinline__ void rk4_substep(R p[3], R q[4], R v[3], R w[3], R rr
 // is wave-uniform, so every lane of the branch joins each shuffle.
 template <class R>
 __device__ __forceinline__ void variant_substeps(const StepParams<R>& p, int base, int nsh, int n, R pos[3], R q[4],
-                                                 R v[3], R w[3], const R rpm[4], R lr[4], R rr[3]) {
+                                                 R v[3], R w[3], const R rpm[4], R lr[4], R rr[3],
+                                                 double* pacc = nullptr) {
     const int ph = p.physics;
     const bool gnd = ph == CH_PHYS_PYB_GND || ph == CH_PHYS_PYB_GND_DRAG_DW;
     const bool drag = ph == CH_PHYS_PYB_DRAG || ph == CH_PHYS_PYB_GND_DRAG_DW;
@@ -516,9 +525,9 @@ __device__ __forceinline__ void variant_substeps(const StepParams<R>& p, int bas
     const R h_clip = R(p.gnd_h_clip);
     for (int s = 0; s < p.substeps; ++s) {
         if (ph == CH_PHYS_DYN) {
-            dyn_substep(pos, q, v, w, rr, rpm, R(p.dt));
+            dyn_substep(pos, q, v, w, rr, rpm, R(p.dt), pacc);
         } else if (ph == CH_PHYS_DYN_RK4) {
-            rk4_substep(pos, q, v, w, rr, rpm, R(p.dt));
+            rk4_substep(pos, q, v, w, rr, rpm, R(p.dt), pacc);
         } else {
             // extra() runs before drone_substep moves the body: pos/q/v are the substep-start state
             auto extra = [&](const R* M, R* F, R* Tw) {
@@ -532,7 +541,7 @@ __device__ __forceinline__ void variant_substeps(const StepParams<R>& p, int bas
                     }
                 }
             };
-            drone_substep(pos, q, v, w, rpm, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0, extra);
+            drone_substep(pos, q, v, w, rpm, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0, extra, pacc);
         }
 #pragma unroll
         for (int c = 0; c < 4; ++c) lr[c] = rpm[c];   // last_clipped_action (BaseAviary.py:450)

@@ -69,6 +69,13 @@ struct StepParams {
     double* evald;            // optional [E][NC]: update_evaluation_metrics' per-drone episode distance
     const int* reset_n;       // optional (ch_reset_with): NUM_DRONES of each reset env instead of the Philox draw
     const double* reset_vel;  // optional (ch_reset_with): [E][M][2] cattle spawn velocities instead of Philox
+    // f32 mode (CH_PREC_F32): the positions and the centroid distance carried in f64 (every other state component is
+    // f32): drone xyz [3][E][NC], cattle xy [2][E][M], prev_cent [E].  The kernels integrate positions into them
+    // (f32 increments, f64 sums) and form centroids and the approach delta from them; the f32 arrays keep the rounded
+    // copies the f32 arithmetic reads.  NULL in f64 mode (the R arrays are the f64 state).
+    double* pos64;
+    double* cpos64;
+    double* prev64;
 };
 
 // device error word bits (ch_api.cpp reports them as CH_ERR_DEVICE)
@@ -100,7 +107,7 @@ constexpr int kV2Flags = 32;         // LDS hand-off counters between the drone 
 // from the velocities when the rows are summed), reused for that env's shepherd terms -- so the LDS
 // no longer grows with G*P and a whole CU's envs fit in one workgroup.
 struct V2Layout {
-    enum { CX = 0, DRONE, DCOW, ENVR, PAIRS, TD, MET, IMG, EI, LEVELS, PAIRL, BYTES, NOFF };
+    enum { CX = 0, DRONE, DCOW, ENVR, PAIRS, TD, MET, IMG, EI, LEVELS, PAIRL, XD, BYTES, NOFF };
     int G, N, M, P, rows, W;
     bool sep;      // shared tables: the shepherd terms in a region of their own (not reusing the pair table)
     size_t slot;   // W > 0: reals per wave slot
@@ -123,6 +130,8 @@ struct V2Layout {
         off[EI] = o;     o = al(o + ((size_t)kV2EnvInts * G + 2 * G + 2 + kV2Flags) * 4);   // + flock/reset lists
         off[LEVELS] = o; o = al(o + 8 * sizeof(Level));              // curriculum table
         off[PAIRL] = o;  o = al(o + 2 * (size_t)P);                  // unordered cow pairs (i | j << 8)
+        // f32 mode: f64 copies of the positions and centroid inputs (drone x y, cattle x y, herd centroid x y, prev)
+        off[XD] = o;     o = al(o + (rb == 4 ? (2 * (size_t)G * N + 2 * (size_t)G * M + 3 * (size_t)G) * 8 : 0));
         const size_t tabs = W ? (size_t)W : (size_t)G;               // pair flags and term flags: per slot / per env
         // per-cow neighbour masks (u64) and "has a neighbour in sensing range" bytes, then the queue of pairs
         // inside the bump's support (u16; one per slot for W > 0, one for the workgroup otherwise)

@@ -20,6 +20,9 @@ template <class R, int TEAM>
 struct Slot {
     R cx[TEAM], cy[TEAM], cvx[TEAM], cvy[TEAM];
     R dx[kNMax], dy[kNMax];
+    // f32 mode: f64 positions for the centroids (StepParams::pos64); unused in f64 mode
+    double cxd[sizeof(R) == 4 ? TEAM : 1], cyd[sizeof(R) == 4 ? TEAM : 1];
+    double dxd[sizeof(R) == 4 ? kNMax : 1], dyd[sizeof(R) == 4 ? kNMax : 1];
     R pa[kNMax], pb[kNMax], pcat[kNMax];
     R sa[kNMax], sb[kNMax], ca[kNMax], cb[kNMax], scat[kNMax];
     float own[kNMax][10];
@@ -44,7 +47,10 @@ __device__ __forceinline__ float obs_val(const Slot<R, TEAM>& S, int row, int co
     if (col < cat_off) return 0.0f;
     int k = (col - cat_off) >> 1;
     if (k >= m_obs) return 0.0f;
-    return (col & 1) ? (float)(S.cy[k] - S.dy[row]) : (float)(S.cx[k] - S.dx[row]);
+    if constexpr (sizeof(R) == 4)   // f32 mode: offsets from the f64 positions
+        return (col & 1) ? (float)(S.cyd[k] - S.dyd[row]) : (float)(S.cxd[k] - S.dxd[row]);
+    else
+        return (col & 1) ? (float)(S.cy[k] - S.dy[row]) : (float)(S.cx[k] - S.dx[row]);
 }
 
 // the env's [rows][86] block with 16-byte (or 8-byte) coalesced stores; (row, col) advance
@@ -95,10 +101,17 @@ __device__ __forceinline__ void neighbour_obs(Slot<R, TEAM>& S, int i, int n) {
         if (i1 < 0 || d < b1) { i2 = i1; b2 = b1; i1 = j; b1 = d; }
         else if (i2 < 0 || d < b2) { i2 = j; b2 = d; }
     }
-    S.nbr[i][0] = i1 >= 0 ? (float)(S.dx[i1] - S.dx[i]) : 0.0f;
-    S.nbr[i][1] = i1 >= 0 ? (float)(S.dy[i1] - S.dy[i]) : 0.0f;
-    S.nbr[i][2] = i2 >= 0 ? (float)(S.dx[i2] - S.dx[i]) : 0.0f;
-    S.nbr[i][3] = i2 >= 0 ? (float)(S.dy[i2] - S.dy[i]) : 0.0f;
+    if constexpr (sizeof(R) == 4) {   // f32 mode: offsets from the f64 positions
+        S.nbr[i][0] = i1 >= 0 ? (float)(S.dxd[i1] - S.dxd[i]) : 0.0f;
+        S.nbr[i][1] = i1 >= 0 ? (float)(S.dyd[i1] - S.dyd[i]) : 0.0f;
+        S.nbr[i][2] = i2 >= 0 ? (float)(S.dxd[i2] - S.dxd[i]) : 0.0f;
+        S.nbr[i][3] = i2 >= 0 ? (float)(S.dyd[i2] - S.dyd[i]) : 0.0f;
+    } else {
+        S.nbr[i][0] = i1 >= 0 ? (float)(S.dx[i1] - S.dx[i]) : 0.0f;
+        S.nbr[i][1] = i1 >= 0 ? (float)(S.dy[i1] - S.dy[i]) : 0.0f;
+        S.nbr[i][2] = i2 >= 0 ? (float)(S.dx[i2] - S.dx[i]) : 0.0f;
+        S.nbr[i][3] = i2 >= 0 ? (float)(S.dy[i2] - S.dy[i]) : 0.0f;
+    }
 }
 
 template <class R, int TEAM>
@@ -114,12 +127,17 @@ __device__ __forceinline__ void reset_env(const StepParams<R>& p, Slot<R, TEAM>&
             for (int c = 0; c < kPhysComps; ++c) p.phys[c * DS + (long long)e * p.NC + t] = R(0);
         }
         S.dx[t] = x; S.dy[t] = y;
+        if constexpr (sizeof(R) == 4) { S.dxd[t] = x; S.dyd[t] = y; }   // exact: multiples of 1.75
         *own_z = z;
     }
     if (t < p.M) {
         R x, y, vx, vy;
         reset_cow(p, (long long)e * p.M + t, env_id, t, spawn, episode, x, y, vx, vy);
         S.cx[t] = x; S.cy[t] = y; S.cvx[t] = vx; S.cvy[t] = vy;
+        if constexpr (sizeof(R) == 4) {   // the spawn position in f64
+            const double* tab = p.spawn + ((long long)spawn * p.n_cows + t) * 2;
+            S.cxd[t] = tab[0]; S.cyd[t] = tab[1];
+        }
     }
 }
 
@@ -134,17 +152,19 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
     const long long E = p.E;
     const long long DS = E * p.NC, CS = E * p.M;
     constexpr bool marl = MODE == 1;   // CTDE and MARL are separate instantiations (smaller code)
+    constexpr bool MIX = sizeof(R) == 4;   // f32 mode: positions, centroids and prev_cent in f64 (StepParams::pos64)
     const int m_obs = p.M < 16 ? p.M : 16;
     const int cat_off = marl ? 18 : 34;
 
     // ---- env scalars (broadcast loads) -------------------------------------------------------
     int n = 0, sc = 0, scA = 0, has_prev = 0, level = 0, tally = 0, spawn = 0, active = 0, episode = 0, stepi = 0;
-    R prev = 0, clock = 0;
+    double prev = 0;   // prev_cent_dists: f64 in both modes (f32 mode: StepParams::prev64)
+    R clock = 0;
     if (valid) {
         n = p.envi[0 * E + e]; sc = p.envi[1 * E + e]; scA = p.envi[2 * E + e]; has_prev = p.envi[3 * E + e];
         level = p.envi[4 * E + e]; tally = p.envi[5 * E + e]; spawn = p.envi[6 * E + e]; active = p.envi[7 * E + e];
         episode = p.envi[8 * E + e]; stepi = p.envi[9 * E + e];
-        prev = p.envr[0 * E + e]; clock = p.envr[1 * E + e];
+        prev = MIX ? p.prev64[e] : (double)p.envr[0 * E + e]; clock = p.envr[1 * E + e];
     }
     if (t == 0) { S.done = 0; S.reset = 0; S.n = n; }
     // metric accumulators are fetched now so their latency hides behind the physics
@@ -164,6 +184,11 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
         if (valid && t < n) {
             const long long di = (long long)e * p.NC + t;
             R pos[3] = {ld(p.drone, 0, DS, di), ld(p.drone, 1, DS, di), ld(p.drone, 2, DS, di)};
+            double pd[3] = {0, 0, 0};
+            if constexpr (MIX) {
+#pragma unroll
+                for (int c = 0; c < 3; ++c) { pd[c] = p.pos64[c * DS + di]; pos[c] = R(pd[c]); }
+            }
             const R px0 = pos[0], py0 = pos[1];
             R q[4] = {ld(p.drone, 3, DS, di), ld(p.drone, 4, DS, di), ld(p.drone, 5, DS, di), ld(p.drone, 6, DS, di)};
             R v[3] = {ld(p.drone, 7, DS, di), ld(p.drone, 8, DS, di), ld(p.drone, 9, DS, di)};
@@ -197,19 +222,25 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
                     for (int c = 0; c < 4; ++c) lr[c] = p.phys[c * PS + di];
 #pragma unroll
                     for (int c = 0; c < 3; ++c) rr[c] = p.phys[(4 + c) * PS + di];
-                    variant_substeps(p, slot * TEAM, p.NC, n, pos, q, v, w, rpm, lr, rr);
+                    variant_substeps(p, slot * TEAM, p.NC, n, pos, q, v, w, rpm, lr, rr, MIX ? pd : nullptr);
 #pragma unroll
                     for (int c = 0; c < 4; ++c) p.phys[c * PS + di] = lr[c];
 #pragma unroll
                     for (int c = 0; c < 3; ++c) p.phys[(4 + c) * PS + di] = rr[c];
                 } else {
                     for (int s = 0; s < p.substeps; ++s)
-                        drone_substep(pos, q, v, w, rpm, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0);
+                        drone_substep(pos, q, v, w, rpm, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0,
+                                      NoExtraForces(), MIX ? pd : nullptr);
                 }
             }
             R* D = p.drone;
             if (p.evald) p.evald[di] = eval_distance_step(p.evald[di], sc == 0, px0, py0, pos[0], pos[1]);
             D[0 * DS + di] = pos[0]; D[1 * DS + di] = pos[1]; D[2 * DS + di] = pos[2];
+            if constexpr (MIX) {
+#pragma unroll
+                for (int c = 0; c < 3; ++c) p.pos64[c * DS + di] = pd[c];
+                S.dxd[t] = pd[0]; S.dyd[t] = pd[1];
+            }
             D[3 * DS + di] = q[0]; D[4 * DS + di] = q[1]; D[5 * DS + di] = q[2]; D[6 * DS + di] = q[3];
             D[7 * DS + di] = v[0]; D[8 * DS + di] = v[1]; D[9 * DS + di] = v[2];
             D[10 * DS + di] = w[0]; D[11 * DS + di] = w[1]; D[12 * DS + di] = w[2];
@@ -228,9 +259,19 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
             R x = ld(p.cattle, 0, CS, ci), y = ld(p.cattle, 1, CS, ci);
             cvx = ld(p.cattle, 2, CS, ci); cvy = ld(p.cattle, 3, CS, ci);
             const R dt = R(p.dt);
+            double xd = 0, yd = 0;
+            if constexpr (MIX) { xd = p.cpos64[ci]; yd = p.cpos64[CS + ci]; }
             // no p.stepSimulation under Physics.DYN: the cattle bodies keep their positions (BaseAviary.py:447-448)
             if (!PHYS || (p.physics != CH_PHYS_DYN && p.physics != CH_PHYS_DYN_RK4))
-                for (int s = 0; s < p.substeps; ++s) { x += cvx * dt; y += cvy * dt; }
+                for (int s = 0; s < p.substeps; ++s) {
+                    if constexpr (MIX) { xd += (double)(cvx * dt); yd += (double)(cvy * dt); }
+                    else { x += cvx * dt; y += cvy * dt; }
+                }
+            if constexpr (MIX) {
+                x = R(xd); y = R(yd);
+                p.cpos64[ci] = xd; p.cpos64[CS + ci] = yd;
+                S.cxd[t] = xd; S.cyd[t] = yd;
+            }
             p.cattle[0 * CS + ci] = x; p.cattle[1 * CS + ci] = y;
             S.cx[t] = x; S.cy[t] = y; S.cvx[t] = cvx; S.cvy[t] = cvy;
         }
@@ -344,15 +385,20 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
 
         // ---- phase 4: order-dependent task bookkeeping on lane 0 ----------------------------------
         if (valid && task && t == 0) {
-            R scx = 0, scy = 0, sdx = 0, sdy = 0;
+            // centroids and their distance in f64 (f32 mode: from the f64 positions)
+            double scxd = 0, scyd = 0, sdx = 0, sdy = 0;
             int herded = 0;
 #pragma unroll 8
-            for (int j = 0; j < p.M; ++j) { scx += S.cx[j]; scy += S.cy[j]; herded += S.herded[j]; }
+            for (int j = 0; j < p.M; ++j) {
+                scxd += MIX ? S.cxd[j] : (double)S.cx[j]; scyd += MIX ? S.cyd[j] : (double)S.cy[j];
+                herded += S.herded[j];
+            }
 #pragma unroll 4
-            for (int i = 0; i < n; ++i) { sdx += S.dx[i]; sdy += S.dy[i]; }
-            scx /= R(p.M); scy /= R(p.M); sdx /= R(n); sdy /= R(n);
-            R ex = sdx - scx, ey = sdy - scy;
-            const R cent = sqrt(ex * ex + ey * ey + R(0) * R(0));
+            for (int i = 0; i < n; ++i) { sdx += MIX ? S.dxd[i] : (double)S.dx[i]; sdy += MIX ? S.dyd[i] : (double)S.dy[i]; }
+            scxd /= double(p.M); scyd /= double(p.M); sdx /= double(n); sdy /= double(n);
+            const double ex = sdx - scxd, ey = sdy - scyd;
+            const double cent = sqrt(ex * ex + ey * ey + 0.0 * 0.0);
+            const R centR = R(cent), scx = R(scxd), scy = R(scyd);
             const R eff = R((double)herded / p.M * 100);
             R ms = R(INFINITY);
             bool anynan = false;
@@ -363,7 +409,7 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
                 any_alt |= S.dflags[i] & F_ALT; any_coll |= S.dflags[i] & F_COLL; any_iso |= S.dflags[i] & F_ISO;
             }
             if (anynan) ms = R(NAN);
-            const R max_step = R(0.3 * kMaxSpeedKmh * (1000.0 / 3600.0)) / R(p.ctrl_freq);
+            const double max_step = (0.3 * kMaxSpeedKmh * (1000.0 / 3600.0)) / double(p.ctrl_freq);
             const bool time_up = (double)sc / p.ctrl_freq > p.episode_len;
             int done = 0;
             double ret = 0;
@@ -382,7 +428,7 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
                 }
                 sp_complex /= R(n * 2.0); sp_simple /= R(n * 2.0);
                 R approach = 0;
-                if (has_prev) approach = clip(((prev - cent) / (max_step + R(1e-6))) * R(5), R(-1.0), R(1.0));
+                if (has_prev) approach = R(clip(((prev - cent) / (max_step + 1e-6)) * 5.0, -1.0, 1.0));
                 prev = cent; has_prev = 1;
                 for (int i = 0; i < n; ++i) cat += S.scat[i];
                 cat /= R(n);
@@ -394,10 +440,10 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
                 for (int i = 0; i < n; ++i) tot += rg + R(0.5) * ((per_sp[i] - msp) + (S.scat[i] - mcat));
                 R rew = tot / R(n);
                 const R inc = R(1.0 / 240);
-                bool te = term_call(kLevels, level, clock, inc, ms, cent, eff);
+                bool te = term_call(kLevels, level, clock, inc, ms, centR, eff);
                 if (te) curriculum_success(kLevels, level, tally);
-                bool te2 = term_call(kLevels, level, clock, inc, ms, cent, eff);
-                bool tr = any_alt || any_coll || any_iso || cent > R(kMissionBoundary) || time_up;
+                bool te2 = term_call(kLevels, level, clock, inc, ms, centR, eff);
+                bool tr = any_alt || any_coll || any_iso || cent > kMissionBoundary || time_up;
                 p.reward[e] = (float)rew;
                 p.term[e] = te2; p.trunc[e] = tr;
                 done = te2 || tr;
@@ -413,7 +459,7 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
                 // the wrapper sees step_counter after env.step's += 1 (rllib_envs/BaseAviary.py:436)
                 const bool time_up_w = (double)(sc + 1) / p.ctrl_freq > p.episode_len;
                 auto trunc_i = [&](int i, bool tu) -> bool {
-                    return (S.dflags[i] & (F_ALT | F_COLL | F_ISO)) || cent > R(kMissionBoundary) || tu;
+                    return (S.dflags[i] & (F_ALT | F_COLL | F_ISO)) || cent > kMissionBoundary || tu;
                 };
                 auto reward_i = [&](int i, bool tu) -> R {
                     const Level& L = kLevels[level];
@@ -430,14 +476,14 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
                     r += simple * R(L.w_simple);
                     r += cplx * R(L.w_complex);
                     r += R(0.1) * R(L.w_survival);
-                    R change = has_prev ? prev - cent : R(0.0);
+                    double change = has_prev ? prev - cent : 0.0;
                     prev = cent; has_prev = 1;
-                    r += clip((change / (max_step + R(1e-6))) * R(5), R(-1.0), R(1.0)) * R(L.w_approach);
+                    r += R(clip((change / (max_step + 1e-6)) * 5.0, -1.0, 1.0)) * R(L.w_approach);
                     r += (eff / R(100)) * R(L.w_eff);
                     r += S.scat[i] * R(L.w_cattle);
-                    if (term_call(kLevels, level, clock, inc, ms, cent, eff)) {
+                    if (term_call(kLevels, level, clock, inc, ms, centR, eff)) {
                         // _endOfEpisodeReward (MARLCattleAviary.py:183-241)
-                        R eor = marl_end_of_episode(kLevels, level, a, b, cent, eff, norm2(scx - S.dx[i], scy - S.dy[i]), n);
+                        R eor = marl_end_of_episode(kLevels, level, a, b, centR, eff, norm2(scx - S.dx[i], scy - S.dy[i]), n);
                         r += eor;
                         curriculum_success(kLevels, level, tally);
                     } else if (trunc_i(i, tu)) {
@@ -448,13 +494,13 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
                 R r1[kNMax];
                 uint8_t d1[kNMax];
                 for (int i = 0; i < n; ++i) r1[i] = reward_i(i, time_up);
-                for (int i = 0; i < n; ++i) d1[i] = term_call(kLevels, level, clock, inc, ms, cent, eff);
+                for (int i = 0; i < n; ++i) d1[i] = term_call(kLevels, level, clock, inc, ms, centR, eff);
                 for (int i = 0; i < p.NC; ++i) { rout[i] = R(NAN); tout[i] = 0; trout[i] = 0; }
                 if (p.marl_wrapper) {
                     for (int i = 0; i < n; ++i) {
                         if (!((active >> i) & 1)) continue;
                         rout[i] = reward_i(i, time_up_w);
-                        tout[i] = term_call(kLevels, level, clock, inc, ms, cent, eff);
+                        tout[i] = term_call(kLevels, level, clock, inc, ms, centR, eff);
                         trout[i] = trunc_i(i, time_up_w);
                     }
                     int live = 0;
@@ -554,7 +600,8 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
         p.envi[4 * E + e] = level; p.envi[5 * E + e] = tally; p.envi[6 * E + e] = spawn; p.envi[7 * E + e] = active;
         p.envi[8 * E + e] = episode;
         if (!RESET_ONLY) p.envi[9 * E + e] = stepi + 1;   // ch_step calls on this env (Philox action counter)
-        p.envr[0 * E + e] = prev; p.envr[1 * E + e] = clock;
+        p.envr[0 * E + e] = R(prev); p.envr[1 * E + e] = clock;
+        if constexpr (MIX) p.prev64[e] = prev;
     }
 }
 

@@ -143,6 +143,9 @@ struct V2Smem {
     R *rdx, *rdy, *rdz;                              // [G*N] auto-reset: the new episode's drone positions
     R* dcow;                                         // [G*N*M] squared cow-drone distances, (g*N + k)*M + j
     R *prev, *clock, *hcx, *hcy;                     // [G] env reals; herd centroid (cow waves)
+    // f64 positions and centroid inputs (the same arrays as dx, dy, cx, cy, hcx, hcy, prev in f64 mode; f32 mode keeps
+    // f64 copies beside its f32 ones: StepParams::pos64)
+    double *dxd, *dyd, *cxd, *cyd, *hcxd, *hcyd, *prevd;
     R *tgx, *tgy, *tcx, *tcy;                        // [G*P] alpha pair table
     R* td;                                           // sep: [4][G*M] shepherd sums, new velocities; else [6][G*M*N] shepherd/predator terms (the pair table's space)
     int* cnt;                                        // sep: [G*M] per-cow arrivals (alpha row, shepherd sum)
@@ -167,6 +170,13 @@ struct V2Smem {
         rdx = dq + 4 * GN; rdy = rdx + GN; rdz = rdy + GN;
         dcow = (R*)(base + L.off[V2Layout::DCOW]);
         prev = (R*)(base + L.off[V2Layout::ENVR]); clock = prev + L.G; hcx = clock + L.G; hcy = hcx + L.G;
+        if constexpr (sizeof(R) == 8) {
+            dxd = (double*)dx; dyd = (double*)dy; cxd = (double*)cx; cyd = (double*)cy;
+            hcxd = (double*)hcx; hcyd = (double*)hcy; prevd = (double*)prev;
+        } else {
+            dxd = (double*)(base + L.off[V2Layout::XD]); dyd = dxd + GN; cxd = dyd + GN; cyd = cxd + GM;
+            hcxd = cyd + GM; hcyd = hcxd + L.G; prevd = hcyd + L.G;
+        }
         pl = (const uint16_t*)(base + L.off[V2Layout::PAIRL]);
         tgx = (R*)(base + L.off[V2Layout::PAIRS]); tgy = tgx + GP; tcx = tgy + GP; tcy = tcx + GP;
         td = L.sep ? (R*)(base + L.off[V2Layout::TD]) : tgx;
@@ -267,9 +277,9 @@ __device__ __forceinline__ void obs_nbr(float* eb, const R* dx, const R* dy, int
 }
 
 // cattle-relative entries of cow j for every live drone row (BaseRLAviary.py:319-331)
-template <class R>
-__device__ __forceinline__ void obs_cattle(float* eb, const R* dx, const R* dy, int b0, int j, int n, int cat_off, R qx,
-                                           R qy) {
+template <class A, class Q>
+__device__ __forceinline__ void obs_cattle(float* eb, const A* dx, const A* dy, int b0, int j, int n, int cat_off, Q qx,
+                                           Q qy) {
     for (int r = 0; r < n; ++r) st2(eb, r * 86 + cat_off + 2 * j, (float)(qx - dx[b0 + r]), (float)(qy - dy[b0 + r]));
 }
 
@@ -650,6 +660,9 @@ template <class R, int MODE, int GT, int NT, int MT, bool PHYS = false, bool PW 
 __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
     extern __shared__ __align__(16) unsigned char smem[];
     constexpr bool marl = MODE == 1;
+    // f32 mode: positions, centroids and the approach delta in f64 (StepParams::pos64); PT = their type
+    constexpr bool MIX = sizeof(R) == 4;
+    using PT = double;
     // SPLIT (opt-in, CH_SPLIT; the CTDE 16-env x 4-drone geometry): the drones' spacing and cattle reward terms
     // run on the cow waves, next to the drone wave's bookkeeping instead of before it; the reward waits for
     // them (F_S).  The drone wave then ends ~3k cycles earlier, but the cow waves, already the busier side after
@@ -694,6 +707,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
     bool co_simd = false;   // a cow wave on the drone wave's SIMD (starved while the drone wave issues)
     // cow waves: the first cow of this lane and, on the first cow wave's env lanes, the env scalars
     R c0[4] = {0, 0, 0, 0};
+    double c0d[2] = {0, 0}, prev0d = 0, pd[3] = {0, 0, 0};   // MIX: f64 cow position, prev_cent, drone position
     int ei0[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     R er0[2] = {0, 0};
     double met0[kMetricRows];
@@ -704,6 +718,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             const long long ci = (long long)e0 * M + ct;
 #pragma unroll
             for (int c = 0; c < 4; ++c) c0[c] = p.cattle[c * CS + ci];
+            if constexpr (MIX) { c0d[0] = p.cpos64[ci]; c0d[1] = p.cpos64[CS + ci]; }
         }
         if (ct < Gv) {
             const int e = e0 + ct;
@@ -712,6 +727,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             // constant obs bytes unknown: flagged, or this buffer is not the one that holds them
             ei0[9] = p.stale[E + e] | (p.obs_tag[e] != (unsigned long long)(uintptr_t)p.obs ? 1 : 0);
             er0[0] = p.envr[e]; er0[1] = p.envr[E + e];
+            if constexpr (MIX) prev0d = p.prev64[e];
 #pragma unroll
             for (int r = 0; r < kMetricRows; ++r) met0[r] = p.metrics[r * E + e];
         }
@@ -722,6 +738,10 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         rpy_valid = p.stale[e0 + dg] == 0;   // this env's Euler cache (written by the last v2 step)
         if (marl) act0 = p.envi[7 * E + e0 + dg];
         pos[0] = p.drone[0 * DS + di]; pos[1] = p.drone[1 * DS + di]; pos[2] = p.drone[2 * DS + di];
+        if constexpr (MIX) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) { pd[c] = p.pos64[c * DS + di]; pos[c] = R(pd[c]); }
+        }
 #pragma unroll
         for (int c = 0; c < 4; ++c) q[c] = p.drone[(3 + c) * DS + di];
 #pragma unroll
@@ -758,9 +778,19 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             R x = first ? c0[0] : p.cattle[0 * CS + ci], y = first ? c0[1] : p.cattle[1 * CS + ci];
             const R vx = first ? c0[2] : p.cattle[2 * CS + ci], vy = first ? c0[3] : p.cattle[3 * CS + ci];
             const R dt = R(p.dt);
+            double xd = 0, yd = 0;
+            if constexpr (MIX) { xd = first ? c0d[0] : p.cpos64[ci]; yd = first ? c0d[1] : p.cpos64[CS + ci]; }
             // frictionless cube (trace-pinned); no p.stepSimulation under Physics.DYN (BaseAviary.py:447-448)
             if (!PHYS || (p.physics != CH_PHYS_DYN && p.physics != CH_PHYS_DYN_RK4))
-                for (int s = 0; s < p.substeps; ++s) { x += vx * dt; y += vy * dt; }
+                for (int s = 0; s < p.substeps; ++s) {
+                    if constexpr (MIX) { xd += (double)(vx * dt); yd += (double)(vy * dt); }
+                    else { x += vx * dt; y += vy * dt; }
+                }
+            if constexpr (MIX) {
+                x = R(xd); y = R(yd);
+                CH_STS(&p.cpos64[ci], xd); CH_STS(&p.cpos64[CS + ci], yd);
+                S.cxd[u] = xd; S.cyd[u] = yd;
+            }
             CH_STS(&p.cattle[0 * CS + ci], x); CH_STS(&p.cattle[1 * CS + ci], y);
             S.cx[u] = x; S.cy[u] = y; S.cvx[u] = vx; S.cvy[u] = vy;
         }
@@ -784,6 +814,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             ei[I_FLOCK * G + g] = flk; ei[I_RESET * G + g] = 0; ei[I_HERD * G + g] = 0;
             ei[I_OBSD * G + g] = ei0[9];   // the obs block's constant bytes are unknown
             S.prev[g] = er0[0]; S.clock[g] = er0[1];
+            if constexpr (MIX) S.prevd[g] = prev0d;
 #pragma unroll
             for (int r = 0; r < kMetricRows; ++r) S.met[r * G + g] = met0[r];
         }
@@ -807,9 +838,10 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             // cows, so it is done before the drone hand-off (signal HC)
             const int g = ct;
             if (g < Gv) {
-                R sx = 0, sy = 0;
-                CH_UNROLL for (int j = 0; j < M; ++j) { sx += S.cx[g * M + j]; sy += S.cy[g * M + j]; }
-                S.hcx[g] = sx / R(M); S.hcy[g] = sy / R(M);
+                PT sx = 0, sy = 0;
+                CH_UNROLL for (int j = 0; j < M; ++j) { sx += S.cxd[g * M + j]; sy += S.cyd[g * M + j]; }
+                S.hcxd[g] = sx / PT(M); S.hcyd[g] = sy / PT(M);
+                if constexpr (MIX) { S.hcx[g] = R(S.hcxd[g]); S.hcy[g] = R(S.hcyd[g]); }
             }
             lds_signal(fl + F_HC);
         }
@@ -842,7 +874,8 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
     float* obs_wg = p.obs + (long long)e0 * RW;
     // final per-env scalars, held by the drone wave's env lanes until the write-back
     int f_n = 0, f_sc = 0, f_scA = 0, f_hp = 0, f_level = 0, f_tally = 0, f_spawn = 0, f_active = 0, f_episode = 0;
-    R f_prev = 0, f_clock = 0;
+    PT f_prev = 0;   // prev_cent_dists (f64 also in f32 mode: the approach delta is a difference of two ~10 m distances)
+    R f_clock = 0;
 
     if (tid < 64) {
         // ============ drone wave: the critical path ============================================
@@ -872,17 +905,23 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                 R rpm[4];
                 pid_vel(pos, q, v, Rm, rpy, a, R(p.dt_ctrl), pid, rpm, p.debug ? p.debug + di * 16 : nullptr);
                 if constexpr (PHYS) {
-                    variant_substeps(p, dg * N, N, n, pos, q, v, w, rpm, ph_lr, ph_rr);
+                    variant_substeps(p, dg * N, N, n, pos, q, v, w, rpm, ph_lr, ph_rr, MIX ? pd : nullptr);
 #pragma unroll
                     for (int c = 0; c < 4; ++c) CH_STS(&p.phys[c * DS + di], ph_lr[c]);
 #pragma unroll
                     for (int c = 0; c < 3; ++c) CH_STS(&p.phys[(4 + c) * DS + di], ph_rr[c]);
                 } else {
                     for (int s = 0; s < p.substeps; ++s)
-                        drone_substep(pos, q, v, w, rpm, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0);
+                        drone_substep(pos, q, v, w, rpm, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0,
+                                      NoExtraForces(), MIX ? pd : nullptr);
                 }
             }
             R* D = p.drone;
+            if constexpr (MIX) {
+#pragma unroll
+                for (int c = 0; c < 3; ++c) CH_STS(&p.pos64[c * DS + di], pd[c]);
+                S.dxd[tid] = pd[0]; S.dyd[tid] = pd[1];
+            }
 #pragma unroll
             for (int c = 0; c < 3; ++c) CH_STS(&D[c * DS + di], pos[c]);
 #pragma unroll
@@ -926,7 +965,8 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             if (fabs(pos[2] - R(kTargetAlt)) > R(kTargetAlt * 0.6)) f |= 1;
             S.pa[tid] = m1; S.pb[tid] = m2; S.dflags[tid] = f;
             if constexpr (!SPLIT) spacing_terms(S, LT[ei[I_LEVEL * G + dg]], p.compat != 0, tid, m1, m2);
-            if (wobs) obs_nbr(obs_wg + dg * RW, S.dx, S.dy, b0, i, i1, i2);
+            // offsets from the f64 positions in f32 mode (S.dxd; the same array as S.dx in f64 mode)
+            if (wobs) obs_nbr(obs_wg + dg * RW, S.dxd, S.dyd, b0, i, i1, i2);
         }
         lds_signal(fl + F_T);
         if (tid == 0) TS(5, (long long)clock64());
@@ -977,15 +1017,15 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                 P += simple * R(Lv.w_simple);
                 P += cplx * R(Lv.w_complex);
                 P += R(0.1) * R(Lv.w_survival);
-                R sdx = 0, sdy = 0;
+                PT sdx = 0, sdy = 0;
                 CH_UNROLL for (int i = 0; i < N; ++i) {
                     const bool li = i < n;
-                    sdx += li ? S.dx[b0 + i] : R(0); sdy += li ? S.dy[b0 + i] : R(0);
+                    sdx += li ? S.dxd[b0 + i] : PT(0); sdy += li ? S.dyd[b0 + i] : PT(0);
                 }
-                sdx = divc(sdx, R(n)); sdy = divc(sdy, R(n));
+                sdx = divc(sdx, PT(n)); sdy = divc(sdy, PT(n));
                 const R scx = S.hcx[g], scy = S.hcy[g];
-                const R ex = sdx - scx, ey = sdy - scy;
-                const R cent = sqrt(ex * ex + ey * ey + R(0) * R(0));
+                const PT ex = sdx - S.hcxd[g], ey = sdy - S.hcyd[g];
+                const R cent = R(sqrt(ex * ex + ey * ey + PT(0) * PT(0)));
                 const R eff = R((double)ei[I_HERD * G + g] / M * 100);
                 R Q = P;
                 Q += divc(eff, R(100)) * R(Lv.w_eff);
@@ -1005,28 +1045,29 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             f_n = ei[I_N * G + g]; f_sc = ei[I_SC * G + g]; f_scA = ei[I_SCA * G + g]; f_hp = ei[I_HASPREV * G + g];
             f_level = ei[I_LEVEL * G + g]; f_tally = ei[I_TALLY * G + g]; f_spawn = ei[I_SPAWN * G + g];
             f_active = ei[I_ACTIVE * G + g]; f_episode = ei[I_EPISODE * G + g];
-            f_prev = S.prev[g]; f_clock = S.clock[g];
+            f_prev = S.prevd[g]; f_clock = S.clock[g];
         }
         int done = 0, rs = 0, n_term = 0, n_trunc = 0, n_nan = 0, level_r = f_level;
         double ret = 0;
         bool te2 = false, tr = false;
-        R cent = 0, eff = 0, ms = R(INFINITY), scx = 0, scy = 0;
-        const R max_step = R(0.3 * kMaxSpeedKmh * (1000.0 / 3600.0)) / R(p.ctrl_freq);
+        PT cent = 0;   // HerdCentroid/DroneCentroid distance (f64 also in f32 mode; R(cent) where the f32 math reads it)
+        R eff = 0, ms = R(INFINITY), scx = 0, scy = 0;
+        const PT max_step_p = PT(0.3 * kMaxSpeedKmh * (1000.0 / 3600.0)) / PT(p.ctrl_freq);
         if (envl && task) {
             const int n = f_n;
-            R sdx = 0, sdy = 0;
+            PT sdx = 0, sdy = 0;
             const int herded = h_done ? ei[I_HERD * G + g] : 0;   // counted by the cow waves (winding number)
             scx = S.hcx[g]; scy = S.hcy[g];          // herd centroid, summed by the cow waves
             // per-drone sums without per-lane branches: a drone beyond NUM_DRONES adds +0, which leaves a sum
             // that starts at +0 unchanged (x + +0 = x unless x = -0, and such a sum is never -0)
             CH_UNROLL for (int i = 0; i < N; ++i) {
                 const bool li = i < n;
-                const R xi = S.dx[b0 + i], yi = S.dy[b0 + i];
-                sdx += li ? xi : R(0); sdy += li ? yi : R(0);
+                const PT xi = S.dxd[b0 + i], yi = S.dyd[b0 + i];
+                sdx += li ? xi : PT(0); sdy += li ? yi : PT(0);
             }
-            sdx = divc(sdx, R(n)); sdy = divc(sdy, R(n));
-            R ex = sdx - scx, ey = sdy - scy;
-            cent = sqrt(ex * ex + ey * ey + R(0) * R(0));   // HerdCentroid/DroneCentroid, z = 0.95 both
+            sdx = divc(sdx, PT(n)); sdy = divc(sdy, PT(n));
+            PT ex = sdx - S.hcxd[g], ey = sdy - S.hcyd[g];
+            cent = sqrt(ex * ex + ey * ey + PT(0) * PT(0));   // HerdCentroid/DroneCentroid, z = 0.95 both
             eff = h_done ? R((double)herded / M * 100) : R(0);   // (not read by this step's terminated calls)
             bool anynan = false;
             uint8_t any = 0;
@@ -1046,10 +1087,10 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                 // _computeTruncated.  The terminated calls read nothing the reward writes (the reward uses the
                 // level it started with), so they run first and the reset decision is published early.
                 const R inc = R(1.0 / 240);
-                bool te = term_call(LT, f_level, f_clock, inc, ms, cent, eff);
+                bool te = term_call(LT, f_level, f_clock, inc, ms, R(cent), eff);
                 if (te) curriculum_success(LT, f_level, f_tally);
-                te2 = term_call(LT, f_level, f_clock, inc, ms, cent, eff);
-                tr = (any & 7) || cent > R(kMissionBoundary) || time_up;
+                te2 = term_call(LT, f_level, f_clock, inc, ms, R(cent), eff);
+                tr = (any & 7) || cent > PT(kMissionBoundary) || time_up;
                 done = te2 || tr;
             } else {
                 // MARLCattleAviary reward / terminated / truncated in the order env.step
@@ -1061,7 +1102,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                 int& tally = f_tally;
                 int& has_prev = f_hp;
                 int& active = f_active;
-                R& prev = f_prev;
+                PT& prev = f_prev;
                 R& clock = f_clock;
                 const R inc = R(1.0) / R(p.ctrl_freq);
                 const int lvl0 = level;
@@ -1092,7 +1133,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                 auto EO = AG(r_eo, S.meor[b0 + i_]);
 #undef AG
                 Level Lc = LT[level];   // the current level's constants (re-read when the level changes)
-                const R approach_div = max_step + R(1e-6);
+                const PT approach_div = max_step_p + PT(1e-6);
                 const R eff100 = divc(eff, R(100));   // eff / 100, the same for every call of this step
                 auto succeed = [&]() {   // curriculum_success (curriculum_learning.py:200-219)
                     tally += 1;
@@ -1104,15 +1145,16 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                     }
                 };
                 auto trunc_i = [&](int i, bool tu) -> bool {
-                    return (DF(i) & 7) || cent > R(kMissionBoundary) || tu;
+                    return (DF(i) & 7) || cent > PT(kMissionBoundary) || tu;
                 };
+                const R centR = R(cent);
                 auto reward_i = [&](int i, bool tu) -> R {
                     const R a = PA(i), b = PB(i);
                     const bool same = level == lvl0;   // the drone lanes' prefixes hold for this level
-                    R change = has_prev ? prev - cent : R(0.0);
+                    PT change = has_prev ? prev - cent : PT(0.0);
                     prev = cent; has_prev = 1;
                     R r;
-                    if (same && change == R(0)) {
+                    if (same && change == PT(0)) {
                         // the approach term is +-0 and leaves P unchanged: the reward is Q
                         r = QQ(i);
                     } else {
@@ -1131,12 +1173,12 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                             r += cplx * R(Lc.w_complex);
                             r += R(0.1) * R(Lc.w_survival);
                         }
-                        r += clip(divc(change, approach_div) * R(5), R(-1.0), R(1.0)) * R(Lc.w_approach);
+                        r += R(clip(divc(change, approach_div) * PT(5), PT(-1.0), PT(1.0))) * R(Lc.w_approach);
                         r += eff100 * R(Lc.w_eff);
                         r += SC(i) * R(Lc.w_cattle);
                     }
-                    if (term_call_L(Lc, level, clock, inc, ms, cent, eff)) {
-                        r += same ? EO(i) : marl_end_of_episode_L(Lc, level, a, b, cent, eff, DH(i), n);
+                    if (term_call_L(Lc, level, clock, inc, ms, centR, eff)) {
+                        r += same ? EO(i) : marl_end_of_episode_L(Lc, level, a, b, centR, eff, DH(i), n);
                         succeed();
                     } else if (trunc_i(i, tu)) {
                         r -= R(50);
@@ -1167,7 +1209,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                             ck = 0;
                         }
                     } else if (K > 0) {
-                        fast = !term_call_L(Lc, level, ck, inc, ms, cent, eff);
+                        fast = !term_call_L(Lc, level, ck, inc, ms, centR, eff);
                     }
                     if (fast) {
                         clock = ck;
@@ -1201,7 +1243,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                     }
                     CH_UNROLL for (int i = 0; i < N; ++i) {
                         if (i >= n) break;
-                        const uint8_t d = term_call_L(Lc, level, clock, inc, ms, cent, eff);
+                        const uint8_t d = term_call_L(Lc, level, clock, inc, ms, centR, eff);
                         if constexpr (NT > 0) r_d1[i] = d; else S.md1[b0 + i] = d;
                     }
                     if (g == 0) TS(34, (long long)clock64());
@@ -1213,7 +1255,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                             uint8_t tt = 0, trr = 0;
                             if (i < n && ((act0 >> i) & 1)) {
                                 rr = reward_i(i, time_up_w);
-                                tt = term_call_L(Lc, level, clock, inc, ms, cent, eff);
+                                tt = term_call_L(Lc, level, clock, inc, ms, centR, eff);
                                 trr = trunc_i(i, time_up_w);
                             }
                             CH_ST(&p.reward[(long long)e * N + i], (float)rr);
@@ -1265,14 +1307,15 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             wave_sync();   // the reset flags and NUM_DRONES draws of the env lanes
             const bool rd = dlane && ei[I_RESET * G + dg];
             const int n_new = rd ? ei[I_NEWN * G + dg] : 0;
-            R x = 0, y = 0, z = 0;
+            double xd = 0, yd = 0, zd = 0;
             if (rd) {
-                reset_drone_xyz(dk, n_new, x, y, z);
-                S.rdx[tid] = x; S.rdy[tid] = y; S.rdz[tid] = z;
+                reset_drone_xyz(dk, n_new, xd, yd, zd);
+                S.rdx[tid] = R(xd); S.rdy[tid] = R(yd); S.rdz[tid] = R(zd);
             }
+            const R z = R(zd);
             wave_sync();   // the env's new drone positions (nearest neighbours)
             if (rd) {
-                reset_drone_store(p, di, x, y, z);
+                reset_drone_store(p, di, xd, yd, zd);
                 if constexpr (PHYS) {   // last_clipped_action, rpy_rates = 0 (_housekeeping, BaseAviary.py:565, 581-582)
 #pragma unroll
                     for (int c = 0; c < kPhysComps; ++c) CH_STS(&p.phys[c * DS + di], R(0));
@@ -1323,7 +1366,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                 const R n2 = R(n * 2.0), nn = R(n);
                 sp_complex = divc(sp_complex, n2); sp_simple = divc(sp_simple, n2);
                 R approach = 0;
-                if (f_hp) approach = clip(divc(f_prev - cent, max_step + R(1e-6)) * R(5), R(-1.0), R(1.0));
+                if (f_hp) approach = R(clip(divc(f_prev - cent, max_step_p + PT(1e-6)) * PT(5), PT(-1.0), PT(1.0)));
                 f_prev = cent; f_hp = 1;
                 CH_UNROLL for (int i = 0; i < N; ++i) cat += i < n ? scat_i[i] : R(0);
                 cat = divc(cat, nn);
@@ -1384,7 +1427,8 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             CH_STS(&p.envi[3 * E + e], f_hp); CH_STS(&p.envi[4 * E + e], f_level); CH_STS(&p.envi[5 * E + e], f_tally);
             CH_STS(&p.envi[6 * E + e], f_spawn); CH_STS(&p.envi[7 * E + e], f_active); CH_STS(&p.envi[8 * E + e], f_episode);
             CH_STS(&p.envi[9 * E + e], stepi_env + 1);   // ch_step calls on this env
-            CH_STS(&p.envr[0 * E + e], f_prev); CH_STS(&p.envr[1 * E + e], f_clock);
+            CH_STS(&p.envr[0 * E + e], R(f_prev)); CH_STS(&p.envr[1 * E + e], f_clock);
+            if constexpr (MIX) CH_STS(&p.prev64[e], f_prev);
             // this step wrote the env's Euler cache and, unless obs were masked off, its whole obs block
             p.stale[e] = 0;
             if (wobs) p.stale[E + e] = 0;
@@ -1417,6 +1461,12 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         // after the reset list arrives with +4; whichever of the two comes last stores the velocity -- the new
         // episode's draw for a fast-reset env
         R* const nv = S.td + 2 * G * M;
+        // spawn position component c of cow j in env g's next episode (scenario index + 1, BaseAviary.py:600-606), f64
+        auto spawn_d = [&](int g, int j, int c) -> double {
+            int sp = ei[I_SPAWN * G + g] + 1;
+            if (sp >= p.n_scen) sp = 0;
+            return p.spawn[((long long)sp * p.n_cows + j) * 2 + c];
+        };
         auto store_final = [&](int u) {
             const int g = qdiv(u, M, 1.0f / (float)M);
             const long long ci = (long long)e0 * M + u;
@@ -1549,7 +1599,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                 }
                 if (wn != 0) atomicAdd(&ei[I_HERD * G + g], 1);
             }
-            if (j < m_obs && wobs && !late) obs_cattle(obs_wg + g * RW, S.dx, S.dy, b0, j, n, cat_off, qix, qiy);
+            if (j < m_obs && wobs && !late) obs_cattle(obs_wg + g * RW, S.dxd, S.dyd, b0, j, n, cat_off, S.cxd[u], S.cyd[u]);
             }
             // H counts finished items, so a wave still busy with an alpha chunk does not hold the drone wave up
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -1737,8 +1787,10 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                 const int n_old = ei[I_N * G + g];
                 const long long ci = (long long)e0 * M + u;
                 if (rs_) {
-                    const R x = S.spx[u], y = S.spy[u];
-                    p.cattle[0 * CS + ci] = x; p.cattle[1 * CS + ci] = y;
+                    // the new episode's spawn position (prefetched in LDS; in f32 mode re-read in f64 from the table)
+                    const double x = MIX ? spawn_d(g, j, 0) : (double)S.spx[u], y = MIX ? spawn_d(g, j, 1) : (double)S.spy[u];
+                    p.cattle[0 * CS + ci] = R(x); p.cattle[1 * CS + ci] = R(y);
+                    if constexpr (MIX) { p.cpos64[ci] = x; p.cpos64[CS + ci] = y; }
                     if (!ei[I_FLOCK * G + g]) {   // no flock update: the velocity is written here
                         R vx, vy;
                         reset_cow_vel(p, ci, p.env_off + e0 + g, j, (uint32_t)ei[I_EPISODE * G + g], vx, vy);
@@ -1750,7 +1802,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                         for (int r = 0; r < N; ++r) {
                             if (r >= n_new && r >= n_old) break;
                             if (r < n_new) {
-                                R dx, dy, dz;
+                                double dx, dy, dz;
                                 reset_drone_xyz(r, n_new, dx, dy, dz);
                                 st2(eb, r * 86 + cat_off + 2 * j, (float)(x - dx), (float)(y - dy));
                             } else {
@@ -1759,7 +1811,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                         }
                     }
                 } else if (wobs && j < m_obs) {
-                    obs_cattle(obs_wg + g * RW, S.dx, S.dy, g * N, j, n_old, cat_off, S.cx[u], S.cy[u]);
+                    obs_cattle(obs_wg + g * RW, S.dxd, S.dyd, g * N, j, n_old, cat_off, S.cxd[u], S.cyd[u]);
                 }
                 if (ei[I_FLOCK * G + g]) arrive_final(u);
             }
@@ -1783,13 +1835,13 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             const int dl = W1 >= 2 ? 64 : CW, c0l = W1 >= 2 ? 64 : 0, cl = CW - c0l;
             // drones: one per lane of the first cow wave (nr * N <= G * N <= 64 <= dl)
             const bool dit = ct < dl && ct < nr * N;
-            R rx = 0, ry = 0, rz = 0;
+            double rx = 0, ry = 0, rz = 0;
             if (dit) {
                 const int k0 = qdiv(ct, N, rN), g = rl[k0], k = ct - k0 * N, ud = g * N + k;
                 const int n = reset_draw_n(p, ei[I_EPISODE * G + g], p.env_off + e0 + g);
                 if (k == 0) ei[I_NEWN * G + g] = n;
                 reset_drone_xyz(k, n, rx, ry, rz);
-                S.rdx[ud] = rx; S.rdy[ud] = ry; S.rdz[ud] = rz;
+                S.rdx[ud] = R(rx); S.rdy[ud] = R(ry); S.rdz[ud] = R(rz);
             }
             // cattle: the first two per lane in registers (the rest, beyond 2 cl, after the sync)
             constexpr int RI = 2;
@@ -1824,7 +1876,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                         // identity quaternion: getEulerFromQuaternion gives atan2(+0, 1), asin(-2 * (+0)), atan2(+0, 1)
                         // = (+0, -0, +0) (quat_to_euler); zero velocities
                         const R zero3[3] = {0, 0, 0}, rpy0[3] = {R(0), -R(0), R(0)};
-                        obs_own(eb, k, rz, rpy0, zero3, zero3);
+                        obs_own(eb, k, R(rz), rpy0, zero3, zero3);
                         const int nb = nearest_two(S.rdx, S.rdy, g * N, k, n);
                         obs_nbr(eb, S.rdx, S.rdy, g * N, k, (nb & 0xff) - 1, (nb >> 8) - 1);
                     } else if (k < ei[I_N * G + g]) {
@@ -1839,7 +1891,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                     R vx = i == 0 ? cvx_r[0] : cvx_r[1], vy = i == 0 ? cvy_r[0] : cvy_r[1];
                     if (i >= RI)
                         reset_cow_vel(p, (long long)e0 * M + uc, p.env_off + e0 + g, j, (uint32_t)ei[I_EPISODE * G + g], vx, vy);
-                    const R x = S.spx[uc], y = S.spy[uc];
+                    const double x = MIX ? spawn_d(g, j, 0) : (double)S.spx[uc], y = MIX ? spawn_d(g, j, 1) : (double)S.spy[uc];
                     reset_cow_store(p, (long long)e0 * M + uc, x, y, vx, vy);
                     if (wobs && j < m_obs) obs_cattle(obs_wg + g * RW, S.rdx, S.rdy, g * N, j, ei[I_NEWN * G + g], cat_off, x, y);
                 }

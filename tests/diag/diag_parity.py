@@ -4,7 +4,7 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(ROOT, "rl-cattle-herding_amd"), os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle")]
 import torch  # noqa: E402
 from helpers import load, stack, state_at  # noqa: E402
