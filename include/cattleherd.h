@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CH_ABI_VERSION 4
+#define CH_ABI_VERSION 5
 
 enum {
     CH_OK = 0,
@@ -212,7 +212,16 @@ typedef struct ch_mlp {
     int32_t hidden_act;        /* CH_ACT_* applied after every layer but the last */
     int32_t clip;              /* non-zero: clip the output to [lo, hi] */
     float lo, hi;
+    const float* packed;       /* NULL, or the same weights in the MFMA operand layout written by ch_mlp_pack
+                                  (read instead of `weight`; re-pack after every weight update) */
 } ch_mlp;
+
+/* The operand layout of the forward kernel: per layer [16-column tile][32-wide K pair][half][lane][4], so that
+ * each wave's weight load is one contiguous 1 KB block.  ch_mlp_packed_size: floats of device memory the
+ * layout of `net` takes; ch_mlp_pack: writes it (from net->weight) into dst on `stream`.  No reference
+ * counterpart: the reference's torch forward reads nn.Linear weights (CTDECattleHerder.py:203). */
+int64_t ch_mlp_packed_size(const ch_mlp* net);
+int ch_mlp_pack(const ch_mlp* net, float* dst, void* stream);
 
 /* Replaces: stable_baselines3 ActorCriticPolicy.predict(obs, deterministic=True) for a Box action
  * space (mlp_extractor.policy_net -> action_net -> np.clip to the space, CTDECattleHerder.py:203,

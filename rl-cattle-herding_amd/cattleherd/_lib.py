@@ -15,7 +15,7 @@ CH_PREC_F64, CH_PREC_F32 = 0, 1
 CH_STEP_AUTORESET, CH_STEP_RANDOM_ACTIONS = 0x1, 0x2
 METRIC_NAMES = ("steps", "episodes", "return_sum", "length_sum", "terminated", "truncated", "nan_rewards",
                 "effectiveness_sum")
-ABI_VERSION = 4
+ABI_VERSION = 5
 # Physics enum (utils/enums.py:13-21, include/cattleherd.h CH_PHYS_*)
 PHYSICS = {"pyb": 0, "dyn": 1, "pyb_gnd": 2, "pyb_drag": 3, "pyb_dw": 4, "pyb_gnd_drag_dw": 5, "dyn_rk4": 6}
 
@@ -24,7 +24,8 @@ EXPORTS = ("ch_default_config", "ch_create", "ch_destroy", "ch_last_error", "ch_
            "ch_step",
            "ch_state_size", "ch_get_state", "ch_set_state", "ch_metrics", "ch_metrics_device", "ch_sync",
            "ch_get_eval", "ch_builtin_spawn_table", "ch_rollout_store", "ch_rollout_post", "ch_rollout_gae", "ch_rollout_collect",
-           "ch_spawn_table", "ch_mlp_forward", "ch_mlp_forward_masked", "ch_policy_forward")
+           "ch_spawn_table", "ch_mlp_forward", "ch_mlp_forward_masked", "ch_policy_forward", "ch_mlp_packed_size",
+           "ch_mlp_pack")
 CH_ACT_NONE, CH_ACT_TANH, CH_ACT_RELU = 0, 1, 2
 
 
@@ -50,7 +51,7 @@ class ChStepIO(ctypes.Structure):
 class ChMlp(ctypes.Structure):
     _fields_ = [("n_layers", ctypes.c_int32), ("dims", ctypes.c_int32 * 5), ("weight", ctypes.c_void_p * 4),
                 ("bias", ctypes.c_void_p * 4), ("hidden_act", ctypes.c_int32), ("clip", ctypes.c_int32),
-                ("lo", ctypes.c_float), ("hi", ctypes.c_float)]
+                ("lo", ctypes.c_float), ("hi", ctypes.c_float), ("packed", ctypes.c_void_p)]
 
 
 class ChError(RuntimeError):
@@ -94,9 +95,12 @@ def lib():
     L.ch_mlp_forward.argtypes = [P(ChMlp), vp, i64, vp, vp]
     L.ch_mlp_forward_masked.argtypes = [P(ChMlp), vp, i64, vp, vp, vp]
     L.ch_policy_forward.argtypes = [vp, P(ChMlp), vp, vp, vp]
+    L.ch_mlp_packed_size.argtypes = [P(ChMlp)]
+    L.ch_mlp_pack.argtypes = [P(ChMlp), vp, vp]
     for name in EXPORTS:
         if name not in ("ch_last_error",):
             getattr(L, name).restype = ctypes.c_int
+    L.ch_mlp_packed_size.restype = ctypes.c_int64
     _lib = L
     return L
 

@@ -63,6 +63,24 @@ class DevicePolicy:
         net.clip = 1 if clip is not None else 0
         net.lo, net.hi = (clip if clip is not None else (0.0, 0.0))
         self._net = net
+        # the weights in the kernel's operand layout (ch_mlp_pack), re-packed whenever a weight or bias tensor
+        # was modified in place since (torch's per-tensor version counter): the forward reads this copy
+        n = L.lib().ch_mlp_packed_size(ctypes.byref(net))
+        self._packed = torch.empty(max(int(n), 4), dtype=torch.float32, device=self.device)
+        self._packed_at = None
+        net.packed = self._packed.data_ptr()
+
+    def _versions(self):
+        return tuple(w._version for w in self.weights)
+
+    def pack(self):
+        """Re-pack the weights now (on the current stream); forward() does it by itself after in-place updates."""
+        L.check(L.lib().ch_mlp_pack(ctypes.byref(self._net), ctypes.c_void_p(self._packed.data_ptr()), self._stream()))
+        self._packed_at = self._versions()
+
+    def _ensure_packed(self):
+        if self._packed_at != self._versions():
+            self.pack()
 
     # ---- constructors for the reference's models ------------------------------------------------
     @classmethod
@@ -140,6 +158,7 @@ class DevicePolicy:
         (uint8/bool [rows] device tensor): only the selected rows are computed and written
         (ch_mlp_forward_masked)."""
         torch = self.torch
+        self._ensure_packed()
         x = x.to(device=self.device, dtype=torch.float32).contiguous()
         rows = x.numel() // self.dims[0]
         if x.numel() != rows * self.dims[0]:
@@ -163,6 +182,7 @@ class DevicePolicy:
         """The forward on a HerdBatch's current observations (one row per env for CTDE, per agent for
         MARL), skipping the input columns past each env's NUM_DRONES."""
         torch = self.torch
+        self._ensure_packed()
         rows = batch.n_envs if batch.mode == L.CH_MODE_CTDE else batch.n_envs * batch.num_drones
         if out is None:
             out = torch.empty((rows, self.dims[-1]), dtype=torch.float32, device=self.device)

@@ -79,6 +79,9 @@ class DeviceRolloutBuffer:
         b, lib = self.batch, self._lib
         torch = b.torch
         log_std = log_std.to(device=b.device, dtype=torch.float32).contiguous()
+        for net in (actor, critic):
+            if net is not None:
+                net._ensure_packed()
         io = ChRolloutIO()
         io.step = ctypes.pointer(b._io)
         if critic is None:

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -710,6 +711,12 @@ int ch__obs_invalidate(ch_handle* h, void* stream) {
     return CH_OK;
 }
 
+// diagnostics: k_mlp2 writes wave 0's phase clocks of every workgroup to dev[blockIdx][16] (NULL: off)
+extern "C" int ch__set_mlp_tstamp(long long* dev) {
+    g_mlp_tstamp = dev;
+    return CH_OK;
+}
+
 int ch__set_phase_mask(ch_handle* h, int32_t mask) {
     if (!h) return CH_ERR_INVALID;
     h->phase_mask = mask;
@@ -733,6 +740,35 @@ static int mlp_args(const ch_mlp* net, const float* x, int64_t rows, float* y, M
     if (net->hidden_act < CH_ACT_NONE || net->hidden_act > CH_ACT_RELU) { err = "unknown activation"; return CH_ERR_INVALID; }
     a.hidden_act = net->hidden_act; a.clip = net->clip != 0; a.lo = net->lo; a.hi = net->hi;
     a.x = x; a.rows = rows; a.y = y; a.rows_per_env = 1;
+    a.kcap = net->dims[0];
+    // float4 weight loads need 16-B aligned rows of a multiple of 8 floats (k_mlp2 reads 8 per lane), inputs 4
+    for (int i = 0; i < net->n_layers; ++i)
+        if (net->dims[i] % 8 == 0 && (reinterpret_cast<uintptr_t>(net->weight[i]) & 15) == 0) a.vec_w |= 1 << i;
+    if (net->dims[0] % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) a.vec_w |= 1 << 7;
+    if (net->packed) {
+        if (reinterpret_cast<uintptr_t>(net->packed) & 15) { err = "packed weights must be 16-byte aligned"; return CH_ERR_INVALID; }
+        a.packed = net->packed;
+        mlp_packed_floats(a.layers, a.dims, a.pk_off, a.pk_pairs);
+    }
+    return CH_OK;
+}
+
+int64_t ch_mlp_packed_size(const ch_mlp* net) {
+    if (!net || net->n_layers < 1 || net->n_layers > 4) return -1;
+    for (int i = 0; i <= net->n_layers; ++i)
+        if (net->dims[i] < 1 || (i > 0 && net->dims[i] > 256)) return -1;
+    return mlp_packed_floats(net->n_layers, net->dims, nullptr, nullptr);
+}
+
+int ch_mlp_pack(const ch_mlp* net, float* dst, void* stream) {
+    MlpArgs a;
+    std::string err;
+    float one = 0.0f;
+    const int rc = mlp_args(net, &one, 0, &one, a, err);
+    if (rc) return fail(nullptr, rc, "ch_mlp_pack: " + err);
+    if (!dst || (reinterpret_cast<uintptr_t>(dst) & 15)) return fail(nullptr, CH_ERR_INVALID, "ch_mlp_pack: dst NULL or not 16-byte aligned");
+    const hipError_t e = launch_mlp_pack(a, dst, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(nullptr, CH_ERR_DEVICE, std::string("ch_mlp_pack launch: ") + hipGetErrorString(e));
     return CH_OK;
 }
 
@@ -760,20 +796,29 @@ int ch_mlp_forward_masked(const ch_mlp* net, const float* x, int64_t rows, const
     return CH_OK;
 }
 
-int ch_policy_forward(ch_handle* h, const ch_mlp* net, const float* obs, float* y, void* stream) {
-    if (!h) return fail(nullptr, CH_ERR_INVALID, "ch_policy_forward: NULL handle");
+// the forward of `net` on a handle's observation buffer: one row per env (CTDE) or agent (MARL), live widths from
+// NUM_DRONES (envi row 0)
+static int policy_args(ch_handle* h, const ch_mlp* net, const float* obs, float* y, MlpArgs& a, const char* who) {
     const bool marl = h->cfg.mode == CH_MODE_MARL;
     const int64_t rows = marl ? h->E * h->NC : h->E;
     const int want = marl ? 86 : h->rows * 86;
     if (net && net->dims[0] != want)
-        return fail(h, CH_ERR_INVALID, "ch_policy_forward: dims[0] must be " + std::to_string(want) + " for this handle");
-    MlpArgs a;
+        return fail(h, CH_ERR_INVALID, std::string(who) + ": dims[0] must be " + std::to_string(want) + " for this handle");
     std::string err;
     const int rc = mlp_args(net, obs, rows, y, a, err);
-    if (rc) return fail(h, rc, "ch_policy_forward: " + err);
+    if (rc) return fail(h, rc, std::string(who) + ": " + err);
     a.env_n = h->envi;   // envi row 0: NUM_DRONES of the episode each env is in
     a.rows_per_env = marl ? h->NC : 1;
     a.k_unit = 86;
+    a.kcap = std::min(a.dims[0], marl ? 86 : h->NC * 86);   // NUM_DRONES <= the constructor's drones
+    return CH_OK;
+}
+
+int ch_policy_forward(ch_handle* h, const ch_mlp* net, const float* obs, float* y, void* stream) {
+    if (!h) return fail(nullptr, CH_ERR_INVALID, "ch_policy_forward: NULL handle");
+    MlpArgs a;
+    const int rc = policy_args(h, net, obs, y, a, "ch_policy_forward");
+    if (rc) return rc;
     HIP_TRY(h, hipSetDevice(h->device));
     const hipError_t e = launch_mlp(a, (hipStream_t)stream);
     if (e != hipSuccess) return fail(h, CH_ERR_DEVICE, std::string("ch_policy_forward launch: ") + hipGetErrorString(e));
@@ -812,7 +857,7 @@ int ch_rollout_store(ch_handle* h, const ch_rollout* rb, int32_t t, const float*
     if ((reinterpret_cast<uintptr_t>(obs) | reinterpret_cast<uintptr_t>(rb->obs)) & 15)
         return fail(h, CH_ERR_INVALID, "ch_rollout_store: obs buffers must be 16-byte aligned");
     a.t = t; a.obs_now = obs; a.mean = mean; a.value = value; a.log_std = log_std; a.seed = seed;
-    a.env_actions = env_actions;
+    a.env_actions = env_actions; a.copy_obs = 1;
     HIP_TRY(h, hipSetDevice(h->device));
     HIP_TRY(h, launch_rollout(a, 0, (hipStream_t)stream));
     return CH_OK;
@@ -890,20 +935,51 @@ int ch_rollout_collect(ch_handle* h, const ch_rollout* rb, const ch_rollout_io* 
     a.terminal_value = bootstrap_truncated ? tval : nullptr; a.gamma = gamma;
     a.obs_now = sio->obs; a.mean = io->mean; a.value = value; a.log_std = log_std; a.seed = seed;
     a.env_actions = io->env_actions;
+    // The step writes its observations straight into the buffer's next slot (obs[t + 1]; the last step into the
+    // env's own obs buffer): the obs of step t > 0 is already in place when it is stored, and only obs[0] is copied
+    // (a v2 step into a buffer other than the one it wrote last writes every block in full, ch_step's obs_zero_ptr).
+    // The forwards that need the same step's outputs go out as one launch (launch_mlp_multi): after step t, the
+    // critic on the terminal observations of the envs that reset (V(terminal obs), the truncation bootstrap) and
+    // the actor and critic on obs[t + 1]; their workgroups share the CUs, so each forward's latencies hide behind
+    // the others' matrix work.
+    static const bool copy_each = [] { const char* v = getenv("CH_ROLLOUT_COPY"); return v && v[0] == '1'; }();
+    const size_t slot = (size_t)h->E * (size_t)ra.obs_dim;
+    auto obs_at = [&](int32_t t) { return (t == 0 || t == rb->n_steps || copy_each) ? sio->obs : rb->obs + (size_t)t * slot; };
+    MlpArgs fa, fc, ftv;
+    if ((rc = policy_args(h, actor, sio->obs, io->mean, fa, "ch_rollout_collect (actor)"))) return rc;
+    if (!fused && (rc = policy_args(h, critic, sio->obs, io->value, fc, "ch_rollout_collect (critic)"))) return rc;
+    {
+        // V(terminal obs) of the envs that just reset: the pre-reset blocks, zero past the constructor's drones
+        std::string err;
+        if ((rc = mlp_args(vnet, sio->terminal_obs, h->E, tv_out, ftv, err))) return fail(h, rc, "ch_rollout_collect: " + err);
+        ftv.row_mask = sio->reset_happened;
+        ftv.kcap = std::min(ftv.dims[0], h->NC * 86);
+    }
+    MlpArgs segs[3];
     HIP_TRY(h, hipSetDevice(h->device));
+    segs[0] = fa; segs[1] = fc;
+    HIP_TRY(h, launch_mlp_multi(segs, fused ? 1 : 2, st));
     for (int32_t t = 0; t < rb->n_steps; ++t) {
         // SB3 collect_rollouts, one step of every env: policy(obs) -> sample, log-prob, value -> env.step ->
         // bootstrap truncated rewards with V(terminal obs) -> buffer (OnPolicyAlgorithm.collect_rollouts)
-        if ((rc = ch_policy_forward(h, actor, sio->obs, io->mean, stream))) return rc;
-        if (!fused && (rc = ch_policy_forward(h, critic, sio->obs, io->value, stream))) return rc;
         a.t = t;
+        a.copy_obs = t == 0 || copy_each;
         HIP_TRY(h, launch_rollout(a, 0, st));
+        s.obs = (t + 1 < rb->n_steps && !copy_each) ? rb->obs + (size_t)(t + 1) * slot : sio->obs;
         if ((rc = ch_step(h, &s, stream))) return rc;
-        if (bootstrap_truncated &&
-            (rc = ch_mlp_forward_masked(vnet, sio->terminal_obs, h->E, sio->reset_happened, tv_out, stream)))
-            return fail(h, rc, "ch_rollout_collect: " + std::string(ch_last_error(nullptr)));
+        int n = 0;
+        if (bootstrap_truncated) segs[n++] = ftv;
+        if (t + 1 < rb->n_steps) {
+            fa.x = fc.x = obs_at(t + 1);
+            segs[n++] = fa;
+            if (!fused) segs[n++] = fc;
+        } else {   // the last observations' values: GAE's last_value
+            MlpArgs fv = fused ? fa : fc;
+            fv.x = obs_at(t + 1);
+            segs[n++] = fv;
+        }
+        HIP_TRY(h, launch_mlp_multi(segs, n, st));
     }
-    if ((rc = ch_policy_forward(h, vnet, sio->obs, fused ? io->mean : io->value, stream))) return rc;
     a.gamma_lambda = (float)((double)gamma * (double)gae_lambda);   // SB3: float32(self.gamma * self.gae_lambda)
     HIP_TRY(h, launch_rollout(a, 2, st));
     return CH_OK;

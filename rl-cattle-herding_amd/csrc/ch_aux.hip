@@ -75,19 +75,23 @@ __device__ __forceinline__ void rollout_post_env(const RolloutArgs& a, int t, lo
     a.last_episode_starts[e] = (te || tr) ? 1.0f : 0.0f;
 }
 
-// one workgroup per env: the observation row into the buffer, the Gaussian sample, its log-probability
-// (summed in action order by one lane), the clipped env action, value and episode start; with post_prev, the
-// previous step's post first (one launch per step less in ch_rollout_collect)
+// one wave per env (kRollThreads / 64 envs per workgroup): the observation row into the buffer (copy_obs), the
+// Gaussian sample of every action (lane k: action k, k + 64, ...), the summed log-probability (a wave tree
+// sum), the clipped env action, value and episode start; with post_prev, the previous step's post first (one
+// launch per step less in ch_rollout_collect)
 __global__ __launch_bounds__(kRollThreads) void k_rollout_store(RolloutArgs a) {
-    __shared__ float lp[kRollThreads];
-    const long long e = blockIdx.x;
-    const int tid = threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const long long e = (long long)blockIdx.x * (kRollThreads / 64) + (threadIdx.x >> 6);
+    if (e >= a.rows) return;
     const long long row = (long long)a.t * a.rows + e;
-    if (a.post_prev && a.t > 0 && tid == 0) rollout_post_env(a, a.t - 1, e);
-    const float4* src = reinterpret_cast<const float4*>(a.obs_now + e * a.obs_dim);
-    float4* dst = reinterpret_cast<float4*>(a.obs + row * a.obs_dim);
-    for (int k = tid; k < a.obs_dim / 4; k += kRollThreads) dst[k] = src[k];
-    for (int k = tid; k < a.act_dim; k += kRollThreads) {
+    if (a.post_prev && a.t > 0 && lane == 0) rollout_post_env(a, a.t - 1, e);
+    if (a.copy_obs) {
+        const float4* src = reinterpret_cast<const float4*>(a.obs_now + e * a.obs_dim);
+        float4* dst = reinterpret_cast<float4*>(a.obs + row * a.obs_dim);
+        for (int k = lane; k < a.obs_dim / 4; k += 64) dst[k] = src[k];
+    }
+    float lps = 0.0f;
+    for (int k = lane; k < a.act_dim; k += 64) {
         // standard normal from Philox4x32-10 (seed, step, env, action) by Box-Muller
         uint32_t c[4] = {(uint32_t)a.t, (uint32_t)k, (uint32_t)e, (uint32_t)(e >> 32)};
         philox_k(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
@@ -99,14 +103,13 @@ __global__ __launch_bounds__(kRollThreads) void k_rollout_store(RolloutArgs a) {
         a.actions[row * a.act_dim + k] = act;
         // torch.distributions.Normal.log_prob: -((x - mu)^2) / (2 var) - log(std) - log(sqrt(2 pi))
         const float d = act - mu, var = sd * sd;
-        lp[k] = -(d * d) / (2.0f * var) - ls - 0.91893853320467274f;
+        lps += -(d * d) / (2.0f * var) - ls - 0.91893853320467274f;
         if (k < a.env_act_dim) a.env_actions[e * a.env_act_dim + k] = fminf(fmaxf(act, -1.0f), 1.0f);
     }
-    __syncthreads();
-    if (tid == 0) {
-        float s = 0.0f;
-        for (int k = 0; k < a.act_dim; ++k) s += lp[k];
-        a.log_probs[row] = s;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) lps += __shfl_xor(lps, o);
+    if (lane == 0) {
+        a.log_probs[row] = lps;
         a.values[row] = a.value[e * a.value_ld];
         a.episode_starts[row] = a.last_episode_starts[e];
     }
@@ -139,7 +142,9 @@ __global__ void k_rollout_gae(RolloutArgs a) {
 }
 
 hipError_t launch_rollout(const RolloutArgs& a, int which, hipStream_t st) {
-    if (which == 0) hipLaunchKernelGGL(k_rollout_store, dim3((unsigned)a.rows), dim3(kRollThreads), 0, st, a);
+    if (which == 0)
+        hipLaunchKernelGGL(k_rollout_store, dim3((unsigned)((a.rows + kRollThreads / 64 - 1) / (kRollThreads / 64))),
+                           dim3(kRollThreads), 0, st, a);
     else if (which == 1) hipLaunchKernelGGL(k_rollout_post, dim3((unsigned)((a.rows + 255) / 256)), dim3(256), 0, st, a);
     else hipLaunchKernelGGL(k_rollout_gae, dim3((unsigned)((a.rows + 63) / 64)), dim3(64), 0, st, a);
     return hipGetLastError();

@@ -157,7 +157,25 @@ struct MlpArgs {
     const uint8_t* row_mask;   // optional: only rows with a non-zero byte are computed and written
     long long rows_per_env;    // 1: CTDE (live width n * k_unit); N: MARL (agent j live iff j < n)
     int k_unit;
+    int kcap;                  // widest live input row any tile can have (<= dims[0]): sizes k_mlp2's input tile
+    int vec_w;                 // bit i: layer i's weights are 16-B aligned rows (float4 loads); bit 7: so is x
+    long long* tstamp;         // diagnostics (ch__set_mlp_tstamp): k_mlp2 phase clocks [grid][16], or NULL
+    const float* packed;       // ch_mlp_pack layout of every layer (NULL: the raw nn.Linear weights)
+    long long pk_off[4];       // layer li's offset in `packed` (floats)
+    int pk_pairs[4];           // layer li's padded K pair count in `packed`
 };
+extern long long* g_mlp_tstamp;
+// floats of the packed layout of an MLP (per-layer offsets / pair counts out, optional)
+long long mlp_packed_floats(int layers, const int* dims, long long* off, int* pairs);
+hipError_t launch_mlp_pack(const MlpArgs& a, float* dst, hipStream_t st);
+// up to three independent forwards in one launch (ch_policy.hip k_mlp2)
+struct MlpMulti {
+    MlpArgs seg[3];
+    int nseg;
+    int start[4];              // first workgroup of each segment (start[nseg] = grid)
+    int lda, ldh;
+};
+hipError_t launch_mlp_multi(const MlpArgs* segs, int nseg, hipStream_t st);
 size_t mlp_lds_bytes();
 hipError_t launch_mlp(const MlpArgs& a, hipStream_t st);
 
@@ -172,6 +190,7 @@ struct RolloutArgs {
     int mean_ld, value_ld, tv_ld;   // row strides of mean / value / terminal_value (a fused actor-critic's output
                                     // holds both heads in one [rows][act_dim + 1] buffer)
     int post_prev;                  // store (t) / gae: first run step t - 1's (T - 1's) post (ch_rollout_collect)
+    int copy_obs;                   // store: copy obs_now into obs[t] (0: the step already wrote obs[t] there)
     long long rows;
     unsigned long long seed;
     float gamma, gamma_lambda;

@@ -4,23 +4,28 @@
 // one launch, f32 in / f32 out on the matrix cores.
 //
 // Layout: a workgroup owns 16 input rows (envs or agents) and carries them through every layer.
-// The 4 waves split each layer's output columns into 16x16 tiles (v_mfma_f32_16x16x4_f32: exact f32,
-// a k-ordered fma chain per output element).  The K dimension streams in chunks of 64 through LDS, from
-// a register ring that keeps the next 3 chunks of input and weight rows in flight (1 for 256-wide
-// layers) while the current one is multiplied.  Hidden activations stay in LDS between layers.  The grid is rows/16
-// workgroups: 4096 envs fill 256 CUs with one workgroup each.
+// The 8 waves split each layer's output columns into 16x16 tiles (v_mfma_f32_16x16x4_f32: exact f32,
+// a k-ordered fma chain per output element).  Hidden activations stay in LDS between layers.  The grid is
+// rows/16 workgroups: 4096 envs fill 256 CUs with one workgroup each.  Two kernels: k_mlp2 (the default,
+// further down) stages the input rows in LDS once and streams each wave's weight rows from global memory
+// straight into registers; k_mlp (the round-2 kernel, kept for first-layer widths past 1152 and for A/B with
+// CH_MLP_V1=1) streams K chunks of 64 of inputs and weights through LDS.
 //
 // Zero input columns.  An observation row has NUM_DRONES live rows of 86 features and zeros after
 // them (BaseRLAviary.py:272-342).  With per-row live widths the tile multiplies only the chunks below
 // its widest live row: the skipped products are 0 * w, which add +-0 to the sums.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdlib>
+#include <cstring>
 
 #include "ch_internal.h"
 
 namespace ch {
+
+long long* g_mlp_tstamp = nullptr;
 
 namespace {
 
@@ -242,14 +247,335 @@ __global__ __launch_bounds__(64 * NW) void k_mlp(MlpArgs a) {
     }
 }
 
+// ---- k_mlp2: weights streamed from global memory straight into the MFMA operand layout (the default) --------------
+//
+// k_mlp (above) staged every 64-wide K chunk of the weights through LDS between two barriers, with two chunks in
+// flight: 20 us for the 4096-row SB3 actor forward, 17 % of the f32 MFMA peak, the waves mostly waiting.  k_mlp2
+// keeps the 16-row tile and the 8 waves (each wave 16 or 32 of a layer's output columns), but
+//   * the input rows of the tile are staged in LDS once, whole (the live width only), with one barrier;
+//   * each wave loads its own weight columns straight from global memory (L2-resident: every workgroup reads the
+//     same matrix) into registers, and keeps D = 4 K-pairs of 32 in flight with no barrier inside a layer;
+//   * the next layer's first pairs are requested before this layer's epilogue, and the barriers order LDS only
+//     (a __syncthreads would wait for those loads).
+// K order.  Pair p of 32 columns is 8 MFMAs; in MFMA e lane group g = lane >> 4 supplies k = 32 p + 8 g + e
+// (A[row][k] from LDS, B[k][col] = W[col][k]).  Each output is the f32 fma chain over k in the order (p, e, g);
+// zero columns (dead observation rows, block-diagonal zeros) add +0 exactly, so the live-width skip and the fused
+// actor-critic stay bit-identical to the full-width and separate forwards.
+// Packed weights (ch_mlp.packed, ch_mlp_pack): layer li as [tile t][pair p][half h][lane l][4], element
+// W[16 t + (l & 15)][32 p + 8 (l >> 4) + 4 h + q] (zero past N and K): a wave's load of one half-pair is 1 KB
+// contiguous.  Raw nn.Linear weights: each lane reads two float4 of its own row, 16 rows per instruction.
+// Static load counts.  Every fetch issues the same loads whatever its pair index (raw: addresses clamped into
+// the row; the A side is zero past the live width, the layer width and the padded pair count, so a clamped weight
+// meets a zero), and the pair count is padded to a multiple of D: no load is conditional, so the compiler's vmcnt
+// waits count exactly the D - 1 younger pairs instead of draining every load in flight.
+
+constexpr int kD2 = 4;         // K pairs in flight per wave
+constexpr int kMaxPair0 = 36;  // first-layer live width <= 1152 (else k_mlp)
+constexpr int kLdsMax2 = 160 * 1024 - 1024;   // k_mlp2 dynamic LDS cap (the static kmax word included)
+
+template <int TW>
+struct Ring2 {
+    float4 v[kD2][TW][2];
+};
+
+__device__ __host__ __forceinline__ int pad_pairs(int k) { return ((k + 31) / 32 + kD2 - 1) / kD2 * kD2; }
+
+// the wave's weight source for one layer: per tile, the packed tile's lane base, or the raw row
+template <int TW>
+struct WSrc {
+    const float* w[TW];
+    int K;
+};
+
+// request pair p into ring slot S (S a literal: the ring stays in registers).  MODE 0: packed; 1: raw rows,
+// K % 8 == 0 and 16-B aligned (two float4 at min(k, K - 8)); 2: raw rows, element loads at min(k + q, K - 1)
+template <int S, int TW, int MODE>
+__device__ __forceinline__ void mlp2_fetch(Ring2<TW>& r, const WSrc<TW>& ws, int p, int g) {
+#pragma unroll
+    for (int j = 0; j < TW; ++j) {
+        if constexpr (MODE == 0) {
+            r.v[S][j][0] = *reinterpret_cast<const float4*>(ws.w[j] + p * 512);
+            r.v[S][j][1] = *reinterpret_cast<const float4*>(ws.w[j] + p * 512 + 256);
+        } else if constexpr (MODE == 1) {
+            const float* src = ws.w[j] + min(32 * p + 8 * g, ws.K - 8);
+            r.v[S][j][0] = *reinterpret_cast<const float4*>(src);
+            r.v[S][j][1] = *reinterpret_cast<const float4*>(src + 4);
+        } else {
+            const float* src = ws.w[j];
+            const int k = 32 * p + 8 * g, K = ws.K;
+            r.v[S][j][0] = make_float4(src[min(k, K - 1)], src[min(k + 1, K - 1)], src[min(k + 2, K - 1)], src[min(k + 3, K - 1)]);
+            r.v[S][j][1] = make_float4(src[min(k + 4, K - 1)], src[min(k + 5, K - 1)], src[min(k + 6, K - 1)], src[min(k + 7, K - 1)]);
+        }
+    }
+}
+
+__device__ __forceinline__ float f4_at(const float4& v, int i) {
+    return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
+}
+
+// pair p from ring slot S: the lane's 8 A values from LDS, 8 MFMAs per tile; then (FETCH) refill the slot with
+// pair p + D
+template <int S, int NT, int TW, int MODE, bool FETCH>
+__device__ __forceinline__ void mlp2_pair(f32x4 (&acc)[TW], Ring2<TW>& r, const WSrc<TW>& ws, const float* A, int lda,
+                                          int p, int lane) {
+    const int g = lane >> 4;
+    const float* ap = A + (lane & 15) * lda + 32 * p + 8 * g;
+    const float4 a0 = *reinterpret_cast<const float4*>(ap);
+    const float4 a1 = *reinterpret_cast<const float4*>(ap + 4);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const float av = f4_at(e < 4 ? a0 : a1, e & 3);
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, f4_at(r.v[S][j][e >> 2], e & 3), acc[j], 0, 0, 0);
+    }
+    if constexpr (FETCH) mlp2_fetch<S, TW, MODE>(r, ws, p + kD2, g);
+    // keep the refill here: left alone, the scheduler sinks all four refills below the group's last MFMAs, and
+    // the next group then waits for loads issued a moment earlier
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// npad (a multiple of D) pairs: the steady state refills every slot it drains, the last D pairs only drain
+template <int NT, int TW, int MODE>
+__device__ __forceinline__ void mlp2_loop(f32x4 (&acc)[TW], Ring2<TW>& r, const WSrc<TW>& ws, const float* A, int lda,
+                                          int npad, int lane) {
+    int p0 = 0;
+    for (; p0 < npad - kD2; p0 += kD2) {
+        mlp2_pair<0, NT, TW, MODE, true>(acc, r, ws, A, lda, p0 + 0, lane);
+        mlp2_pair<1, NT, TW, MODE, true>(acc, r, ws, A, lda, p0 + 1, lane);
+        mlp2_pair<2, NT, TW, MODE, true>(acc, r, ws, A, lda, p0 + 2, lane);
+        mlp2_pair<3, NT, TW, MODE, true>(acc, r, ws, A, lda, p0 + 3, lane);
+    }
+    mlp2_pair<0, NT, TW, MODE, false>(acc, r, ws, A, lda, p0 + 0, lane);
+    mlp2_pair<1, NT, TW, MODE, false>(acc, r, ws, A, lda, p0 + 1, lane);
+    mlp2_pair<2, NT, TW, MODE, false>(acc, r, ws, A, lda, p0 + 2, lane);
+    mlp2_pair<3, NT, TW, MODE, false>(acc, r, ws, A, lda, p0 + 3, lane);
+}
+
+template <int TW>
+__device__ __forceinline__ int layer_mode(const MlpArgs& a, int li) {
+    return a.packed ? 0 : (((a.vec_w >> li) & 1) ? 1 : 2);
+}
+
+// the wave's weight source for layer li (tiles past the layer width clamped to its last tile / row: computed,
+// never stored) and the loads of its first D pairs
+template <int NW, int TW>
+__device__ __forceinline__ void mlp2_prologue(const MlpArgs& a, int li, Ring2<TW>& r, WSrc<TW>& ws, int wave, int lane) {
+    const int N = a.dims[li + 1], K = a.dims[li], nt = (N + 15) >> 4;
+    const int mode = layer_mode<TW>(a, li);
+    ws.K = K;
+#pragma unroll
+    for (int j = 0; j < TW; ++j) {
+        const int t = min(wave + NW * j, nt - 1);
+        ws.w[j] = mode == 0 ? a.packed + a.pk_off[li] + (long long)t * a.pk_pairs[li] * 512 + lane * 4
+                            : a.w[li] + (long long)min(t * 16 + (lane & 15), N - 1) * K;
+    }
+    const int g = lane >> 4;
+#define CH_MLP2_PRO(M)                                                                                              \
+    mlp2_fetch<0, TW, M>(r, ws, 0, g); mlp2_fetch<1, TW, M>(r, ws, 1, g);                                            \
+    mlp2_fetch<2, TW, M>(r, ws, 2, g); mlp2_fetch<3, TW, M>(r, ws, 3, g)
+    if (mode == 0) { CH_MLP2_PRO(0); } else if (mode == 1) { CH_MLP2_PRO(1); } else { CH_MLP2_PRO(2); }
+#undef CH_MLP2_PRO
+}
+
+// a workgroup barrier ordering LDS only: the weight loads in flight stay in flight (__syncthreads' release fence
+// would wait for every outstanding global load)
+__device__ __forceinline__ void mlp2_lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// NW waves of TW 16-column tiles each (<4, 2>: layers <= 128 wide, one wave per SIMD with two independent
+// accumulator chains; <8, 2>: <= 256 wide).  lda / ldh: LDS row strides (floats) of the staged input rows and of
+// the hidden activations, both = 4 mod 64 (conflict-free 16-B operand reads), wide enough for the padded pair
+// counts.
+template <int NW, int TW>
+__device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int lda, int ldh) {
+    extern __shared__ __align__(16) float sm[];
+    float* xa = sm;                    // [16][lda]
+    float* hb0 = xa + kTM * lda;       // [16][ldh]
+    float* hb1 = hb0 + kTM * ldh;
+    __shared__ int kmax;
+    constexpr int kT = 64 * NW;        // threads
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const long long row0 = blk * kTM;
+    if (tid == 0) kmax = 0;
+    __syncthreads();
+    if (tid < kTM && row0 + tid < a.rows) {
+        int k = a.dims[0];
+        if (a.env_n) {
+            const long long r = row0 + tid, e = r / a.rows_per_env;
+            const int j = (int)(r - e * a.rows_per_env), n = a.env_n[e];
+            k = a.rows_per_env == 1 ? n * a.k_unit : (j < n ? a.k_unit : 0);
+            k = min(k, a.dims[0]);
+        }
+        atomicMax(&kmax, k);
+    }
+    const bool any = __syncthreads_or(a.row_mask && tid < kTM && row0 + tid < a.rows && a.row_mask[row0 + tid] != 0);
+    if (a.row_mask && !any) return;
+    const int kloop = min(kmax, a.kcap);   // (the host sized the tile for kcap)
+    const int np0 = min(pad_pairs(max(kloop, 1)), kMaxPair0);
+    long long* ts = a.tstamp && tid == 0 ? a.tstamp + blk * 16 : nullptr;
+    if (ts) ts[0] = clock64();
+
+    // the first layer's first weight pairs (L2 hits), then the tile's input rows (from HBM): thread t owns row
+    // t / (4 NW) and float4 columns t % (4 NW) + 4 NW i, i < nld, of the padded width 32 np0
+    Ring2<TW> ring;
+    WSrc<TW> ws;
+    mlp2_prologue<NW, TW>(a, 0, ring, ws, wave, lane);
+    if (ts) ts[1] = clock64();
+    constexpr int kTPR = 4 * NW, kQ = 8 * kMaxPair0 / kTPR;
+    const int K0 = a.dims[0], srow = tid / kTPR, sc = 4 * (tid % kTPR), nld = (8 * np0 + kTPR - 1) / kTPR;
+    const bool srv = row0 + srow < a.rows;
+    const float* xs = a.x + min(row0 + srow, a.rows - 1) * K0;
+    float4 xr[kQ];
+    if ((a.vec_w >> 7) & 1) {
+#pragma unroll
+        for (int i = 0; i < kQ; ++i)
+            if (i < nld) xr[i] = *reinterpret_cast<const float4*>(xs + min(sc + 4 * kTPR * i, K0 - 4));
+    } else {
+#pragma unroll
+        for (int i = 0; i < kQ; ++i) {
+            const int c = sc + 4 * kTPR * i;
+            if (i < nld)
+                xr[i] = make_float4(xs[min(c, K0 - 1)], xs[min(c + 1, K0 - 1)], xs[min(c + 2, K0 - 1)], xs[min(c + 3, K0 - 1)]);
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);   // every load above issued before the first wait
+    if (ts) ts[2] = clock64();
+#pragma unroll
+    for (int i = 0; i < kQ; ++i) {
+        const int c = sc + 4 * kTPR * i;
+        if (i < nld && c < 32 * np0) {
+            float4 v = xr[i];
+            v.x = srv && c < kloop ? v.x : 0.0f;
+            v.y = srv && c + 1 < kloop ? v.y : 0.0f;
+            v.z = srv && c + 2 < kloop ? v.z : 0.0f;
+            v.w = srv && c + 3 < kloop ? v.w : 0.0f;
+            *reinterpret_cast<float4*>(xa + srow * lda + c) = v;
+        }
+    }
+    if (ts) ts[3] = clock64();
+    mlp2_lds_barrier();
+    if (ts) ts[4] = clock64();
+
+    const float* cur = xa;
+    int ldc = lda;
+    int npad = np0;
+    for (int li = 0; li < a.layers; ++li) {
+        const bool last = li == a.layers - 1;
+        const int N = a.dims[li + 1];
+        const int mode = layer_mode<TW>(a, li);
+        const int nt = (N + 15) >> 4;
+        const int ntw = (wave < nt) + (TW > 1 && wave + NW < nt);   // this wave's tiles (wave-uniform)
+        float bcol[TW];
+#pragma unroll
+        for (int j = 0; j < TW; ++j) {
+            const int col = (wave + NW * j) * 16 + (lane & 15);
+            bcol[j] = a.b[li] && col < N ? a.b[li][col] : 0.0f;
+        }
+        f32x4 acc[TW];
+#pragma unroll
+        for (int j = 0; j < TW; ++j) acc[j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#define CH_MLP2_LOOP(NT_)                                                                                           \
+        if (mode == 0) mlp2_loop<NT_, TW, 0>(acc, ring, ws, cur, ldc, npad, lane);                                   \
+        else if (mode == 1) mlp2_loop<NT_, TW, 1>(acc, ring, ws, cur, ldc, npad, lane);                              \
+        else mlp2_loop<NT_, TW, 2>(acc, ring, ws, cur, ldc, npad, lane)
+        if (ntw == TW) { CH_MLP2_LOOP(TW); } else if (ntw > 0) { CH_MLP2_LOOP(1); }
+#undef CH_MLP2_LOOP
+        if (ts && li < 3) ts[5 + 2 * li] = clock64();
+        // the next layer's first pairs, in flight during this epilogue and barrier
+        const int npn = last ? 0 : pad_pairs(N);
+        if (!last) mlp2_prologue<NW, TW>(a, li + 1, ring, ws, wave, lane);
+        float* out = li & 1 ? hb1 : hb0;
+        // epilogue: C/D map col = lane & 15, row = 4 (lane >> 4) + r
+#pragma unroll
+        for (int j = 0; j < TW; ++j) {
+            if (j >= ntw) continue;
+            const int col = (wave + NW * j) * 16 + (lane & 15);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = (lane >> 4) * 4 + r;
+                float v = acc[j][r] + bcol[j];
+                if (!last) {
+                    if (col < N) out[row * ldh + col] = act_fn(v, a.hidden_act);
+                } else if (col < N && row0 + row < a.rows && (!a.row_mask || a.row_mask[row0 + row])) {
+                    if (a.clip) v = fminf(fmaxf(v, a.lo), a.hi);
+                    a.y[(row0 + row) * (long long)N + col] = v;
+                }
+            }
+        }
+        if (last) break;
+        // columns [N, 32 npn) of the activations: zero for the next layer's padded pairs
+        const int zc = 32 * npn - N;
+        for (int idx = tid; idx < kTM * zc; idx += kT) {
+            const int r = idx / zc;
+            out[r * ldh + N + idx - r * zc] = 0.0f;
+        }
+        mlp2_lds_barrier();
+        if (ts && li < 2) ts[6 + 2 * li] = clock64();
+        cur = out;
+        ldc = ldh;
+        npad = npn;
+    }
+    if (ts) ts[10] = clock64();
+}
+
+// up to three independent forwards in one launch (MlpMulti): workgroups [start[s], start[s + 1]) run segment s.
+// Their workgroups share the CUs (two <4, 2> workgroups fit one CU), so one forward's load latencies overlap the
+// other's matrix work -- the rollout's actor, critic and terminal-value critic in one launch.
+template <int NW, int TW>
+__global__ __launch_bounds__(64 * NW, NW == 8 && TW == 1 ? 4 : 1) void k_mlp2(MlpMulti m) {
+    int sg = 0;
+    if (m.nseg > 1 && (int)blockIdx.x >= m.start[1]) sg = 1;
+    if (m.nseg > 2 && (int)blockIdx.x >= m.start[2]) sg = 2;
+    mlp2_body<NW, TW>(m.seg[sg], (long long)blockIdx.x - m.start[sg], m.lda, m.ldh);
+}
+
+// ch_mlp_pack: layer li's weights into the [tile][pair][half][lane][4] layout (zero past N and K)
+__global__ void k_mlp_pack(const float* __restrict__ W, int N, int K, int P, float* __restrict__ out, long long total) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+        const int q = (int)(i & 3), l = (int)((i >> 2) & 63), h = (int)((i >> 8) & 1);
+        const long long tp = i >> 9;
+        const int p = (int)(tp % P), t = (int)(tp / P);
+        const int n = 16 * t + (l & 15), k = 32 * p + 8 * (l >> 4) + 4 * h + q;
+        out[i] = n < N && k < K ? W[(long long)n * K + k] : 0.0f;
+    }
+}
+
 }  // namespace
 
 size_t mlp_lds_bytes() { return sizeof(float) * (kTM * kKS + kWMax * kKS + 2 * kTM * (kWMax + 4)); }
 
-hipError_t launch_mlp(const MlpArgs& a, hipStream_t st) {
+long long mlp_packed_floats(int layers, const int* dims, long long* off, int* pairs) {
+    long long total = 0;
+    for (int li = 0; li < layers; ++li) {
+        const int P = pad_pairs(dims[li]), nt = (dims[li + 1] + 15) / 16;
+        if (off) off[li] = total;
+        if (pairs) pairs[li] = P;
+        total += (long long)nt * P * 512;
+    }
+    return total;
+}
+
+hipError_t launch_mlp_pack(const MlpArgs& a, float* dst, hipStream_t st) {
+    long long off[4];
+    int pairs[4];
+    mlp_packed_floats(a.layers, a.dims, off, pairs);
+    for (int li = 0; li < a.layers; ++li) {
+        const long long n = (long long)((a.dims[li + 1] + 15) / 16) * pairs[li] * 512;
+        const int blocks = (int)std::min<long long>((n + 255) / 256, 4096);
+        hipLaunchKernelGGL(k_mlp_pack, dim3(blocks), dim3(256), 0, st, a.w[li], a.dims[li + 1], a.dims[li], pairs[li],
+                           dst + off[li], n);
+    }
+    return hipGetLastError();
+}
+
+static hipError_t mlp_attrs() {
     // the dynamic-LDS opt-in, once per device (the attribute is per device context)
     static std::atomic<unsigned long long> attr_set{0};
-    static const bool wide4 = [] { const char* v = getenv("CH_MLP_WIDE4"); return v && v[0] == '1'; }();
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
@@ -260,16 +586,77 @@ hipError_t launch_mlp(const MlpArgs& a, hipStream_t st) {
             e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp_lds_bytes());
             if (e != hipSuccess) return e;
         }
+        for (const void* f : {reinterpret_cast<const void*>(&k_mlp2<4, 2>), reinterpret_cast<const void*>(&k_mlp2<8, 2>),
+                              reinterpret_cast<const void*>(&k_mlp2<8, 1>)}) {
+            e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax2);
+            if (e != hipSuccess) return e;
+        }
         attr_set.fetch_or(bit, std::memory_order_relaxed);
     }
-    const long long grid = (a.rows + kTM - 1) / kTM;
-    if (grid == 0) return hipSuccess;
-    int maxw = 0;
-    for (int i = 1; i <= a.layers; ++i) maxw = a.dims[i] > maxw ? a.dims[i] : maxw;
-    if (maxw <= 128) hipLaunchKernelGGL((k_mlp<8, 1, 2>), dim3((unsigned)grid), dim3(512), mlp_lds_bytes(), st, a);
-    else if (wide4) hipLaunchKernelGGL((k_mlp<4, 4, 1>), dim3((unsigned)grid), dim3(256), mlp_lds_bytes(), st, a);
-    else hipLaunchKernelGGL((k_mlp<8, 2, 2>), dim3((unsigned)grid), dim3(512), mlp_lds_bytes(), st, a);
-    return hipGetLastError();
+    return hipSuccess;
 }
+
+// k_mlp2's shape for one net: widest layer, LDS strides (the live input width rounded to whole K pairs, rows
+// padded to 4 mod 64 floats); false when the net does not fit it (then k_mlp)
+static bool mlp2_shape(const MlpArgs& a, int& maxw, int& lda, int& ldh) {
+    int maxhid = 32;
+    maxw = 0;
+    for (int i = 1; i <= a.layers; ++i) {
+        maxw = a.dims[i] > maxw ? a.dims[i] : maxw;
+        if (i < a.layers) maxhid = a.dims[i] > maxhid ? a.dims[i] : maxhid;
+    }
+    const int np0 = pad_pairs(std::max(a.kcap, 1));
+    lda = (32 * np0 + 63) / 64 * 64 + 4;
+    ldh = (std::max(maxhid, 32 * kD2) + 32 * kD2 - 1) / (32 * kD2) * (32 * kD2) + 4;
+    return np0 <= kMaxPair0 && sizeof(float) * (size_t)kTM * (lda + 2 * ldh) <= (size_t)kLdsMax2;
+}
+
+hipError_t launch_mlp_multi(const MlpArgs* segs, int nseg, hipStream_t st) {
+    static const bool v1 = [] { const char* v = getenv("CH_MLP_V1"); return v && v[0] == '1'; }();
+    static const bool nw4 = [] { const char* v = getenv("CH_MLP2_NW4"); return v && v[0] == '1'; }();   // A/B
+    static const bool wide4 = [] { const char* v = getenv("CH_MLP_WIDE4"); return v && v[0] == '1'; }();
+    if (nseg < 1 || nseg > 3) return hipErrorInvalidValue;
+    hipError_t e = mlp_attrs();
+    if (e != hipSuccess) return e;
+    MlpMulti m;
+    std::memset(&m, 0, sizeof(m));
+    int maxw = 0, fits = !v1, grid = 0, n = 0;
+    for (int s = 0; s < nseg; ++s) {
+        const long long g = (segs[s].rows + kTM - 1) / kTM;
+        if (g == 0) continue;
+        int w, la, lh;
+        fits &= mlp2_shape(segs[s], w, la, lh);
+        maxw = std::max(maxw, w); m.lda = std::max(m.lda, la); m.ldh = std::max(m.ldh, lh);
+        m.seg[n] = segs[s];
+        m.seg[n].tstamp = g_mlp_tstamp;
+        m.start[n] = grid;
+        grid += (int)g;
+        ++n;
+    }
+    if (n == 0) return hipSuccess;
+    m.nseg = n;
+    m.start[n] = grid;
+    const size_t lds2 = sizeof(float) * (size_t)kTM * (m.lda + 2 * m.ldh);
+    if (fits && lds2 <= (size_t)kLdsMax2) {
+        if (maxw > 128) hipLaunchKernelGGL((k_mlp2<8, 2>), dim3((unsigned)grid), dim3(512), lds2, st, m);
+        else if (nw4) hipLaunchKernelGGL((k_mlp2<4, 2>), dim3((unsigned)grid), dim3(256), lds2, st, m);
+        else hipLaunchKernelGGL((k_mlp2<8, 1>), dim3((unsigned)grid), dim3(512), lds2, st, m);
+        return hipGetLastError();
+    }
+    // the round-2 kernel, one launch per net
+    for (int s = 0; s < n; ++s) {
+        const MlpArgs& a = m.seg[s];
+        const unsigned g = (unsigned)((a.rows + kTM - 1) / kTM);
+        int w = 0;
+        for (int i = 1; i <= a.layers; ++i) w = std::max(w, a.dims[i]);
+        if (w <= 128) hipLaunchKernelGGL((k_mlp<8, 1, 2>), dim3(g), dim3(512), mlp_lds_bytes(), st, a);
+        else if (wide4) hipLaunchKernelGGL((k_mlp<4, 4, 1>), dim3(g), dim3(256), mlp_lds_bytes(), st, a);
+        else hipLaunchKernelGGL((k_mlp<8, 2, 2>), dim3(g), dim3(512), mlp_lds_bytes(), st, a);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_mlp(const MlpArgs& a, hipStream_t st) { return launch_mlp_multi(&a, 1, st); }
 
 }  // namespace ch

@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _header_symbols():
     src = open(os.path.join(ROOT, "include", "cattleherd.h")).read()
-    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(ch_\w+)\(", src, re.M)))
+    return sorted(set(re.findall(r"^(?:int|int64_t|const char\*)\s+(ch_\w+)\(", src, re.M)))
 
 
 def test_library_exports_header_symbols():
@@ -88,3 +88,19 @@ def test_physics_field_default_and_range():
         c.physics = bad
         assert L.ch_create(ctypes.byref(c), 8, 0, ctypes.byref(h)) == _lib.CH_ERR_INVALID
         assert b"physics" in L.ch_last_error(None)
+
+
+def test_mlp_packed_size_is_the_operand_layout():
+    """ch_mlp_packed_size (host only): per layer ceil(N / 16) tiles x K pairs of 32 padded to a multiple of 4 x
+    512 floats (two halves of 64 lanes x 4); invalid nets report -1."""
+    from cattleherd import _lib
+    L = _lib.lib()
+    net = _lib.ChMlp()
+    net.n_layers = 3
+    for i, d in enumerate((1032, 128, 128, 48)):
+        net.dims[i] = d
+    pairs = lambda k: (((k + 31) // 32) + 3) // 4 * 4  # noqa: E731
+    want = 8 * pairs(1032) * 512 + 8 * pairs(128) * 512 + 3 * pairs(128) * 512
+    assert L.ch_mlp_packed_size(ctypes.byref(net)) == want
+    net.dims[1] = 300
+    assert L.ch_mlp_packed_size(ctypes.byref(net)) == -1

@@ -86,8 +86,11 @@ def test_rollout_buffer_matches_sb3_semantics(E, n, m, compat, level):
     assert np.allclose(rb.rewards.cpu().numpy(), rew, rtol=1e-5, atol=1e-5)   # V(terminal) MFMA vs torch
     assert np.array_equal(es[1:], dn[:-1].astype(np.float32))
     assert dn.any() and np.array(tl).any()
-    # 4. GAE bit for bit against the float32 recursion
-    last_v = critic.reference(b2.obs.view(E, -1))[:, 0].cpu().numpy()
+    # 4. GAE bit for bit against the float32 recursion, from the device's V(last obs) (itself held to torch
+    # at the values' tolerance: the MFMA and torch sum the 1032 products in different orders)
+    last_v_ref = critic.reference(b2.obs.view(E, -1))[:, 0]
+    assert torch.allclose(rb.value[:, 0], last_v_ref, rtol=1e-5, atol=1e-5)
+    last_v = rb.value[:, 0].cpu().numpy()
     adv, ret = _gae_numpy(rb.rewards.cpu().numpy(), rb.values.cpu().numpy(), es, last_v, dn[-1],
                           0.99, 0.95)
     assert np.allclose(rb.advantages.cpu().numpy(), adv, rtol=2e-6, atol=2e-6)

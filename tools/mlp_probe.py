@@ -33,6 +33,8 @@ def timed(fn, k=200):
 
 
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "trace":
+        return trace()
     a = actor()
     if len(sys.argv) > 1 and sys.argv[1] == "sweep":
         for rows in (16, 256, 1024, 4096, 16384, 65536):
@@ -45,6 +47,39 @@ def main():
     b.reset()
     y = torch.empty(4096, 48, device=b.device)
     print(f"batch forward (live width 344): {timed(lambda: a.forward_batch(b, y), reps):.2f} us", flush=True)
+
+
+def trace():
+    """k_mlp2 phase clocks (ch__set_mlp_tstamp): wave 0 of every workgroup, cycles from its start."""
+    import ctypes
+    from cattleherd import _lib
+    a = actor()
+    b = HerdBatch(4096, 4, 16)
+    b.reset()
+    y = torch.empty(4096, 48, device=b.device)
+    ts = torch.zeros(256 * 16, dtype=torch.int64, device=b.device)
+    lib = _lib.lib()
+    lib.ch__set_mlp_tstamp.argtypes = [ctypes.c_void_p]
+    for _ in range(20):
+        a.forward_batch(b, y)
+    for rep in range(4):
+        packed = rep % 2 == 0
+        a._net.packed = a._packed.data_ptr() if packed else None
+        lib.ch__set_mlp_tstamp(ctypes.c_void_p(ts.data_ptr()))
+        a.forward_batch(b, y)
+        torch.cuda.synchronize()
+        t = ts.view(256, 16).cpu().numpy().astype(np.float64)[:, :11]
+        d = t - t[:, :1]
+        names = ["start", "x issued", "w issued", "x stored", "staged", "L0 loop", "L0 done", "L1 loop", "L1 done",
+                 "L2 loop", "end"]
+        print("rep", rep, "packed" if packed else "raw", " ".join(f"{nm} {np.mean(d[:, i]):.0f}/{np.max(d[:, i]):.0f}" for i, nm in enumerate(names)),
+              flush=True)
+    lib.ch__set_mlp_tstamp(None)
+    for packed in (True, False):
+        a._net.packed = a._packed.data_ptr() if packed else None
+        print(f"forward (timed, {'packed' if packed else 'raw'} weights): {timed(lambda: a.forward_batch(b, y)):.2f} us",
+              flush=True)
+    a._net.packed = a._packed.data_ptr()
 
 
 if __name__ == "__main__":
