@@ -214,6 +214,11 @@ typedef struct ch_mlp {
     float lo, hi;
     const float* packed;       /* NULL, or the same weights in the MFMA operand layout written by ch_mlp_pack
                                   (read instead of `weight`; re-pack after every weight update) */
+    int32_t split_out[4];      /* block-diagonal layer i (i >= 1; 0 = dense): outputs [0, split_out) read only */
+    int32_t split_in[4];       /* inputs [0, split_in), outputs [split_out, N) only [split_in, K) -- the weights
+                                  outside the two blocks are zero and are not multiplied (e.g. SB3's actor and
+                                  critic packed as one net).  Used when split_in % 128 == 0 and split_out % 32 == 0,
+                                  else the layer runs dense (same result). */
 } ch_mlp;
 
 /* The operand layout of the forward kernel: per layer [16-column tile][32-wide K pair][half][lane][4], so that

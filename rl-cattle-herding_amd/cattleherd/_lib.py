@@ -51,7 +51,8 @@ class ChStepIO(ctypes.Structure):
 class ChMlp(ctypes.Structure):
     _fields_ = [("n_layers", ctypes.c_int32), ("dims", ctypes.c_int32 * 5), ("weight", ctypes.c_void_p * 4),
                 ("bias", ctypes.c_void_p * 4), ("hidden_act", ctypes.c_int32), ("clip", ctypes.c_int32),
-                ("lo", ctypes.c_float), ("hi", ctypes.c_float), ("packed", ctypes.c_void_p)]
+                ("lo", ctypes.c_float), ("hi", ctypes.c_float), ("packed", ctypes.c_void_p),
+                ("split_out", ctypes.c_int32 * 4), ("split_in", ctypes.c_int32 * 4)]
 
 
 class ChError(RuntimeError):

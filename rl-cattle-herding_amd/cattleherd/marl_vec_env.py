@@ -85,19 +85,21 @@ class CattleHerdMultiAgentVecEnv:
         start), ``terminated``, ``truncated`` [E, N] bool, ``agents_before`` [E, N] (the wrapper's agents the
         step started with: its dicts carry these keys), ``agents`` [E, N] (the next step's: the survivors, or
         the new episode's where the env was reset) and ``all_done`` [E] (``"__all__"``: every agent
-        terminated; those envs are reset in the same launch, their new observations in ``self.batch.obs``)."""
+        terminated; those envs are reset in the same launch, their new observations in ``self.batch.obs``).
+        ``reward``, ``terminated``, ``truncated`` and ``all_done`` are views of the batch's output buffers: valid
+        until the next step."""
         b = self.batch
         torch = b.torch
         if self._before is None:
             raise RuntimeError("call reset() first")
         before = self._before
         b.step(actions, autoreset=True, terminal_obs=True)
-        reset = b.reset_happened.bool()
-        after = b.agent_active.bool()
-        self._before = after.clone()
+        # the uint8 flag buffers reinterpreted as bool (no copy); agent_active is rewritten by the next step
+        reset = b.reset_happened.view(torch.bool)
+        self._before = b.agent_active.view(torch.bool).clone()
         return {"obs": torch.where(reset[:, None, None], b.terminal_obs, b.obs), "reward": b.reward,
-                "terminated": b.terminated.bool(), "truncated": b.truncated.bool(), "agents_before": before,
-                "agents": self._before, "all_done": reset}
+                "terminated": b.terminated.view(torch.bool), "truncated": b.truncated.view(torch.bool),
+                "agents_before": before, "agents": self._before, "all_done": reset}
 
     def step(self, action_dicts):
         """RLlibMultiAgentWrapper.step (marl_wrapper.py:77-119) for every env: ``action_dicts`` is a list of

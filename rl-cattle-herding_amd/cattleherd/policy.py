@@ -32,7 +32,7 @@ class DevicePolicy:
     ``layers``: list of (weight [out, in], bias [out] or None) tensors in ``nn.Linear`` layout;
     ``hidden_act`` after every layer but the last; ``clip`` = (lo, hi) or None on the output."""
 
-    def __init__(self, layers, hidden_act="tanh", clip=None, device=None):
+    def __init__(self, layers, hidden_act="tanh", clip=None, device=None, splits=None):
         import torch
         if not torch.cuda.is_available():
             raise RuntimeError("DevicePolicy needs a ROCm GPU; there is no CPU fallback")
@@ -62,6 +62,10 @@ class DevicePolicy:
         net.hidden_act = _ACTS[hidden_act]
         net.clip = 1 if clip is not None else 0
         net.lo, net.hi = (clip if clip is not None else (0.0, 0.0))
+        # block-diagonal layers {layer: (split_out, split_in)}: the kernel skips the zero blocks (ch_mlp.split_*)
+        for i, (so, si) in (splits or {}).items():
+            net.split_out[i], net.split_in[i] = int(so), int(si)
+        self.splits = dict(splits or {})
         self._net = net
         # the weights in the kernel's operand layout (ch_mlp_pack), re-packed whenever a weight or bias tensor
         # was modified in place since (torch's per-tensor version counter): the forward reads this copy
@@ -117,7 +121,8 @@ class DevicePolicy:
         layers = [(torch.cat([aw[0], cw[0]], 0), torch.cat([ab[0], cb[0]], 0))]
         for i in (1, 2):
             layers.append((torch.block_diag(aw[i], cw[i]), torch.cat([ab[i], cb[i]], 0)))
-        net = cls(layers, "tanh", None, device)
+        splits = {i: (int(aw[i].shape[0]), int(aw[i].shape[1])) for i in (1, 2)}
+        net = cls(layers, "tanh", None, device, splits=splits)
         net.heads = (int(aw[2].shape[0]), int(cw[2].shape[0]))
         return net
 
@@ -132,7 +137,8 @@ class DevicePolicy:
             w = torch.cat([aw, cw], 0) if i == 0 else torch.block_diag(aw, cw)
             z = lambda w_, b_: b_ if b_ is not None else torch.zeros(w_.shape[0], device=w_.device)  # noqa: E731
             layers.append((w, torch.cat([z(aw, ab), z(cw, cb)], 0)))
-        net = cls(layers, actor.hidden_act, None, actor.device)
+        splits = {i: (int(actor.weights[i].shape[0]), int(actor.weights[i].shape[1])) for i in range(1, len(layers))}
+        net = cls(layers, actor.hidden_act, None, actor.device, splits=splits)
         net.heads = (actor.dims[-1], critic.dims[-1])
         return net
 

@@ -66,6 +66,13 @@ struct ch_handle {
     double* rdv = nullptr;
     double* mdev = nullptr;     // device [CH_METRIC_COUNT + 1]: reduced metrics + error word
     double* mhost = nullptr;    // pinned host copy of mdev
+    // ch_rollout_collect's deferred-bootstrap queue (allocated on first use): terminal observations, their rewards
+    // rows, the count, the values
+    float* tv_obs = nullptr;
+    long long* tv_row = nullptr;
+    int* tv_count = nullptr;
+    float* tv_val = nullptr;
+    size_t tv_obs_n = 0, tv_val_n = 0;
     std::string err;
 };
 
@@ -236,6 +243,8 @@ static void free_all(ch_handle* h) {
     void* ptrs[] = {h->drone, h->rpy, h->cattle, h->phys, h->envr, h->envi, h->metrics, h->spawn, h->pairs,
                     h->errw, h->mdev, h->stale, h->obs_tag, h->evald, h->rdn, h->rdv, h->pos64, h->cpos64, h->prev64};
     for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    for (void* p : {(void*)h->tv_obs, (void*)h->tv_row, (void*)h->tv_count, (void*)h->tv_val})
         if (p) (void)hipFree(p);
     if (h->mhost) (void)hipHostFree(h->mhost);
 }
@@ -745,6 +754,13 @@ static int mlp_args(const ch_mlp* net, const float* x, int64_t rows, float* y, M
     for (int i = 0; i < net->n_layers; ++i)
         if (net->dims[i] % 8 == 0 && (reinterpret_cast<uintptr_t>(net->weight[i]) & 15) == 0) a.vec_w |= 1 << i;
     if (net->dims[0] % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) a.vec_w |= 1 << 7;
+    // block-diagonal layers the kernel can skip by whole K-pair groups (ch_mlp.split_*); others run dense
+    for (int i = 1; i < net->n_layers; ++i) {
+        const int so = net->split_out[i], si = net->split_in[i];
+        if (so > 0 && so < net->dims[i + 1] && so % 32 == 0 && si > 0 && si < net->dims[i] && si % 128 == 0) {
+            a.split_out[i] = so; a.split_in[i] = si;
+        }
+    }
     if (net->packed) {
         if (reinterpret_cast<uintptr_t>(net->packed) & 15) { err = "packed weights must be 16-byte aligned"; return CH_ERR_INVALID; }
         a.packed = net->packed;
@@ -938,25 +954,59 @@ int ch_rollout_collect(ch_handle* h, const ch_rollout* rb, const ch_rollout_io* 
     // The step writes its observations straight into the buffer's next slot (obs[t + 1]; the last step into the
     // env's own obs buffer): the obs of step t > 0 is already in place when it is stored, and only obs[0] is copied
     // (a v2 step into a buffer other than the one it wrote last writes every block in full, ch_step's obs_zero_ptr).
-    // The forwards that need the same step's outputs go out as one launch (launch_mlp_multi): after step t, the
-    // critic on the terminal observations of the envs that reset (V(terminal obs), the truncation bootstrap) and
-    // the actor and critic on obs[t + 1]; their workgroups share the CUs, so each forward's latencies hide behind
-    // the others' matrix work.
+    // The actor and critic on obs[t + 1] go out as one launch (launch_mlp_multi; their workgroups share the CUs,
+    // so each forward's latencies hide behind the other's matrix work).  The truncation bootstrap is deferred: the
+    // post of step t queues the terminal observations of the envs that were truncated and not terminated, and
+    // every kTvEvery steps one forward over the queue gives their values, added to those rewards rows (the queue
+    // holds at most kTvEvery * E rows).  Per step that leaves three launches: forwards, store, step.
+    constexpr int kTvEvery = 8;
     static const bool copy_each = [] { const char* v = getenv("CH_ROLLOUT_COPY"); return v && v[0] == '1'; }();
     const size_t slot = (size_t)h->E * (size_t)ra.obs_dim;
     auto obs_at = [&](int32_t t) { return (t == 0 || t == rb->n_steps || copy_each) ? sio->obs : rb->obs + (size_t)t * slot; };
     MlpArgs fa, fc, ftv;
     if ((rc = policy_args(h, actor, sio->obs, io->mean, fa, "ch_rollout_collect (actor)"))) return rc;
     if (!fused && (rc = policy_args(h, critic, sio->obs, io->value, fc, "ch_rollout_collect (critic)"))) return rc;
-    {
-        // V(terminal obs) of the envs that just reset: the pre-reset blocks, zero past the constructor's drones
-        std::string err;
-        if ((rc = mlp_args(vnet, sio->terminal_obs, h->E, tv_out, ftv, err))) return fail(h, rc, "ch_rollout_collect: " + err);
-        ftv.row_mask = sio->reset_happened;
-        ftv.kcap = std::min(ftv.dims[0], h->NC * 86);
-    }
-    MlpArgs segs[3];
     HIP_TRY(h, hipSetDevice(h->device));
+    const long long cap = (long long)h->E * kTvEvery;
+    RolloutArgs ap = a;   // k_rollout_apply over the queue
+    if (bootstrap_truncated) {
+        const size_t nobs = (size_t)cap * ra.obs_dim, nval = (size_t)cap * out_w;
+        if (h->tv_obs_n < nobs) {
+            if (h->tv_obs) HIP_TRY(h, hipFree(h->tv_obs));
+            h->tv_obs = nullptr;
+            HIP_TRY(h, hipMalloc(&h->tv_obs, sizeof(float) * nobs));
+            if (h->tv_row) HIP_TRY(h, hipFree(h->tv_row));
+            h->tv_row = nullptr;
+            HIP_TRY(h, hipMalloc(&h->tv_row, sizeof(long long) * (size_t)cap));
+            h->tv_obs_n = nobs;
+        }
+        if (h->tv_val_n < nval) {
+            if (h->tv_val) HIP_TRY(h, hipFree(h->tv_val));
+            h->tv_val = nullptr;
+            HIP_TRY(h, hipMalloc(&h->tv_val, sizeof(float) * nval));
+            h->tv_val_n = nval;
+        }
+        if (!h->tv_count) HIP_TRY(h, hipMalloc(&h->tv_count, sizeof(int)));
+        HIP_TRY(h, hipMemsetAsync(h->tv_count, 0, sizeof(int), st));
+        // V(terminal obs) over the queue: whole (12, 86) blocks, zero past the constructor's drones
+        std::string err;
+        if ((rc = mlp_args(vnet, h->tv_obs, cap, h->tv_val, ftv, err))) return fail(h, rc, "ch_rollout_collect: " + err);
+        ftv.rows_dev = h->tv_count;
+        ftv.kcap = std::min(ftv.dims[0], h->NC * 86);
+        a.defer = 1; a.term_obs = sio->terminal_obs; a.tv_obs = h->tv_obs; a.tv_count = h->tv_count; a.tv_row = h->tv_row;
+        a.terminal_value = nullptr;
+        ap = a;
+        ap.rows = cap;
+        ap.terminal_value = h->tv_val + (fused ? rb->act_dim : 0);
+        ap.tv_ld = fused ? out_w : 1;   // the value net's output width
+    }
+    auto flush = [&]() -> hipError_t {
+        hipError_t e = launch_mlp_multi(&ftv, 1, st);
+        if (e == hipSuccess) e = launch_rollout(ap, 3, st);
+        if (e == hipSuccess) e = hipMemsetAsync(h->tv_count, 0, sizeof(int), st);
+        return e;
+    };
+    MlpArgs segs[2];
     segs[0] = fa; segs[1] = fc;
     HIP_TRY(h, launch_mlp_multi(segs, fused ? 1 : 2, st));
     for (int32_t t = 0; t < rb->n_steps; ++t) {
@@ -964,11 +1014,11 @@ int ch_rollout_collect(ch_handle* h, const ch_rollout* rb, const ch_rollout_io* 
         // bootstrap truncated rewards with V(terminal obs) -> buffer (OnPolicyAlgorithm.collect_rollouts)
         a.t = t;
         a.copy_obs = t == 0 || copy_each;
-        HIP_TRY(h, launch_rollout(a, 0, st));
+        HIP_TRY(h, launch_rollout(a, 0, st));   // (with the post of step t - 1)
+        if (bootstrap_truncated && t > 0 && t % kTvEvery == 0) HIP_TRY(h, flush());
         s.obs = (t + 1 < rb->n_steps && !copy_each) ? rb->obs + (size_t)(t + 1) * slot : sio->obs;
         if ((rc = ch_step(h, &s, stream))) return rc;
         int n = 0;
-        if (bootstrap_truncated) segs[n++] = ftv;
         if (t + 1 < rb->n_steps) {
             fa.x = fc.x = obs_at(t + 1);
             segs[n++] = fa;
@@ -979,6 +1029,15 @@ int ch_rollout_collect(ch_handle* h, const ch_rollout* rb, const ch_rollout_io* 
             segs[n++] = fv;
         }
         HIP_TRY(h, launch_mlp_multi(segs, n, st));
+    }
+    if (bootstrap_truncated) {
+        // the last step's post (and queue), the last flush; GAE then runs without a post of its own
+        RolloutArgs pa = a;
+        pa.t = rb->n_steps;
+        pa.post_only = 1;
+        HIP_TRY(h, launch_rollout(pa, 0, st));
+        HIP_TRY(h, flush());
+        a.post_prev = 0;
     }
     a.gamma_lambda = (float)((double)gamma * (double)gae_lambda);   // SB3: float32(self.gamma * self.gae_lambda)
     HIP_TRY(h, launch_rollout(a, 2, st));

@@ -66,13 +66,19 @@ constexpr int kRollThreads = 256;
 }  // namespace
 
 // after the env step t: reward (+ gamma V(terminal obs) for truncations) into the buffer, next episode start
-__device__ __forceinline__ void rollout_post_env(const RolloutArgs& a, int t, long long e) {
+// (returned too, so that the caller need not read back what it just stored); *queue: the bootstrap is deferred
+// (a.defer) and this env's terminal observation must be queued
+__device__ __forceinline__ float rollout_post_env(const RolloutArgs& a, int t, long long e, bool* queue = nullptr) {
     const long long row = (long long)t * a.rows + e;
     const bool te = a.terminated[e] != 0, tr = a.truncated[e] != 0;
     float r = a.reward[e];
-    if (tr && !te && a.terminal_value) r += a.gamma * a.terminal_value[e * a.tv_ld];   // rewards[idx] += gamma * terminal_value
+    const bool boot = tr && !te && (a.terminal_value || a.defer);
+    if (boot && !a.defer) r = fmaf(a.gamma, a.terminal_value[e * a.tv_ld], r);   // rewards[idx] += gamma * terminal_value
     a.rewards[row] = r;
-    a.last_episode_starts[e] = (te || tr) ? 1.0f : 0.0f;
+    if (queue) *queue = boot && a.defer;
+    const float les = (te || tr) ? 1.0f : 0.0f;
+    a.last_episode_starts[e] = les;
+    return les;
 }
 
 // one wave per env (kRollThreads / 64 envs per workgroup): the observation row into the buffer (copy_obs), the
@@ -84,7 +90,19 @@ __global__ __launch_bounds__(kRollThreads) void k_rollout_store(RolloutArgs a) {
     const long long e = (long long)blockIdx.x * (kRollThreads / 64) + (threadIdx.x >> 6);
     if (e >= a.rows) return;
     const long long row = (long long)a.t * a.rows + e;
-    if (a.post_prev && a.t > 0 && lane == 0) rollout_post_env(a, a.t - 1, e);
+    float les = 0.0f;
+    bool queue = false;
+    if (lane == 0) les = a.post_prev && a.t > 0 ? rollout_post_env(a, a.t - 1, e, &queue) : a.last_episode_starts[e];
+    if (__ballot(queue)) {
+        // deferred bootstrap: the terminal observation of step t - 1 into the queue (the wave copies it)
+        int slot = 0;
+        if (lane == 0) { slot = atomicAdd(a.tv_count, 1); a.tv_row[slot] = (long long)(a.t - 1) * a.rows + e; }
+        slot = __shfl(slot, 0);
+        const float4* src = reinterpret_cast<const float4*>(a.term_obs + e * a.obs_dim);
+        float4* dst = reinterpret_cast<float4*>(a.tv_obs + (long long)slot * a.obs_dim);
+        for (int k = lane; k < a.obs_dim / 4; k += 64) dst[k] = src[k];
+    }
+    if (a.post_only) return;
     if (a.copy_obs) {
         const float4* src = reinterpret_cast<const float4*>(a.obs_now + e * a.obs_dim);
         float4* dst = reinterpret_cast<float4*>(a.obs + row * a.obs_dim);
@@ -111,7 +129,7 @@ __global__ __launch_bounds__(kRollThreads) void k_rollout_store(RolloutArgs a) {
     if (lane == 0) {
         a.log_probs[row] = lps;
         a.values[row] = a.value[e * a.value_ld];
-        a.episode_starts[row] = a.last_episode_starts[e];
+        a.episode_starts[row] = les;
     }
 }
 
@@ -122,22 +140,43 @@ __global__ void k_rollout_post(RolloutArgs a) {
     rollout_post_env(a, a.t, e);
 }
 
-// RolloutBuffer.compute_returns_and_advantage, one env per thread, backwards over the buffer in float32
+// the deferred bootstraps: rewards[row of slot] += gamma V(terminal obs of slot), for the queued slots
+__global__ void k_rollout_apply(RolloutArgs a, const float* tv_val) {
+    const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= *a.tv_count) return;
+    const long long row = a.tv_row[q];
+    a.rewards[row] = fmaf(a.gamma, tv_val[q * a.tv_ld], a.rewards[row]);
+}
+
+// RolloutBuffer.compute_returns_and_advantage, one env per thread, backwards over the buffer in float32.  The
+// recursion is serial in the step; its inputs are not: each chunk of kGaeChunk steps is loaded at once (one memory
+// round trip per chunk instead of per step), then folded backwards.
+constexpr int kGaeChunk = 16;
 __global__ void k_rollout_gae(RolloutArgs a) {
     const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= a.rows) return;
-    if (a.post_prev) rollout_post_env(a, a.T - 1, e);   // the last step's post (ch_rollout_collect)
+    const float les = a.post_prev ? rollout_post_env(a, a.T - 1, e) : a.last_episode_starts[e];   // the last step's post
     const float g = a.gamma, gl = a.gamma_lambda;
     float last = 0.0f;
-    for (int s = a.T - 1; s >= 0; --s) {
-        const long long row = (long long)s * a.rows + e;
-        float nnt, nv;
-        if (s == a.T - 1) { nnt = 1.0f - a.last_episode_starts[e]; nv = a.value[e * a.value_ld]; }
-        else { nnt = 1.0f - a.episode_starts[row + a.rows]; nv = a.values[row + a.rows]; }
-        const float delta = (a.rewards[row] + (g * nv) * nnt) - a.values[row];
-        last = delta + (gl * nnt) * last;
-        a.advantages[row] = last;
-        a.returns[row] = last + a.values[row];
+    float nnt = 1.0f - les, nv = a.value[e * a.value_ld];   // the step after s: (1 - its episode start), its value
+    for (int s1 = a.T; s1 > 0; s1 -= kGaeChunk) {
+        const int s0 = s1 > kGaeChunk ? s1 - kGaeChunk : 0;
+        float rw[kGaeChunk], vl[kGaeChunk], es[kGaeChunk];
+#pragma unroll
+        for (int i = 0; i < kGaeChunk; ++i) {
+            const long long row = (long long)min(s0 + i, s1 - 1) * a.rows + e;
+            rw[i] = a.rewards[row]; vl[i] = a.values[row]; es[i] = a.episode_starts[row];
+        }
+#pragma unroll
+        for (int i = kGaeChunk - 1; i >= 0; --i) {
+            if (s0 + i >= s1) continue;
+            const long long row = (long long)(s0 + i) * a.rows + e;
+            const float delta = (rw[i] + (g * nv) * nnt) - vl[i];
+            last = delta + (gl * nnt) * last;
+            a.advantages[row] = last;
+            a.returns[row] = last + vl[i];
+            nnt = 1.0f - es[i]; nv = vl[i];
+        }
     }
 }
 
@@ -146,6 +185,8 @@ hipError_t launch_rollout(const RolloutArgs& a, int which, hipStream_t st) {
         hipLaunchKernelGGL(k_rollout_store, dim3((unsigned)((a.rows + kRollThreads / 64 - 1) / (kRollThreads / 64))),
                            dim3(kRollThreads), 0, st, a);
     else if (which == 1) hipLaunchKernelGGL(k_rollout_post, dim3((unsigned)((a.rows + 255) / 256)), dim3(256), 0, st, a);
+    else if (which == 3) hipLaunchKernelGGL(k_rollout_apply, dim3((unsigned)((a.rows + 255) / 256)), dim3(256), 0, st, a,
+                                            a.terminal_value);
     else hipLaunchKernelGGL(k_rollout_gae, dim3((unsigned)((a.rows + 63) / 64)), dim3(64), 0, st, a);
     return hipGetLastError();
 }

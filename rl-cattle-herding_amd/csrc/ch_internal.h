@@ -163,6 +163,8 @@ struct MlpArgs {
     const float* packed;       // ch_mlp_pack layout of every layer (NULL: the raw nn.Linear weights)
     long long pk_off[4];       // layer li's offset in `packed` (floats)
     int pk_pairs[4];           // layer li's padded K pair count in `packed`
+    int split_out[4], split_in[4];   // block-diagonal layers (ch_mlp; 0: dense)
+    const int* rows_dev;       // optional device row count (<= rows): workgroups past it leave at once
 };
 extern long long* g_mlp_tstamp;
 // floats of the packed layout of an MLP (per-layer offsets / pair counts out, optional)
@@ -191,6 +193,16 @@ struct RolloutArgs {
                                     // holds both heads in one [rows][act_dim + 1] buffer)
     int post_prev;                  // store (t) / gae: first run step t - 1's (T - 1's) post (ch_rollout_collect)
     int copy_obs;                   // store: copy obs_now into obs[t] (0: the step already wrote obs[t] there)
+    // deferred truncation bootstrap (ch_rollout_collect): the post of a step whose env was truncated and not
+    // terminated queues the env's terminal observation (term_obs) at slot atomicAdd(tv_count) of tv_obs with its
+    // rewards row in tv_row; every few steps one forward over the queue gives the values and k_rollout_apply adds
+    // gamma V to those rows (the same f32 fma the immediate path does)
+    int defer;
+    int post_only;                  // store: only the previous step's post (the last step's, before GAE)
+    const float* term_obs;
+    float* tv_obs;
+    int* tv_count;
+    long long* tv_row;
     long long rows;
     unsigned long long seed;
     float gamma, gamma_lambda;
@@ -199,7 +211,7 @@ struct RolloutArgs {
     float *env_actions, *obs, *actions, *rewards, *episode_starts, *values, *log_probs, *advantages, *returns,
         *last_episode_starts;
 };
-hipError_t launch_rollout(const RolloutArgs& a, int which, hipStream_t st);   // 0 store, 1 post, 2 gae
+hipError_t launch_rollout(const RolloutArgs& a, int which, hipStream_t st);   // 0 store, 1 post, 2 gae, 3 apply (cap slots)
 
 template <class R> hipError_t launch_step(const StepParams<R>& p, int team, hipStream_t st);
 template <class R> hipError_t launch_reset(const StepParams<R>& p, int team, hipStream_t st);

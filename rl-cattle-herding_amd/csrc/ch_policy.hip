@@ -203,6 +203,7 @@ __global__ __launch_bounds__(64 * NW) void k_mlp(MlpArgs a) {
     const int ldh = kWMax + 4;
     __shared__ int kmax;
     const long long row0 = (long long)blockIdx.x * kTM;
+    if (a.rows_dev && row0 >= *a.rows_dev) return;
     // widest live input row of this tile
     if (threadIdx.x == 0) kmax = 0;
     __syncthreads();
@@ -357,18 +358,52 @@ __device__ __forceinline__ int layer_mode(const MlpArgs& a, int li) {
     return a.packed ? 0 : (((a.vec_w >> li) & 1) ? 1 : 2);
 }
 
-// the wave's weight source for layer li (tiles past the layer width clamped to its last tile / row: computed,
-// never stored) and the loads of its first D pairs
+// one wave's share of layer li: its tiles -- strided (t = wave + NW j) or, in a block-diagonal layer (ch_mlp
+// split_out / split_in), contiguous (t = TW wave + j, all in one block) -- their count, and the K pairs it
+// multiplies, [pb, pb + npad): a block-diagonal layer's wave skips the other block's zero weights (each output's
+// fma chain loses only +0 terms, so the result is bit-identical)
+struct Plan2 {
+    int ntw, pb, npad;
+    bool contig;
+};
+
 template <int NW, int TW>
-__device__ __forceinline__ void mlp2_prologue(const MlpArgs& a, int li, Ring2<TW>& r, WSrc<TW>& ws, int wave, int lane) {
+__device__ __forceinline__ Plan2 mlp2_plan(const MlpArgs& a, int li, int wave, int np0) {
+    const int N = a.dims[li + 1], K = a.dims[li], nt = (N + 15) >> 4;
+    Plan2 pl;
+    pl.contig = li > 0 && a.split_out[li] > 0;   // (validated on the host)
+    if (pl.contig) {
+        const int t0 = TW * wave;
+        pl.ntw = max(0, min(TW, nt - t0));
+        const bool hi = 16 * t0 >= a.split_out[li];
+        pl.pb = hi ? a.split_in[li] / 32 : 0;
+        pl.npad = pad_pairs(hi ? K - a.split_in[li] : a.split_in[li]);
+    } else {
+        pl.ntw = (wave < nt) + (TW > 1 && wave + NW < nt);
+        pl.pb = 0;
+        pl.npad = li == 0 ? np0 : pad_pairs(K);
+    }
+    return pl;
+}
+
+template <int NW, int TW>
+__device__ __forceinline__ int mlp2_tile(const Plan2& pl, int wave, int j) {
+    return pl.contig ? TW * wave + j : wave + NW * j;
+}
+
+// the wave's weight source for layer li (tiles past the layer width clamped to its last tile / row: computed,
+// never stored), starting at pair pl.pb, and the loads of its first D pairs
+template <int NW, int TW>
+__device__ __forceinline__ void mlp2_prologue(const MlpArgs& a, int li, const Plan2& pl, Ring2<TW>& r, WSrc<TW>& ws,
+                                              int wave, int lane) {
     const int N = a.dims[li + 1], K = a.dims[li], nt = (N + 15) >> 4;
     const int mode = layer_mode<TW>(a, li);
-    ws.K = K;
+    ws.K = K - 32 * pl.pb;
 #pragma unroll
     for (int j = 0; j < TW; ++j) {
-        const int t = min(wave + NW * j, nt - 1);
-        ws.w[j] = mode == 0 ? a.packed + a.pk_off[li] + (long long)t * a.pk_pairs[li] * 512 + lane * 4
-                            : a.w[li] + (long long)min(t * 16 + (lane & 15), N - 1) * K;
+        const int t = min(mlp2_tile<NW, TW>(pl, wave, j), nt - 1);
+        ws.w[j] = mode == 0 ? a.packed + a.pk_off[li] + ((long long)t * a.pk_pairs[li] + pl.pb) * 512 + lane * 4
+                            : a.w[li] + (long long)min(t * 16 + (lane & 15), N - 1) * K + 32 * pl.pb;
     }
     const int g = lane >> 4;
 #define CH_MLP2_PRO(M)                                                                                              \
@@ -401,6 +436,7 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const long long row0 = blk * kTM;
+    if (a.rows_dev && row0 >= *a.rows_dev) return;   // (uniform: every thread reads the same count)
     if (tid == 0) kmax = 0;
     __syncthreads();
     if (tid < kTM && row0 + tid < a.rows) {
@@ -424,7 +460,8 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
     // t / (4 NW) and float4 columns t % (4 NW) + 4 NW i, i < nld, of the padded width 32 np0
     Ring2<TW> ring;
     WSrc<TW> ws;
-    mlp2_prologue<NW, TW>(a, 0, ring, ws, wave, lane);
+    Plan2 pl = mlp2_plan<NW, TW>(a, 0, wave, np0);
+    mlp2_prologue<NW, TW>(a, 0, pl, ring, ws, wave, lane);
     if (ts) ts[1] = clock64();
     constexpr int kTPR = 4 * NW, kQ = 8 * kMaxPair0 / kTPR;
     const int K0 = a.dims[0], srow = tid / kTPR, sc = 4 * (tid % kTPR), nld = (8 * np0 + kTPR - 1) / kTPR;
@@ -463,38 +500,41 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
 
     const float* cur = xa;
     int ldc = lda;
-    int npad = np0;
     for (int li = 0; li < a.layers; ++li) {
         const bool last = li == a.layers - 1;
         const int N = a.dims[li + 1];
         const int mode = layer_mode<TW>(a, li);
-        const int nt = (N + 15) >> 4;
-        const int ntw = (wave < nt) + (TW > 1 && wave + NW < nt);   // this wave's tiles (wave-uniform)
+        const int ntw = pl.ntw;
+        const float* A = cur + 32 * pl.pb;
         float bcol[TW];
 #pragma unroll
         for (int j = 0; j < TW; ++j) {
-            const int col = (wave + NW * j) * 16 + (lane & 15);
+            const int col = mlp2_tile<NW, TW>(pl, wave, j) * 16 + (lane & 15);
             bcol[j] = a.b[li] && col < N ? a.b[li][col] : 0.0f;
         }
         f32x4 acc[TW];
 #pragma unroll
         for (int j = 0; j < TW; ++j) acc[j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #define CH_MLP2_LOOP(NT_)                                                                                           \
-        if (mode == 0) mlp2_loop<NT_, TW, 0>(acc, ring, ws, cur, ldc, npad, lane);                                   \
-        else if (mode == 1) mlp2_loop<NT_, TW, 1>(acc, ring, ws, cur, ldc, npad, lane);                              \
-        else mlp2_loop<NT_, TW, 2>(acc, ring, ws, cur, ldc, npad, lane)
+        if (mode == 0) mlp2_loop<NT_, TW, 0>(acc, ring, ws, A, ldc, pl.npad, lane);                                  \
+        else if (mode == 1) mlp2_loop<NT_, TW, 1>(acc, ring, ws, A, ldc, pl.npad, lane);                             \
+        else mlp2_loop<NT_, TW, 2>(acc, ring, ws, A, ldc, pl.npad, lane)
         if (ntw == TW) { CH_MLP2_LOOP(TW); } else if (ntw > 0) { CH_MLP2_LOOP(1); }
 #undef CH_MLP2_LOOP
         if (ts && li < 3) ts[5 + 2 * li] = clock64();
         // the next layer's first pairs, in flight during this epilogue and barrier
+        const Plan2 cpl = pl;
         const int npn = last ? 0 : pad_pairs(N);
-        if (!last) mlp2_prologue<NW, TW>(a, li + 1, ring, ws, wave, lane);
+        if (!last) {
+            pl = mlp2_plan<NW, TW>(a, li + 1, wave, 0);
+            mlp2_prologue<NW, TW>(a, li + 1, pl, ring, ws, wave, lane);
+        }
         float* out = li & 1 ? hb1 : hb0;
         // epilogue: C/D map col = lane & 15, row = 4 (lane >> 4) + r
 #pragma unroll
         for (int j = 0; j < TW; ++j) {
             if (j >= ntw) continue;
-            const int col = (wave + NW * j) * 16 + (lane & 15);
+            const int col = mlp2_tile<NW, TW>(cpl, wave, j) * 16 + (lane & 15);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int row = (lane >> 4) * 4 + r;
@@ -518,7 +558,6 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
         if (ts && li < 2) ts[6 + 2 * li] = clock64();
         cur = out;
         ldc = ldh;
-        npad = npn;
     }
     if (ts) ts[10] = clock64();
 }

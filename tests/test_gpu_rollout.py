@@ -164,3 +164,27 @@ def test_fused_actor_critic_is_bit_identical():
         b.close()
     for k in bufs[0]:
         assert torch.equal(bufs[0][k], bufs[1][k]), k
+
+
+def test_block_diagonal_skip_is_exact():
+    """ch_mlp.split_out / split_in: the kernel skips a block-diagonal layer's zero blocks; the outputs equal the
+    dense forward of the same weights bit for bit (random nets, packed and raw weights, several row counts)."""
+    import torch
+    from cattleherd.policy import DevicePolicy
+    actor = DevicePolicy(DevicePolicy.random_layers([12 * 86, 128, 128, 48], seed=5), "tanh", None)
+    critic = DevicePolicy(DevicePolicy.random_layers([12 * 86, 128, 128, 1], seed=6), "tanh", None)
+    fused = DevicePolicy.fuse(actor, critic)
+    assert fused.splits == {1: (128, 128), 2: (48, 128)}
+    dense = DevicePolicy(list(zip(fused.weights, fused.biases)), "tanh", None)
+    g = torch.Generator().manual_seed(7)
+    for rows in (1, 100, 4096):
+        x = torch.randn(rows, 12 * 86, generator=g) * 0.3
+        x[:, 4 * 86:] = 0.0
+        yb, yd = fused.forward(x), dense.forward(x)
+        assert torch.equal(yb, yd), rows
+        assert torch.equal(yb[:, :48], actor.forward(x)) and torch.equal(yb[:, 48:], critic.forward(x))
+        for net in (fused, dense):
+            net._net.packed = None          # the raw nn.Linear weight path
+        assert torch.equal(fused.forward(x), yb) and torch.equal(dense.forward(x), yd)
+        for net in (fused, dense):
+            net._net.packed = net._packed.data_ptr()
