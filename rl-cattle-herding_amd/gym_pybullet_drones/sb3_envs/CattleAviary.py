@@ -112,9 +112,12 @@ class CattleAviary(_EnvBase):
         a[0, :k] = act[:k]
         torch = self.batch.torch
         obs, rew, te, tr = self.batch.step(torch.from_numpy(a).to(self.batch.device), autoreset=False)
-        obs_np = obs[0].cpu().numpy()
-        reward = float(rew[0, 0].item())
-        terminated, truncated = bool(te[0, 0].item()), bool(tr[0, 0].item())
+        # one device-to-host copy for the observation, reward and both flags (instead of four syncs)
+        nobs = obs[0].numel()
+        out = torch.cat((obs[0].reshape(-1), rew[0, :1], te[0, :1].float(), tr[0, :1].float())).cpu().numpy()
+        obs_np = out[:nobs].reshape(obs.shape[1:])
+        reward = float(out[nobs])
+        terminated, truncated = bool(out[nobs + 1]), bool(out[nobs + 2])
         if self._is_evaluating:
             s = self.batch.get_state()
             self._tracker.after_step(s, self.batch.eval_distances()[0], n, self.NUM_CATTLE, sc_before, self.CTRL_FREQ,
