@@ -1,0 +1,76 @@
+"""The multi-rank path on the HIP step itself: two rank processes on the one GPU of the test box
+(gloo for the collectives), each stepping its env shard through libcattleherd with in-kernel Philox actions and
+auto-reset; the sharded run must equal one process stepping all envs -- every env's state bit for bit (the
+actions, resets and spawn scenarios are functions of the global env id, ch_config.env_id_offset) and the
+all-reduced metric vector (float64 sums in another order: counts exact, sums within 1e-12 relative).
+The 8-GPU RCCL run is the driver's SCALE measurement; this covers the same host logic with the real kernel."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+E_TOTAL, T, N, M = 1024, 90, 4, 16
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(E, offset, steps):
+    import torch
+    from cattleherd.env import HerdBatch
+    b = HerdBatch(E, N, M, mode="ctde", curriculum_level=2, env_id_offset=offset)
+    b.reset()
+    for _ in range(steps):
+        b.step(None, random_actions=True, autoreset=True)
+    torch.cuda.synchronize()
+    st = b.get_state()
+    met = b.metrics()
+    b.close()
+    return {k: np.asarray(v) for k, v in st.items()}, met
+
+
+def _worker(rank, world, port, out):
+    sys.path.insert(0, os.path.join(ROOT, "rl-cattle-herding_amd"))
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from cattleherd import distributed as D
+    r, w, _ = D.init("gloo")
+    per = E_TOTAL // w
+    off = D.env_offset(r, per)
+    st, met = _run(per, off, T)
+    sums, tmax = D.reduce_rollout(met, elapsed=1.0 + r)
+    out[rank] = (st, sums, tmax, off)
+    D.shutdown()
+
+
+def test_sharded_hip_rollout_equals_single_process():
+    sys.path.insert(0, os.path.join(ROOT, "rl-cattle-herding_amd"))
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    out = mgr.dict()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, out)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+        assert p.exitcode == 0
+    single_st, single_met = _run(E_TOTAL, 0, T)
+    per = E_TOTAL // world
+    for r in range(world):
+        st, sums, tmax, off = out[r]
+        assert off == r * per and tmax == 2.0
+        for k, v in st.items():
+            assert np.array_equal(v, single_st[k][off:off + per], equal_nan=True), (r, k)
+        assert np.allclose(sums, single_met, rtol=1e-12, atol=0)
+    assert single_met[1] > 0, "the rollout should end episodes (auto-reset inside the sharded steps)"
