@@ -396,14 +396,22 @@ __device__ __forceinline__ int mlp2_tile(const Plan2& pl, int wave, int j) {
 template <int NW, int TW>
 __device__ __forceinline__ void mlp2_prologue(const MlpArgs& a, int li, const Plan2& pl, Ring2<TW>& r, WSrc<TW>& ws,
                                               int wave, int lane) {
-    const int N = a.dims[li + 1], K = a.dims[li], nt = (N + 15) >> 4;
-    const int mode = layer_mode<TW>(a, li);
+    // the layer's scalars read together and pinned in scalar registers here: read where each is first used
+    // (inside a branch, after another field's use) they would cost a chain of dependent scalar-cache round
+    // trips (~0.5 k cycles each at kernel start) before the first weight load
+    int N = a.dims[li + 1], K = a.dims[li], pkp = a.pk_pairs[li], vw = a.vec_w;
+    const float* pk = a.packed;
+    const float* wl = a.w[li];
+    long long pko = a.pk_off[li];
+    asm volatile("" : "+s"(N), "+s"(K), "+s"(pkp), "+s"(vw), "+s"(pk), "+s"(wl), "+s"(pko));
+    const int nt = (N + 15) >> 4;
+    const int mode = pk ? 0 : (((vw >> li) & 1) ? 1 : 2);
     ws.K = K - 32 * pl.pb;
 #pragma unroll
     for (int j = 0; j < TW; ++j) {
         const int t = min(mlp2_tile<NW, TW>(pl, wave, j), nt - 1);
-        ws.w[j] = mode == 0 ? a.packed + a.pk_off[li] + ((long long)t * a.pk_pairs[li] + pl.pb) * 512 + lane * 4
-                            : a.w[li] + (long long)min(t * 16 + (lane & 15), N - 1) * K + 32 * pl.pb;
+        ws.w[j] = mode == 0 ? pk + pko + ((long long)t * pkp + pl.pb) * 512 + lane * 4
+                            : wl + (long long)min(t * 16 + (lane & 15), N - 1) * K + 32 * pl.pb;
     }
     const int g = lane >> 4;
 #define CH_MLP2_PRO(M)                                                                                              \
@@ -436,21 +444,28 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const long long row0 = blk * kTM;
-    if (a.rows_dev && row0 >= *a.rows_dev) return;   // (uniform: every thread reads the same count)
+    // the arguments the tile's start needs, read together (see mlp2_prologue)
+    const int* rows_dev = a.rows_dev;
+    const int* env_n = a.env_n;
+    const uint8_t* row_mask = a.row_mask;
+    long long rows = a.rows, rpe = a.rows_per_env;
+    int d0 = a.dims[0], ku = a.k_unit;
+    asm volatile("" : "+s"(rows_dev), "+s"(env_n), "+s"(row_mask), "+s"(rows), "+s"(rpe), "+s"(d0), "+s"(ku));
+    if (rows_dev && row0 >= *rows_dev) return;   // (uniform: every thread reads the same count)
     if (tid == 0) kmax = 0;
     __syncthreads();
-    if (tid < kTM && row0 + tid < a.rows) {
-        int k = a.dims[0];
-        if (a.env_n) {
-            const long long r = row0 + tid, e = r / a.rows_per_env;
-            const int j = (int)(r - e * a.rows_per_env), n = a.env_n[e];
-            k = a.rows_per_env == 1 ? n * a.k_unit : (j < n ? a.k_unit : 0);
-            k = min(k, a.dims[0]);
+    if (tid < kTM && row0 + tid < rows) {
+        int k = d0;
+        if (env_n) {
+            const long long r = row0 + tid, e = r / rpe;
+            const int j = (int)(r - e * rpe), n = env_n[e];
+            k = rpe == 1 ? n * ku : (j < n ? ku : 0);
+            k = min(k, d0);
         }
         atomicMax(&kmax, k);
     }
-    const bool any = __syncthreads_or(a.row_mask && tid < kTM && row0 + tid < a.rows && a.row_mask[row0 + tid] != 0);
-    if (a.row_mask && !any) return;
+    const bool any = __syncthreads_or(row_mask && tid < kTM && row0 + tid < rows && row_mask[row0 + tid] != 0);
+    if (row_mask && !any) return;
     const int kloop = min(kmax, a.kcap);   // (the host sized the tile for kcap)
     const int np0 = min(pad_pairs(max(kloop, 1)), kMaxPair0);
     long long* ts = a.tstamp && tid == 0 ? a.tstamp + blk * 16 : nullptr;
