@@ -1008,6 +1008,36 @@ int ch_rollout_collect(ch_handle* h, const ch_rollout* rb, const ch_rollout_io* 
     };
     MlpArgs segs[2];
     segs[0] = fa; segs[1] = fc;
+    static const bool no_epi = [] { const char* v = getenv("CH_ROLLOUT_STORE_KERNEL"); return v && v[0] == '1'; }();
+    if (!fused && !no_epi && mlp_multi_fits(segs, 2)) {
+        // Two launches per step: the actor and critic forwards with the store folded into their epilogues (the
+        // actor's samples its actions, log-probabilities and env actions; the critic's writes the values, the
+        // previous step's post and the episode starts, and at t = 0 copies obs[0]), then the step.
+        const int roles[2] = {kRoleSample, kRoleValue};
+        RolloutArgs ro = a;
+        for (int32_t t = 0; t < rb->n_steps; ++t) {
+            segs[0].x = segs[1].x = obs_at(t);
+            ro.t = t;
+            ro.copy_obs = t == 0 || copy_each;
+            HIP_TRY(h, launch_mlp_multi(segs, 2, st, roles, &ro));
+            if (bootstrap_truncated && t > 0 && t % kTvEvery == 0) HIP_TRY(h, flush());
+            s.obs = (t + 1 < rb->n_steps && !copy_each) ? rb->obs + (size_t)(t + 1) * slot : sio->obs;
+            if ((rc = ch_step(h, &s, stream))) return rc;
+        }
+        // the last step's post (and queue) and flush, V(obs after the last step), GAE without a post of its own
+        RolloutArgs pa = a;
+        pa.t = rb->n_steps;
+        pa.post_only = 1;
+        HIP_TRY(h, launch_rollout(pa, 0, st));
+        if (bootstrap_truncated) HIP_TRY(h, flush());
+        MlpArgs fv = fc;
+        fv.x = obs_at(rb->n_steps);
+        HIP_TRY(h, launch_mlp_multi(&fv, 1, st));
+        a.post_prev = 0;
+        a.gamma_lambda = (float)((double)gamma * (double)gae_lambda);   // SB3: float32(self.gamma * self.gae_lambda)
+        HIP_TRY(h, launch_rollout(a, 2, st));
+        return CH_OK;
+    }
     HIP_TRY(h, launch_mlp_multi(segs, fused ? 1 : 2, st));
     for (int32_t t = 0; t < rb->n_steps; ++t) {
         // SB3 collect_rollouts, one step of every env: policy(obs) -> sample, log-prob, value -> env.step ->

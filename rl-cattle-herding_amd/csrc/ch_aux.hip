@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include "ch_internal.h"
+#include "ch_rollout_dev.h"
 
 namespace ch {
 
@@ -52,34 +53,8 @@ hipError_t launch_metrics_reduce(double* metrics, long long E, double* out, cons
 //   a done that is a truncation (TimeLimit.truncated = truncated and not terminated) bootstraps the
 //   reward with gamma V(terminal_observation); GAE(gamma, lambda) backwards over the buffer in float32.
 namespace {
-__device__ __forceinline__ void philox_k(uint32_t c[4], uint32_t k0, uint32_t k1) {
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        uint32_t lo0 = 0xD2511F53u * c[0], hi0 = __umulhi(0xD2511F53u, c[0]);
-        uint32_t lo1 = 0xCD9E8D57u * c[2], hi1 = __umulhi(0xCD9E8D57u, c[2]);
-        uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
-        c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
-        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
-    }
-}
 constexpr int kRollThreads = 256;
 }  // namespace
-
-// after the env step t: reward (+ gamma V(terminal obs) for truncations) into the buffer, next episode start
-// (returned too, so that the caller need not read back what it just stored); *queue: the bootstrap is deferred
-// (a.defer) and this env's terminal observation must be queued
-__device__ __forceinline__ float rollout_post_env(const RolloutArgs& a, int t, long long e, bool* queue = nullptr) {
-    const long long row = (long long)t * a.rows + e;
-    const bool te = a.terminated[e] != 0, tr = a.truncated[e] != 0;
-    float r = a.reward[e];
-    const bool boot = tr && !te && (a.terminal_value || a.defer);
-    if (boot && !a.defer) r = fmaf(a.gamma, a.terminal_value[e * a.tv_ld], r);   // rewards[idx] += gamma * terminal_value
-    a.rewards[row] = r;
-    if (queue) *queue = boot && a.defer;
-    const float les = (te || tr) ? 1.0f : 0.0f;
-    a.last_episode_starts[e] = les;
-    return les;
-}
 
 // one wave per env (kRollThreads / 64 envs per workgroup): the observation row into the buffer (copy_obs), the
 // Gaussian sample of every action (lane k: action k, k + 64, ...), the summed log-probability (a wave tree
@@ -108,25 +83,17 @@ __global__ __launch_bounds__(kRollThreads) void k_rollout_store(RolloutArgs a) {
         float4* dst = reinterpret_cast<float4*>(a.obs + row * a.obs_dim);
         for (int k = lane; k < a.obs_dim / 4; k += 64) dst[k] = src[k];
     }
-    float lps = 0.0f;
-    for (int k = lane; k < a.act_dim; k += 64) {
-        // standard normal from Philox4x32-10 (seed, step, env, action) by Box-Muller
-        uint32_t c[4] = {(uint32_t)a.t, (uint32_t)k, (uint32_t)e, (uint32_t)(e >> 32)};
-        philox_k(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
-        const float u1 = ((float)(c[0] >> 8) + 1.0f) * (1.0f / 16777216.0f);   // (0, 1]
-        const float u2 = (float)(c[1] >> 8) * (1.0f / 16777216.0f);
-        const float eps = sqrtf(-2.0f * logf(u1)) * cosf(6.2831853071795865f * u2);
-        const float mu = a.mean[e * a.mean_ld + k], ls = a.log_std[k], sd = expf(ls);
-        const float act = mu + sd * eps;
-        a.actions[row * a.act_dim + k] = act;
-        // torch.distributions.Normal.log_prob: -((x - mu)^2) / (2 var) - log(std) - log(sqrt(2 pi))
-        const float d = act - mu, var = sd * sd;
-        lps += -(d * d) / (2.0f * var) - ls - 0.91893853320467274f;
-        if (k < a.env_act_dim) a.env_actions[e * a.env_act_dim + k] = fminf(fmaxf(act, -1.0f), 1.0f);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) lps += __shfl_xor(lps, o);
+    // the log-probability: every dimension's term into LDS, then summed in action order by one lane (the order
+    // the policy forward's sampling epilogue uses too)
+    __shared__ float lpt[kRollThreads / 64][256];
+    float* lp = lpt[threadIdx.x >> 6];
+    for (int k = lane; k < a.act_dim; k += 64) lp[k] = rollout_sample(a, a.t, k, e, a.mean[e * a.mean_ld + k]);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
     if (lane == 0) {
+        float lps = 0.0f;
+        for (int k = 0; k < a.act_dim; ++k) lps += lp[k];
         a.log_probs[row] = lps;
         a.values[row] = a.value[e * a.value_ld];
         a.episode_starts[row] = les;

@@ -170,14 +170,6 @@ extern long long* g_mlp_tstamp;
 // floats of the packed layout of an MLP (per-layer offsets / pair counts out, optional)
 long long mlp_packed_floats(int layers, const int* dims, long long* off, int* pairs);
 hipError_t launch_mlp_pack(const MlpArgs& a, float* dst, hipStream_t st);
-// up to three independent forwards in one launch (ch_policy.hip k_mlp2)
-struct MlpMulti {
-    MlpArgs seg[3];
-    int nseg;
-    int start[4];              // first workgroup of each segment (start[nseg] = grid)
-    int lda, ldh;
-};
-hipError_t launch_mlp_multi(const MlpArgs* segs, int nseg, hipStream_t st);
 size_t mlp_lds_bytes();
 hipError_t launch_mlp(const MlpArgs& a, hipStream_t st);
 
@@ -212,6 +204,24 @@ struct RolloutArgs {
         *last_episode_starts;
 };
 hipError_t launch_rollout(const RolloutArgs& a, int which, hipStream_t st);   // 0 store, 1 post, 2 gae, 3 apply (cap slots)
+
+// up to three independent forwards in one launch (ch_policy.hip k_mlp2).  A segment's role folds the rollout
+// store into its last layer's epilogue (ch_rollout_collect): kRoleSample -- the actor's mean becomes the
+// Gaussian sample, its log-probability and the env actions (k_rollout_store's action half); kRoleValue -- the
+// critic's value goes into the buffer together with the previous step's post and the episode start (its
+// other half).  `ro` holds the rollout buffer for both.
+enum { kRoleNone = 0, kRoleSample = 1, kRoleValue = 2 };
+struct MlpMulti {
+    MlpArgs seg[3];
+    int nseg;
+    int start[4];              // first workgroup of each segment (start[nseg] = grid)
+    int lda, ldh;
+    int role[3];
+    RolloutArgs ro;
+};
+hipError_t launch_mlp_multi(const MlpArgs* segs, int nseg, hipStream_t st, const int* roles = nullptr,
+                            const RolloutArgs* ro = nullptr);
+bool mlp_multi_fits(const MlpArgs* segs, int nseg);   // k_mlp2 takes these nets (the rollout epilogues need it)
 
 template <class R> hipError_t launch_step(const StepParams<R>& p, int team, hipStream_t st);
 template <class R> hipError_t launch_reset(const StepParams<R>& p, int team, hipStream_t st);

@@ -22,6 +22,7 @@
 #include <cstring>
 
 #include "ch_internal.h"
+#include "ch_rollout_dev.h"
 
 namespace ch {
 
@@ -434,12 +435,14 @@ __device__ __forceinline__ void mlp2_lds_barrier() {
 // the hidden activations, both = 4 mod 64 (conflict-free 16-B operand reads), wide enough for the padded pair
 // counts.
 template <int NW, int TW>
-__device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int lda, int ldh) {
+__device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int lda, int ldh, int role,
+                                          const RolloutArgs& ro) {
     extern __shared__ __align__(16) float sm[];
     float* xa = sm;                    // [16][lda]
     float* hb0 = xa + kTM * lda;       // [16][ldh]
     float* hb1 = hb0 + kTM * ldh;
     __shared__ int kmax;
+    __shared__ int qslot[kTM];         // kRoleValue: each row's slot in the deferred-bootstrap queue (-1: none)
     constexpr int kT = 64 * NW;        // threads
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -558,7 +561,8 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
                     if (col < N) out[row * ldh + col] = act_fn(v, a.hidden_act);
                 } else if (col < N && row0 + row < a.rows && (!a.row_mask || a.row_mask[row0 + row])) {
                     if (a.clip) v = fminf(fmaxf(v, a.lo), a.hi);
-                    a.y[(row0 + row) * (long long)N + col] = v;
+                    if (role != kRoleNone) out[row * ldh + col] = v;   // (the rollout epilogue below)
+                    else a.y[(row0 + row) * (long long)N + col] = v;
                 }
             }
         }
@@ -575,6 +579,63 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
         ldc = ldh;
     }
     if (ts) ts[10] = clock64();
+    if (role == kRoleSample) {
+        // the actor's means (staged in the last layer's would-be output buffer) become the samples, their env
+        // actions and per-dimension log-probability terms -- spread over the whole workgroup -- then each row's
+        // terms are summed in action order by one lane (k_rollout_store's order)
+        float* lp = a.layers & 1 ? hb0 : hb1;
+        const int NA = a.dims[a.layers];
+        const int nrow = (int)min((long long)kTM, a.rows - row0);
+        mlp2_lds_barrier();
+        for (int idx = tid; idx < nrow * NA; idx += kT) {
+            const int r = idx / NA, k = idx - r * NA;
+            lp[r * ldh + k] = rollout_sample(ro, ro.t, k, row0 + r, lp[r * ldh + k]);
+        }
+        mlp2_lds_barrier();
+        if (tid < nrow) {
+            float s = 0.0f;
+            for (int k = 0; k < NA; ++k) s += lp[tid * ldh + k];
+            ro.log_probs[(long long)ro.t * ro.rows + row0 + tid] = s;
+        }
+    } else if (role == kRoleValue) {
+        // the critic's values (staged like the actor's means), the previous step's post (reward, next episode
+        // start, deferred-bootstrap queue) and this step's episode starts for the tile's rows; at t = 0 the
+        // observation rows into obs[0]
+        const float* vl = a.layers & 1 ? hb0 : hb1;
+        mlp2_lds_barrier();
+        if (tid < kTM) {
+            const long long e = row0 + tid;
+            int slot = -1;
+            if (e < a.rows) {
+                ro.values[(long long)ro.t * ro.rows + e] = vl[tid * ldh];
+                bool q = false;
+                const float les = ro.t > 0 ? rollout_post_env(ro, ro.t - 1, e, &q) : ro.last_episode_starts[e];
+                ro.episode_starts[(long long)ro.t * ro.rows + e] = les;
+                if (q) {
+                    slot = atomicAdd(ro.tv_count, 1);
+                    ro.tv_row[slot] = (long long)(ro.t - 1) * ro.rows + e;
+                }
+            }
+            qslot[tid] = slot;
+        }
+        mlp2_lds_barrier();
+        const int nq4 = ro.obs_dim / 4;
+        for (int r = 0; r < kTM; ++r) {
+            const int slot = qslot[r];
+            if (slot < 0) continue;
+            const float4* src = reinterpret_cast<const float4*>(ro.term_obs + (row0 + r) * ro.obs_dim);
+            float4* dst = reinterpret_cast<float4*>(ro.tv_obs + (long long)slot * ro.obs_dim);
+            for (int k = tid; k < nq4; k += kT) dst[k] = src[k];
+        }
+        if (ro.copy_obs) {
+            const int nr = (int)min((long long)kTM, a.rows - row0);
+            for (int k = tid; k < nr * nq4; k += kT) {
+                const int r = k / nq4, c = k - r * nq4;
+                reinterpret_cast<float4*>(ro.obs + ((long long)ro.t * ro.rows + row0 + r) * ro.obs_dim)[c] =
+                    reinterpret_cast<const float4*>(a.x + (row0 + r) * (long long)ro.obs_dim)[c];
+            }
+        }
+    }
 }
 
 // up to three independent forwards in one launch (MlpMulti): workgroups [start[s], start[s + 1]) run segment s.
@@ -587,7 +648,7 @@ __global__ __launch_bounds__(64 * NW, SHARE ? 4 : 1) void k_mlp2(MlpMulti m) {
     int sg = 0;
     if (m.nseg > 1 && (int)blockIdx.x >= m.start[1]) sg = 1;
     if (m.nseg > 2 && (int)blockIdx.x >= m.start[2]) sg = 2;
-    mlp2_body<NW, TW>(m.seg[sg], (long long)blockIdx.x - m.start[sg], m.lda, m.ldh);
+    mlp2_body<NW, TW>(m.seg[sg], (long long)blockIdx.x - m.start[sg], m.lda, m.ldh, m.role[sg], m.ro);
 }
 
 // ch_mlp_pack: layer li's weights into the [tile][pair][half][lane][4] layout (zero past N and K)
@@ -659,7 +720,7 @@ static bool mlp2_shape(const MlpArgs& a, int& maxw, int& lda, int& ldh) {
     maxw = 0;
     for (int i = 1; i <= a.layers; ++i) {
         maxw = a.dims[i] > maxw ? a.dims[i] : maxw;
-        if (i < a.layers) maxhid = a.dims[i] > maxhid ? a.dims[i] : maxhid;
+        maxhid = a.dims[i] > maxhid ? a.dims[i] : maxhid;   // (the output too: the sampling epilogue stages there)
     }
     const int np0 = pad_pairs(std::max(a.kcap, 1));
     lda = (32 * np0 + 63) / 64 * 64 + 4;
@@ -667,7 +728,17 @@ static bool mlp2_shape(const MlpArgs& a, int& maxw, int& lda, int& ldh) {
     return np0 <= kMaxPair0 && sizeof(float) * (size_t)kTM * (lda + 2 * ldh) <= (size_t)kLdsMax2;
 }
 
-hipError_t launch_mlp_multi(const MlpArgs* segs, int nseg, hipStream_t st) {
+bool mlp_multi_fits(const MlpArgs* segs, int nseg) {
+    static const bool v1 = [] { const char* v = getenv("CH_MLP_V1"); return v && v[0] == '1'; }();
+    if (v1) return false;
+    for (int s = 0; s < nseg; ++s) {
+        int w, la, lh;
+        if (!mlp2_shape(segs[s], w, la, lh)) return false;
+    }
+    return true;
+}
+
+hipError_t launch_mlp_multi(const MlpArgs* segs, int nseg, hipStream_t st, const int* roles, const RolloutArgs* ro) {
     static const bool v1 = [] { const char* v = getenv("CH_MLP_V1"); return v && v[0] == '1'; }();
     static const bool nw4 = [] { const char* v = getenv("CH_MLP2_NW4"); return v && v[0] == '1'; }();   // A/B
     static const bool wide4 = [] { const char* v = getenv("CH_MLP_WIDE4"); return v && v[0] == '1'; }();
@@ -685,11 +756,13 @@ hipError_t launch_mlp_multi(const MlpArgs* segs, int nseg, hipStream_t st) {
         maxw = std::max(maxw, w); m.lda = std::max(m.lda, la); m.ldh = std::max(m.ldh, lh);
         m.seg[n] = segs[s];
         m.seg[n].tstamp = g_mlp_tstamp;
+        m.role[n] = roles ? roles[s] : kRoleNone;
         m.start[n] = grid;
         grid += (int)g;
         ++n;
     }
     if (n == 0) return hipSuccess;
+    if (ro) m.ro = *ro;
     m.nseg = n;
     m.start[n] = grid;
     const size_t lds2 = sizeof(float) * (size_t)kTM * (m.lda + 2 * m.ldh);
@@ -700,8 +773,9 @@ hipError_t launch_mlp_multi(const MlpArgs* segs, int nseg, hipStream_t st) {
         else hipLaunchKernelGGL((k_mlp2<8, 1>), dim3((unsigned)grid), dim3(512), lds2, st, m);
         return hipGetLastError();
     }
-    // the round-2 kernel, one launch per net
+    // the round-2 kernel, one launch per net (no rollout epilogues: callers check mlp_multi_fits first)
     for (int s = 0; s < n; ++s) {
+        if (m.role[s] != kRoleNone) return hipErrorInvalidValue;
         const MlpArgs& a = m.seg[s];
         const unsigned g = (unsigned)((a.rows + kTM - 1) / kTM);
         int w = 0;
