@@ -68,8 +68,10 @@ __device__ __forceinline__ int reset_draw_n(const StepParams<R>& p, int episode,
 // advanced before use (600-606); prev_cent_dists / spacing clock persist in compat mode (CattleAviary.py:89)
 template <class R, class PR>
 __device__ __forceinline__ void reset_scalars(const StepParams<R>& p, int e, int& n, int& sc, int& scA, int& spawn,
-                                              int& episode, int& active, int& has_prev, PR& prev, R& clock) {
-    const int nn = p.reset_n ? p.reset_n[e] : reset_draw_n(p, episode, p.env_off + e);
+                                              int& episode, int& active, int& has_prev, PR& prev, R& clock,
+                                              int drawn = -1) {
+    // drawn >= 0: the caller's draw for this episode (v2 takes it ahead of the reset decision)
+    const int nn = drawn >= 0 ? drawn : p.reset_n ? p.reset_n[e] : reset_draw_n(p, episode, p.env_off + e);
     n = nn;
     sc = 0; scA = 0;
     spawn += 1;

@@ -1293,7 +1293,11 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         // publish the reset list: the cow waves rebuild those envs while this wave finishes the reward.
         // This wave's drone-state stores are complete first (the cow waves overwrite reset drones).
         if (envl) ei[I_RESET * G + g] = rs;
-        if (envl && rs) ei[I_NEWN * G + g] = p.reset_n ? p.reset_n[e] : reset_draw_n(p, f_episode, p.env_off + e);
+        // the next episode's NUM_DRONES draw (BaseAviary.py:307), once: reset_scalars takes it from here.  (Drawn on
+        // every env lane ahead of the cow items' hand-off instead, measured: no gain, profiles/r03/n/ab_draw.log.)
+        int n_next = 0;
+        if (envl && rs) n_next = p.reset_n ? p.reset_n[e] : reset_draw_n(p, f_episode, p.env_off + e);
+        if (envl && rs) ei[I_NEWN * G + g] = n_next;
         const unsigned long long rbal = __ballot(rs != 0);
         if (rs) ei[RS_LIST + __popcll(rbal & ((1ull << g) - 1ull))] = g;
         if (tid == 0) ei[NR_AT] = __popcll(rbal);
@@ -1413,7 +1417,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             if (g == 0) TS(28, (long long)clock64());
             if (p.reset_happened) p.reset_happened[e] = rs;
             // SB3 auto-reset: the new episode's scalars (the cow waves rebuild its bodies and observation)
-            if (rs) reset_scalars(p, e, f_n, f_sc, f_scA, f_spawn, f_episode, f_active, f_hp, f_prev, f_clock);
+            if (rs) reset_scalars(p, e, f_n, f_sc, f_scA, f_spawn, f_episode, f_active, f_hp, f_prev, f_clock, n_next);
             if (p.agent_active)
                 for (int i = 0; i < N; ++i) p.agent_active[(long long)e * N + i] = (f_active >> i) & 1;
         } else if (envl && p.reset_happened) {
@@ -1776,7 +1780,15 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         if (nr && ct == 0) TS(52, (long long)clock64());
         TS_MAX(56);
         if (late) {
-            euler_pass();
+            // the Euler items (one chunk) go to the first wave that holds no cow of the final pass, so that their
+            // stream overlaps the final pass; a wave with final-pass cows takes them only after its own cows (when
+            // every other wave is still busy with flock work)
+#ifdef CH_EULER_ANYWAVE
+            const bool ew = true;
+#else
+            const bool ew = Gv * M > CW - 64 || ct - lane >= Gv * M;
+#endif
+            if (ew) euler_pass();
             TS_MAX(58);
             // final pass, each cow on its phase-0 lane: cattle observation entries (of the new episode for a
             // fast-reset env, whose new positions and velocities this lane writes too), then the flocking envs'
@@ -1815,6 +1827,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                 }
                 if (ei[I_FLOCK * G + g]) arrive_final(u);
             }
+            if (!ew) euler_pass();
             TS_MAX(60);
         }
         if (nr && !fast) {   // uniform across the cow waves
