@@ -958,7 +958,8 @@ int ch_rollout_collect(ch_handle* h, const ch_rollout* rb, const ch_rollout_io* 
     // so each forward's latencies hide behind the other's matrix work).  The truncation bootstrap is deferred: the
     // post of step t queues the terminal observations of the envs that were truncated and not terminated, and
     // every kTvEvery steps one forward over the queue gives their values, added to those rewards rows (the queue
-    // holds at most kTvEvery * E rows).  Per step that leaves three launches: forwards, store, step.
+    // holds at most kTvEvery * E rows).  Per step that leaves two launches with separate nets (forwards with the
+    // store in their epilogues, step) and three with a fused net or CH_ROLLOUT_STORE_KERNEL=1 (forward, store, step).
     constexpr int kTvEvery = 8;
     static const bool copy_each = [] { const char* v = getenv("CH_ROLLOUT_COPY"); return v && v[0] == '1'; }();
     const size_t slot = (size_t)h->E * (size_t)ra.obs_dim;

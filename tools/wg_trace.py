@@ -25,7 +25,7 @@ def trace(mode, E, n, m, prec, G=None, B=None, steps=4):
     grid = (E + g.value - 1) // g.value
     ts = torch.zeros((grid, 128), dtype=torch.int64, device=b.device)
     b.reset()
-    for _ in range(250):   # steady state: resets have desynchronised the flocking parity
+    for _ in range(0 if os.environ.get("CH_TRACE_NOBURN") else 250):   # steady state: resets have desynchronised the flocking parity
         b.step(random_actions=True, autoreset=True, terminal_obs=False)
     L.ch__set_tstamp(b.handle, ctypes.c_void_p(ts.data_ptr()))
     if os.environ.get("CH_PHASE_MASK"):
