@@ -1444,10 +1444,17 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         const int nf = ei[NF_AT];
         const int* flist = ei + FL_LIST;
         const int lane = tid & 63;
-        // a cow wave on the drone wave's SIMD takes no chunks (phase-mask bits 128: after the drone hand-off,
-        // 256: before it): a chunk it holds finishes late, as the prioritised drone wave wins the SIMD's issue
+        // a cow wave on the drone wave's SIMD takes no chunks before the drone hand-off (phase-mask bit 256: it
+        // does) and, with bit 128, none after it either: a chunk it holds finishes late, as the prioritised drone
+        // wave wins the SIMD's issue.  Before the hand-off that was the last cheap-pass chunk the F_C barrier
+        // waited for (workgroup max 45.7-46.8 k -> 43.2-43.9 k cycles, profiles/r03/q)
         const bool co = co_simd && W1 >= 4;   // the other cow waves (>= 2 of them) take the work
-        const bool skip_pre = co && (p.phase_mask & 256), skip_post = co && (p.phase_mask & 128);
+#ifdef CH_CO_PRE_TAKE
+        const bool skip_pre = co && (p.phase_mask & 256);
+#else
+        const bool skip_pre = co && !(p.phase_mask & 256);
+#endif
+        const bool skip_post = co && (p.phase_mask & 128);
         bool skip_now = skip_pre;
         // PW: this wave's env slot and queue, the env (flock-list index) it holds, the next cheap-pass
         // chunk, and the queue length / position of the expensive pass
