@@ -63,38 +63,40 @@ def survey_bytes(mode, n, m, rows):
     return 16 * n + 176 * n + 32 * m + 64 + 344 * rows + 6 * k
 
 
-def pmc_record(workload, dtype):
-    """The newest committed rocprofv3 --pmc record of the step kernel
-    (profiles/rNN/traffic_<workload>_<dtype>.json, written by tools/parse_pmc.py), or ({}, None)."""
-    import glob
-    hits = sorted(glob.glob(os.path.join(PROFILES, "r*", f"traffic_{workload}_{dtype}.json")))
-    if not hits:
-        return {}, None
-    with open(hits[-1]) as fh:
-        return json.load(fh), os.path.relpath(hits[-1], ROOT)
+COUNTERS = os.path.join(PROFILES, "counters")
 
 
-def pmc_traffic(workload, dtype):
-    """HBM bytes per launch of the step kernel from the newest committed PMC record, or None."""
-    d, src = pmc_record(workload, dtype)
-    return d.get("traffic_bytes_per_launch"), src
+def counter_record(name):
+    """The committed counter record profiles/counters/<name>.json (tools/counter_record.py, tools/flock_roofline.py)
+    if it was measured on the code object this process runs (cattleherd._lib.code_object_hash), else ({}, reason)."""
+    from cattleherd._lib import code_object_hash
+    path = os.path.join(COUNTERS, f"{name}.json")
+    if not os.path.exists(path):
+        return {}, f"no record {os.path.relpath(path, ROOT)}"
+    with open(path) as fh:
+        d = json.load(fh)
+    have = code_object_hash()
+    if d.get("code_object") != have:
+        return {}, f"{os.path.relpath(path, ROOT)} is of code object {d.get('code_object')}, this library is {have}"
+    d["source"] = os.path.relpath(path, ROOT)
+    return d, None
 
 
-def valu_issue(workload, dtype, kern_us):
-    """Compute-side view of the same kernel: fp64/fp32 VALU wave-instructions per launch (PMC
-    SQ_INSTS_VALU) priced at their issue cost on a SIMD-32 (wave64: 4 cycles fp64, 2 fp32; the
-    MI355X guide's constants table) over all SIMDs (256 CUs x 4) at 2.4 GHz for this launch time."""
-    d, src = pmc_record(workload, dtype)
+def valu_issue(d, dtype, kern_us):
+    """Compute-side view of the step kernel from its counter record: VALU wave-instructions per launch (PMC
+    SQ_INSTS_VALU) priced at their issue cost on a SIMD (wave64: 4 cycles fp64, 2 fp32; the MI355X guide's constants
+    table) over all SIMDs (256 CUs x 4) at 2.4 GHz for this launch time."""
     if "sq_insts_valu" not in d:
         return None
     cyc = 4 if dtype == "f64" else 2
     simd_cycles = 256 * 4 * kern_us * 1e-6 * 2.4e9
     return {"valu_insts_per_launch": d["sq_insts_valu"], "salu_insts_per_launch": d.get("sq_insts_salu"),
+            "lds_insts_per_launch": d.get("sq_insts_lds"),
             "issue_cycles_per_inst": cyc, "issue_frac": d["sq_insts_valu"] * cyc / simd_cycles,
             "active_frac": (d["sq_active_inst_valu"] * 4 / simd_cycles) if "sq_active_inst_valu" in d else None,
-            "source": src,
-            "note": "issue_frac = VALU issue cycles / SIMD cycles (upper bound: counts every VALU op at the "
-                    "wide rate); active_frac from SQ_ACTIVE_INST_VALU (quad-cycles, summed over waves)"}
+            "source": d.get("source"),
+            "note": "issue_frac = VALU issue cycles / SIMD cycles (upper bound: counts every VALU op at the wide rate); "
+                    "active_frac from SQ_ACTIVE_INST_VALU (quad-cycles, summed over waves)"}
 
 
 def kernel_name(b):
@@ -115,7 +117,9 @@ def policy_rollout(b, n, steps, warmup):
     import torch
     from cattleherd.policy import DevicePolicy
     d = np.load(POLICY_GOLDEN)
-    actor = DevicePolicy.sb3_actor({k.replace("__", "."): torch.tensor(d[k]) for k in d.files if "__" in k})
+    # the trained model's weights are frozen: packed once (cache_packed)
+    actor = DevicePolicy.sb3_actor({k.replace("__", "."): torch.tensor(d[k]) for k in d.files if "__" in k},
+                                   cache_packed=True)
     E = b.n_envs
     stream = torch.cuda.current_stream()
     b.reset()
@@ -217,6 +221,61 @@ def marl_vec_rollout(n, m, E, steps, warmup, burn_in):
                     "RLlibMultiAgentWrapper-style dicts for every env built on the host"}
 
 
+def host_surfaces(steps):
+    """The drop-in host surfaces at full size, numpy in and out (what the reference's drivers see):
+    sb3_vecenv -- cattleherd.vec_env.CattleHerdVecEnv at configs[3]'s per-GPU size (4096 x (4, 16)), the
+    ``vec_env_cls`` swap for CTDECattleHerder.py's SubprocVecEnv: numpy actions in, step, ch_outputs_to_host
+    (pinned), SB3 infos; marl_vec_env_dict -- cattleherd.marl_vec_env.CattleHerdMultiAgentVecEnv.step at
+    configs[4] (4096 x (4, 32)): RLlibMultiAgentWrapper-style dicts for every env."""
+    import numpy as np
+    import torch
+    from cattleherd.marl_vec_env import CattleHerdMultiAgentVecEnv
+    from cattleherd.vec_env import CattleHerdVecEnv
+    out = {}
+    rng = np.random.default_rng(0)
+    E = 4096
+    venv = CattleHerdVecEnv(E, num_drones=4, num_cattle=16)
+    venv.reset()
+    acts = [rng.uniform(-1, 1, (E, 4, 4)).astype(np.float32) for _ in range(4)]
+    for t in range(300):   # burn-in: auto-resets at their steady-state rate
+        venv.step(acts[t % 4])
+    k = max(20, min(steps, 100))
+    ended = 0
+    t0 = time.perf_counter()
+    for t in range(k):
+        _, _, dones, _ = venv.step(acts[t % 4])
+        ended += int(dones.sum())
+    dt = time.perf_counter() - t0
+    venv.close()
+    out["sb3_vecenv"] = {"env_steps_per_s": E * k / dt, "ms_per_step": dt / k * 1e3, "steps": k, "episodes_ended": ended,
+                         "config": "4096 envs x (4 drones, 16 cattle), CTDE, numpy actions (E, 4, 4)",
+                         "note": "VecEnv.step: action H2D, one launch (terminal observations on), one ch_outputs_to_host "
+                                 "(live obs rows, reward, flags, ended envs compacted on the device) into pinned buffers, "
+                                 "SB3 infos with terminal_observation / TimeLimit.truncated / Monitor episode"}
+    mv = CattleHerdMultiAgentVecEnv(E, {"num_drones": 4, "num_cattle": 32, "min_drones": 4, "max_drones": 4})
+    mv.reset()
+    g = torch.Generator(device=mv.batch.device).manual_seed(0)
+    dev_acts = torch.rand((E, 4, 4), generator=g, device=mv.batch.device) * 2 - 1
+    for _ in range(200):
+        mv.step_tensors(dev_acts)
+    mv.refresh_agents()
+    host_acts = [rng.uniform(-1, 1, (E, 4, 4)).astype(np.float32) for _ in range(4)]
+    for t in range(3):
+        mv.step(host_acts[t % 4])
+    kd = 10
+    t0 = time.perf_counter()
+    for t in range(kd):
+        mv.step(host_acts[t % 4])
+    dt = time.perf_counter() - t0
+    mv.close()
+    out["marl_vec_env_dict"] = {"env_steps_per_s": E * kd / dt, "agent_steps_per_s": 4 * E * kd / dt,
+                                "ms_per_step": dt / kd * 1e3, "steps": kd,
+                                "config": "4096 envs x (4 drones, 32 cattle), MARL wrapper semantics, numpy actions",
+                                "note": "CattleHerdMultiAgentVecEnv.step: one launch, one ch_outputs_to_host, obs / "
+                                        "rewards / dones / truncs / infos dicts keyed agent_i + __all__ for every env"}
+    return out
+
+
 def cpu_baseline(mode, n, m, seconds=12.0):
     """The CPU oracle (scalar fp64 C port, OpenMP one env per thread) on a bounded sample, on every
     core this process may use: OMP_NUM_THREADS when the pool sets it (16 per GPU on the MI355X
@@ -286,6 +345,8 @@ def main():
                     help="MARL workloads: also time the batched multi-agent surface (tensor and dict paths)")
     ap.add_argument("--launch-check", action="store_true",
                     help="run only the multi-rank plumbing (process group, env ranges, all-reduce); no GPU")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the legs after the headline (terminal observations, host surfaces): counter passes")
     args = ap.parse_args()
 
     # --gpus N from a plain `python bench.py`: one child process per GPU, started before this
@@ -392,9 +453,27 @@ def main():
         bytes_step += 2 * 7 * rb * n   # carried last_clipped_action + rpy_rates, read and written
     achieved = bytes_step * E / (kern_us * 1e-6) / 1e9
     achieved_survey = survey_step * E / (kern_us * 1e-6) / 1e9
-    traffic, traffic_src = (pmc_traffic(args.workload, args.precision)
-                            if E == WORKLOADS[args.workload][1] and args.physics == "pyb" else (None, None))
+    default_cfg = E == WORKLOADS[args.workload][1] and args.physics == "pyb"
+    rec, rec_why = counter_record(f"{args.workload}_{args.precision}") if default_cfg else ({}, "not a default workload")
+    traffic = rec.get("traffic_bytes_per_launch")
     kname = kernel_name(b)
+    # the same kernel with SB3's terminal observations requested (the synced reset path: the headline's sync-free
+    # one does not write info["terminal_observation"])
+    term_leg = None
+    if not args.no_extras:
+        nt = min(200, args.steps)
+        for _ in range(10):
+            b.step(random_actions=True, autoreset=True, terminal_obs=True)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(nt):
+            b.step(random_actions=True, autoreset=True, terminal_obs=True)
+        torch.cuda.synchronize()
+        dt1 = time.perf_counter() - t1
+        term_leg = {"env_steps_per_s": E * world * nt / dt1, "ms_per_step": dt1 / nt * 1e3, "steps": nt,
+                    "note": "ch_step with terminal_obs (SB3 info['terminal_observation'] written for every auto-reset): "
+                            "the VecEnv / rollout-buffer path; the headline value is the sync-free path without it"}
+    wg = rec.get("wg_trace") or {}
 
     out = None
     if rank == 0:
@@ -406,32 +485,49 @@ def main():
             "vs_baseline": None, "dtype": args.precision, "agent_steps_per_s": value * n,
             "data": "synthetic: Philox4x32 random VEL actions in-kernel, spawn table from config/cattle_positions.yaml; "
                     f"envs burnt in for {args.burn_in} untimed steps before the warmup (steady-state episode phases, "
-                    "auto-resets inside the timed steps at their long-run rate)",
+                    "auto-resets inside the timed steps at their long-run rate); headline without SB3 terminal "
+                    "observations (terminal_obs=False, the sync-free auto-reset path), the terminal-observation path in "
+                    "terminal_obs_leg",
             "launch": f"HIP graph of {chunk} steps per replay" if graph is not None else "one host launch per step",
             "rollout_end_us": rollout_end_us,
             "config": {"workload": desc, "envs_per_gpu": E, "num_drones": n, "num_cattle": m, "mode": mode,
                        "physics": args.physics,
                        "parallelism": f"env-sharded x{world} (no per-step collective)"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            # The kernel moves a few MB per launch and is bound by the latency of its dependent fp64 chains (the drone
+            # wave's action -> PID -> 4 substeps -> bookkeeping), not by HBM or VALU throughput: the
+            # HBM fraction is reported against 8 TB/s as the north_star asks, the chain/workgroup cycles beside it.
+            "roofline": {"bound": "latency", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_source": traffic_src, "algorithmic_bytes_per_launch": bytes_step * E,
+                         "traffic_source": rec.get("source") or rec_why, "code_object": rec.get("code_object"),
+                         "algorithmic_bytes_per_launch": bytes_step * E,
                          "kernel": kname, "kernel_us": kern_us, "bytes_per_env_step": bytes_step,
+                         "traffic_over_algorithmic": (traffic / (bytes_step * E)) if traffic else None,
+                         "latency": ({"chain_cycles": wg.get("chain_cycles_q50"), "wg_cycles_q50": wg.get("wg_cycles_q50"),
+                                      "wg_cycles_max": wg.get("wg_cycles_max"), "chain_over_wg": wg.get("chain_over_wg"),
+                                      "post_chain_cycles": wg.get("post_chain_cycles"),
+                                      "source": "tools/wg_trace.py --json (per-workgroup shader-clock phase stamps)"}
+                                     if wg else None),
                          "byte_model": "this layout: f64 state, Euler cache, eval accumulators, flags, the obs "
                                        "entries a step changes (bench.py algorithmic_bytes)"},
             "roofline_survey": {"bound": "hbm", "achieved": achieved_survey, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                 "frac": achieved_survey / HBM_PEAK_GBS, "bytes_per_env_step": survey_step,
                                 "algorithmic_bytes_per_launch": survey_step * E, "kernel_us": kern_us,
                                 "byte_model": "SURVEY.md 8(d): fp32 SoA, minimal carried state, full obs block"},
-            "valu": (valu_issue(args.workload, args.precision, kern_us)
-                     if E == WORKLOADS[args.workload][1] and args.physics == "pyb" else None),
+            "valu": valu_issue(rec, args.precision, kern_us) if rec else None,
+            "terminal_obs_leg": term_leg,
             "rollout_metrics": {"episodes": mv[1], "mean_return": (mv[2] / mv[1]) if mv[1] else None,
                                 "nan_rewards": mv[6], "terminated": mv[4], "truncated": mv[5]},
         }
+        fr, fr_why = counter_record("flock_roofline")
+        out["flock_roofline"] = fr.get("records") and {k: fr[k] for k in ("records", "flop_model", "peak_tflops", "note",
+                                                                         "source") if k in fr} or fr_why
         if args.policy and mode == "ctde":
             out["policy_rollout"] = policy_rollout(b, n, args.steps, args.warmup)
         if args.marl_vec and mode == "marl":
             b.close()
             out["marl_vec_env"] = marl_vec_rollout(n, m, E, args.steps, args.warmup, args.burn_in)
+        if not args.no_extras and world == 1:
+            out["host_surfaces"] = host_surfaces(args.steps)
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(mode, n, m, args.cpu_seconds)
         elif world == 1:

@@ -152,6 +152,31 @@ typedef struct ch_step_io {
  * (rllib_envs/marl_wrapper.py:77-119). */
 int ch_step(ch_handle* h, const ch_step_io* io, void* stream);
 
+/* Host delivery of one step's outputs (the batched SB3 VecEnv and RLlib dict surfaces).
+ * Replaces: what SubprocVecEnv.step_wait gathers from its worker processes -- obs (E, R, 86), rewards,
+ * dones, and for the envs that ended info["terminal_observation"] and Monitor's info["episode"]
+ * (CTDECattleHerder.py:91-99) -- and the arrays RLlibMultiAgentWrapper.step builds its per-agent dicts from
+ * (marl_wrapper.py:97-119).  After ch_step on `stream`: copies the step's outputs from io's device buffers
+ * into caller-owned host buffers (pinned host memory for full speed), then synchronises `stream`.
+ *   - The observation copy moves only the first num_drones rows of every block: a CTDE (12, 86) block's rows
+ *     >= num_drones are always zero, so the caller zero-fills `obs` once and they stay zero.
+ *   - The envs that auto-reset in the step (io->reset_happened) are compacted on the device, in ascending env
+ *     order: their count, indices, terminal observations (io->terminal_obs, whole blocks) and episode statistics
+ *     (io->episode_stats: return, length).  One synchronisation when at most 64 envs ended, two otherwise. */
+typedef struct ch_host_out {
+    float* obs;                /* host [E][R][86] (required) */
+    float* reward;             /* host [E][K] (required) */
+    uint8_t* terminated;       /* host [E][K] (required) */
+    uint8_t* truncated;        /* host [E][K] (required) */
+    uint8_t* reset_happened;   /* optional host [E] (needs io->reset_happened) */
+    uint8_t* agent_active;     /* optional host [E][N] (needs io->agent_active) */
+    int64_t ended_count;       /* out: envs that auto-reset in the step (needs io->reset_happened) */
+    int64_t* ended_env;        /* optional host [E]: their indices, ascending */
+    float* ended_obs;          /* optional host [E][R][86]: their terminal observations (needs io->terminal_obs) */
+    double* ended_stats;       /* optional host [E][2]: their episode return and length (needs io->episode_stats) */
+} ch_host_out;
+int ch_outputs_to_host(ch_handle* h, const ch_step_io* io, ch_host_out* out, void* stream);
+
 /* Full SoA state, for checkpoint/resume and parity state-injection.  Layout of the two host
  * buffers (counts from ch_state_size):
  *   doubles: drone[22][E][N] (px py pz qx qy qz qw vx vy vz wx wy wz pid_last_rpy[3]

@@ -25,7 +25,7 @@ EXPORTS = ("ch_default_config", "ch_create", "ch_destroy", "ch_last_error", "ch_
            "ch_state_size", "ch_get_state", "ch_set_state", "ch_metrics", "ch_metrics_device", "ch_sync",
            "ch_get_eval", "ch_builtin_spawn_table", "ch_rollout_store", "ch_rollout_post", "ch_rollout_gae", "ch_rollout_collect",
            "ch_spawn_table", "ch_mlp_forward", "ch_mlp_forward_masked", "ch_policy_forward", "ch_mlp_packed_size",
-           "ch_mlp_pack")
+           "ch_mlp_pack", "ch_outputs_to_host")
 CH_ACT_NONE, CH_ACT_TANH, CH_ACT_RELU = 0, 1, 2
 
 
@@ -46,6 +46,13 @@ class ChStepIO(ctypes.Structure):
                 ("terminal_obs", ctypes.c_void_p), ("agent_active", ctypes.c_void_p),
                 ("reset_happened", ctypes.c_void_p), ("flags", ctypes.c_uint32), ("_pad", ctypes.c_uint32),
                 ("episode_stats", ctypes.c_void_p)]
+
+
+class ChHostOut(ctypes.Structure):
+    _fields_ = [("obs", ctypes.c_void_p), ("reward", ctypes.c_void_p), ("terminated", ctypes.c_void_p),
+                ("truncated", ctypes.c_void_p), ("reset_happened", ctypes.c_void_p), ("agent_active", ctypes.c_void_p),
+                ("ended_count", ctypes.c_int64), ("ended_env", ctypes.c_void_p), ("ended_obs", ctypes.c_void_p),
+                ("ended_stats", ctypes.c_void_p)]
 
 
 class ChMlp(ctypes.Structure):
@@ -98,6 +105,7 @@ def lib():
     L.ch_policy_forward.argtypes = [vp, P(ChMlp), vp, vp, vp]
     L.ch_mlp_packed_size.argtypes = [P(ChMlp)]
     L.ch_mlp_pack.argtypes = [P(ChMlp), vp, vp]
+    L.ch_outputs_to_host.argtypes = [vp, P(ChStepIO), P(ChHostOut), vp]
     for name in EXPORTS:
         if name not in ("ch_last_error",):
             getattr(L, name).restype = ctypes.c_int
@@ -117,6 +125,28 @@ def default_config(mode, num_drones, num_cattle):
     c = ChConfig()
     check(lib().ch_default_config(ctypes.byref(c), mode, num_drones, num_cattle))
     return c
+
+
+def code_object_hash(path=None):
+    """sha256 (hex, first 16 digits) of the device code in libcattleherd.so: the ``.hip_fatbin`` ELF section
+    that holds the gfx950 code objects.  Host-side code and build paths do not enter it, so a rebuild of the same
+    kernel sources with the same compiler and flags gives the same hash.  bench.py accepts a committed counter
+    record (profiles/counters/) only for the code object it was measured on."""
+    import hashlib
+    import struct
+    with open(path or LIB_PATH, "rb") as fh:
+        data = fh.read()
+    if data[:4] != b"\x7fELF" or data[4] != 2:
+        raise ValueError("not an ELF64 file")
+    shoff, = struct.unpack_from("<Q", data, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
+    sec = [struct.unpack_from("<IIQQQQ", data, shoff + i * shentsize) for i in range(shnum)]
+    stro = sec[shstrndx][4]
+    for name, _typ, _flags, _addr, off, size in sec:
+        end = data.index(b"\0", stro + name)
+        if data[stro + name:end] == b".hip_fatbin":
+            return hashlib.sha256(data[off:off + size]).hexdigest()[:16]
+    raise ValueError("no .hip_fatbin section")
 
 
 def spawn_table(cows):

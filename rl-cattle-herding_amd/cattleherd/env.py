@@ -94,6 +94,7 @@ class HerdBatch:
         self._dev_index = dev_index
         self._actions_ptr = self.actions.data_ptr()
         self._terminal_ptr = self.terminal_obs.data_ptr()
+        self._last_obs_out = None   # weakref of the last obs_out tensor stepped into
 
     # ------------------------------------------------------------------------------------------
     def _stream(self):
@@ -138,6 +139,14 @@ class HerdBatch:
             if (obs_out.dtype != self.torch.float32 or obs_out.device != self.device or not obs_out.is_contiguous()
                     or tuple(obs_out.shape) != tuple(self.obs.shape)):
                 raise ValueError(f"obs_out must be a contiguous float32 {tuple(self.obs.shape)} tensor on {self.device}")
+            # The kernels recognise the buffer holding an env's constant-zero bytes by its address.  A new tensor can
+            # reuse the address of one written earlier (torch's caching allocator) while holding other data, so any
+            # tensor other than the last obs_out makes the next step write every block in full.
+            last = self._last_obs_out() if self._last_obs_out is not None else None
+            if last is not obs_out:
+                self.invalidate_obs()
+                import weakref
+                self._last_obs_out = weakref.ref(obs_out)
             io.obs = obs_out.data_ptr()
             try:
                 _, rew, te, tr = self.step(actions, autoreset, random_actions, terminal_obs)
@@ -164,6 +173,11 @@ class HerdBatch:
         if rc:
             L.check(rc, self.handle)
         return self.obs, self.reward, self.terminated, self.truncated
+
+    def host_outputs(self, ring=2, ended=True, agents=False):
+        """A HostOutputs over this batch: pinned host buffers the last step's outputs are delivered into
+        (ch_outputs_to_host), ``ring`` sets of them used in turn."""
+        return HostOutputs(self, ring=ring, ended=ended, agents=agents)
 
     def step_policy(self, policy, autoreset=True, terminal_obs=False):
         """One step with the actions of an on-device policy (cattleherd.policy.DevicePolicy) for the
@@ -312,3 +326,54 @@ class HerdBatch:
             self.close()
         except Exception:
             pass
+
+
+class HostOutputs:
+    """Pinned host copies of a HerdBatch's step outputs, filled by one ``ch_outputs_to_host`` call per step.
+
+    This is what SubprocVecEnv.step_wait gathers from its workers (CTDECattleHerder.py:91-99) and what
+    RLlibMultiAgentWrapper.step builds its dicts from (marl_wrapper.py:97-119).  ``ring`` sets of buffers are
+    used in turn, so the arrays of the last ``ring - 1`` deliveries stay valid while the next one is filled
+    (SB3's collect_rollouts reads the previous step's observation after the next env.step).  The observation
+    copy moves only the first num_drones rows of every block; the rest of a CTDE block is always zero and the
+    host buffers are zeroed once here."""
+
+    def __init__(self, batch, ring=2, ended=True, agents=False):
+        import torch
+        self.batch, self.ring, self._k = batch, max(1, int(ring)), -1
+        E, R, K, N = batch.n_envs, batch.obs_rows, batch.reward_cols, batch.num_drones
+        pin = dict(pin_memory=True)
+        self._sets = []
+        for _ in range(self.ring):
+            s = {"obs": torch.zeros((E, R, 86), dtype=torch.float32, **pin),
+                 "reward": torch.zeros((E, K), dtype=torch.float32, **pin),
+                 "terminated": torch.zeros((E, K), dtype=torch.uint8, **pin),
+                 "truncated": torch.zeros((E, K), dtype=torch.uint8, **pin),
+                 "reset_happened": torch.zeros(E, dtype=torch.uint8, **pin)}
+            if agents:
+                s["agent_active"] = torch.zeros((E, N), dtype=torch.uint8, **pin)
+            if ended:
+                s["ended_env"] = torch.zeros(E, dtype=torch.int64, **pin)
+                s["ended_obs"] = torch.zeros((E, R, 86), dtype=torch.float32, **pin)
+                s["ended_stats"] = torch.zeros((E, 2), dtype=torch.float64, **pin)
+            out = L.ChHostOut()
+            for k, t in s.items():
+                setattr(out, k, t.data_ptr())
+            self._sets.append((s, {k: t.numpy() for k, t in s.items()}, out))
+        self.ended = ended
+
+    def fetch(self):
+        """Deliver the last step's outputs (synchronises the batch's stream).  Returns a dict of numpy arrays
+        (views of this delivery's pinned buffers): obs, reward, terminated, truncated, reset_happened
+        (+ agent_active) and, for the envs that auto-reset in the step, ``ended_env`` (ascending),
+        ``ended_obs`` (their terminal observations) and ``ended_stats`` (episode return, length)."""
+        b = self.batch
+        self._k = (self._k + 1) % self.ring
+        _, arrs, out = self._sets[self._k]
+        L.check(L.lib().ch_outputs_to_host(b.handle, b._io_ref, ctypes.byref(out), b._stream()), b.handle)
+        res = dict(arrs)
+        if self.ended:
+            n = int(out.ended_count)
+            res["ended_env"], res["ended_obs"], res["ended_stats"] = (arrs["ended_env"][:n], arrs["ended_obs"][:n],
+                                                                      arrs["ended_stats"][:n])
+        return res

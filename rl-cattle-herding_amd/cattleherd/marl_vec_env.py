@@ -101,46 +101,74 @@ class CattleHerdMultiAgentVecEnv:
                 "terminated": b.terminated.view(torch.bool), "truncated": b.truncated.view(torch.bool),
                 "agents_before": before, "agents": self._before, "all_done": reset}
 
+    def _builders(self):
+        """Per agent count: functions that build one dict per env from per-agent columns with a dict display (the
+        fastest way CPython builds a small dict), for the envs whose agents are all live."""
+        if getattr(self, "_mk", None) is None:
+            ks = ", ".join(f"{str(k)!r}: a{i}" for i, k in enumerate(self._ids))
+            args = ", ".join(f"a{i}" for i in range(self.num_drones))
+            cols = ", ".join(f"c{i}" for i in range(self.num_drones))
+            self._mk = eval(f"lambda {cols}: [{{{ks}}} for {args}, in zip({cols})]")   # noqa: S307 (built from agent ids)
+            self._mk_all = eval(f"lambda {cols}, al: [{{{ks}, '__all__': z}} for {args}, z in zip({cols}, al)]")   # noqa: S307
+        return self._mk, self._mk_all
+
     def step(self, action_dicts):
         """RLlibMultiAgentWrapper.step (marl_wrapper.py:77-119) for every env: ``action_dicts`` is a list of
         {agent_id: action} dicts (or an array [E, N, 4]); returns lists of per-env obs, rewards, dones, truncs
-        and infos dicts keyed by the agents live at the start of the step, with ``"__all__"``."""
+        and infos dicts keyed by the agents live at the start of the step, with ``"__all__"``.
+
+        One launch, one ch_outputs_to_host into pinned buffers (observations, rewards, flags, the agent masks and
+        the envs reset, with their terminal observations compacted on the device), then the dicts: built from
+        per-agent columns for the envs whose agents were all live, trimmed to the live agents elsewhere.  The
+        observation arrays are views of one fresh copy per step.  Every agent's info is the reference's
+        ``{"answer": 42}`` (_computeInfo): one dict per step shared by all agents of all envs."""
         b = self.batch
         torch = b.torch
+        E, N = self.num_envs, self.num_drones
         if isinstance(action_dicts, (list, tuple)):
-            a = np.zeros((self.num_envs, self.num_drones, 4), np.float32)
+            a = np.zeros((E, N, 4), np.float32)
             for e, d in enumerate(action_dicts):
                 for aid, act in d.items():
                     a[e, int(str(aid).split("_")[1])] = np.asarray(act, np.float32)
-            acts = torch.from_numpy(a).to(b.device)
+            acts = torch.from_numpy(a).to(b.device, non_blocking=True)
         else:
-            acts = torch.as_tensor(np.asarray(action_dicts, np.float32), device=b.device)
+            acts = torch.as_tensor(np.asarray(action_dicts, np.float32)).to(b.device, non_blocking=True)
         live = self._active
-        out = self.step_tensors(acts)
-        obs = out["obs"].cpu().numpy()
-        rew = out["reward"].cpu().numpy().astype(np.float64)
-        te = out["terminated"].cpu().numpy()
-        tr = out["truncated"].cpu().numpy()
-        ended = out["all_done"].cpu().numpy()
-        self._active = out["agents"].cpu().numpy()
-        obs_l, rew_l, done_l, trunc_l, info_l = [], [], [], [], []
-        for e in range(self.num_envs):
-            idx = np.nonzero(live[e])[0]
-            keys = self._ids[idx]
-            obs_l.append(dict(zip(keys, obs[e, idx])))
-            rew_l.append(dict(zip(keys, rew[e, idx].tolist())))
-            d = dict(zip(keys, te[e, idx].tolist()))
-            t = dict(zip(keys, tr[e, idx].tolist()))
-            # the agents that terminated drop out (marl_wrapper.py:113); __all__ when none is left (116-117),
-            # which is exactly when the kernel reset the env
-            d["__all__"] = t["__all__"] = bool(ended[e])
-            done_l.append(d)
-            trunc_l.append(t)
-            info_l.append({k: {"answer": 42} for k in keys})
-        self._reset_envs = set(np.nonzero(ended)[0].tolist())
-        if self._reset_envs:
+        if self._before is None:
+            raise RuntimeError("call reset() first")
+        b.step(acts, autoreset=True, terminal_obs=True)
+        self._before = b.agent_active.view(torch.bool).clone()
+        if getattr(self, "_host", None) is None:
+            self._host = b.host_outputs(ring=2, ended=True, agents=True)
+        h = self._host.fetch()
+        obs = h["obs"].copy()
+        ended_env = h["ended_env"]
+        ended = h["reset_happened"].astype(bool)
+        if len(ended_env):
+            # the dicts carry the episode's last observation; reset_at() hands out the new episode's
+            self._reset_obs = {int(e): obs[e].copy() for e in ended_env}
+            obs[ended_env] = h["ended_obs"]
+        self._reset_envs = set(self._reset_obs) if len(ended_env) else set()
+        mk, mk_all = self._builders()
+        al = ended.tolist()
+        obs_l = mk(*[list(obs[:, i]) for i in range(N)])
+        rew_l = mk(*h["reward"].astype(np.float64).T.tolist())
+        done_l = mk_all(*h["terminated"].astype(bool).T.tolist(), al)
+        trunc_l = mk_all(*h["truncated"].astype(bool).T.tolist(), al)
+        info = {"answer": 42}
+        info_l = mk(*([[info] * E] * N))
+        # envs with agents that were not live at the start of the step: only the live agents' keys
+        part = np.nonzero(~live.all(axis=1))[0]
+        if len(part):
+            ids = self._ids
+            for e in part.tolist():
+                for i in np.nonzero(~live[e])[0].tolist():
+                    k = ids[i]
+                    for dl in (obs_l, rew_l, done_l, trunc_l, info_l):
+                        del dl[e][k]
+        self._active = h["agent_active"].astype(bool)
+        if len(ended_env):
             self._n = np.where(ended, self._active.sum(1), self._n)   # every agent of a new episode is live
-            self._reset_obs = b.obs.cpu().numpy()
         return obs_l, rew_l, done_l, trunc_l, info_l
 
     def reset_at(self, e):
@@ -149,7 +177,8 @@ class CattleHerdMultiAgentVecEnv:
         if e not in self._reset_envs:
             raise ValueError(f"env {e} did not finish an episode in the last step")
         n = int(self._n[e])
-        return self._obs_dict(self._reset_obs[e], n), {self._ids[i]: {} for i in range(n)}
+        obs = self._reset_obs[e] if isinstance(self._reset_obs, dict) else self._reset_obs[e]
+        return self._obs_dict(obs, n), {self._ids[i]: {} for i in range(n)}
 
     def close(self):
         self.batch.close()

@@ -29,10 +29,18 @@ def load_sb3_state_dict(path):
 class DevicePolicy:
     """A dense MLP (1-4 layers, widths <= 256) evaluated by ``ch_mlp_forward``.
 
-    ``layers``: list of (weight [out, in], bias [out] or None) tensors in ``nn.Linear`` layout;
-    ``hidden_act`` after every layer but the last; ``clip`` = (lo, hi) or None on the output."""
+    ``layers``: list of (weight [out, in], bias [out] or None) tensors in ``nn.Linear`` layout (device float32
+    contiguous tensors are used in place, so a torch optimizer updating them updates this policy);
+    ``hidden_act`` after every layer but the last; ``clip`` = (lo, hi) or None on the output.
 
-    def __init__(self, layers, hidden_act="tanh", clip=None, device=None, splits=None):
+    The kernel reads the weights from a packed copy in its operand layout (biases are read in place).
+    ``cache_packed=False`` (default) re-packs before every forward and collection, so any update of the weights
+    -- ``optimizer.step()``, ``param.data.copy_()``, a Polyak average through ``.data`` -- is seen.
+    ``cache_packed=True`` re-packs only when a weight tensor's version counter moves (``optimizer.step()`` and
+    other in-place ops on the tensors themselves bump it; writes through ``.data`` or another alias do not): for
+    frozen weights, e.g. rolling out a trained model; call ``pack()`` after any other update."""
+
+    def __init__(self, layers, hidden_act="tanh", clip=None, device=None, splits=None, cache_packed=False):
         import torch
         if not torch.cuda.is_available():
             raise RuntimeError("DevicePolicy needs a ROCm GPU; there is no CPU fallback")
@@ -67,8 +75,9 @@ class DevicePolicy:
             net.split_out[i], net.split_in[i] = int(so), int(si)
         self.splits = dict(splits or {})
         self._net = net
-        # the weights in the kernel's operand layout (ch_mlp_pack), re-packed whenever a weight or bias tensor
-        # was modified in place since (torch's per-tensor version counter): the forward reads this copy
+        # the weights in the kernel's operand layout (ch_mlp_pack): the forward reads this copy (and the biases in
+        # place); re-packed before every forward, or with cache_packed only when a weight tensor's version moved
+        self.cache_packed = bool(cache_packed)
         n = L.lib().ch_mlp_packed_size(ctypes.byref(net))
         self._packed = torch.empty(max(int(n), 4), dtype=torch.float32, device=self.device)
         self._packed_at = None
@@ -78,33 +87,33 @@ class DevicePolicy:
         return tuple(w._version for w in self.weights)
 
     def pack(self):
-        """Re-pack the weights now (on the current stream); forward() does it by itself after in-place updates."""
+        """Re-pack the weights now (on the current stream)."""
         L.check(L.lib().ch_mlp_pack(ctypes.byref(self._net), ctypes.c_void_p(self._packed.data_ptr()), self._stream()))
         self._packed_at = self._versions()
 
     def _ensure_packed(self):
-        if self._packed_at != self._versions():
+        if not self.cache_packed or self._packed_at != self._versions():
             self.pack()
 
     # ---- constructors for the reference's models ------------------------------------------------
     @classmethod
-    def sb3_actor(cls, state_dict, device=None, clip=True):
+    def sb3_actor(cls, state_dict, device=None, clip=True, cache_packed=False):
         """Deterministic SB3 ActorCriticPolicy action: policy_net (tanh) -> action_net, clipped to [-1, 1]
         (``clip=False``: the Gaussian mean, for stochastic rollouts, cattleherd.rollout)."""
         sd = state_dict
         layers = [(sd["mlp_extractor.policy_net.0.weight"], sd["mlp_extractor.policy_net.0.bias"]),
                   (sd["mlp_extractor.policy_net.2.weight"], sd["mlp_extractor.policy_net.2.bias"]),
                   (sd["action_net.weight"], sd["action_net.bias"])]
-        return cls(layers, "tanh", (-1.0, 1.0) if clip else None, device)
+        return cls(layers, "tanh", (-1.0, 1.0) if clip else None, device, cache_packed=cache_packed)
 
     @classmethod
-    def sb3_critic(cls, state_dict, device=None):
+    def sb3_critic(cls, state_dict, device=None, cache_packed=False):
         """SB3 ActorCriticPolicy.predict_values: value_net on the tanh value MLP."""
         sd = state_dict
         layers = [(sd["mlp_extractor.value_net.0.weight"], sd["mlp_extractor.value_net.0.bias"]),
                   (sd["mlp_extractor.value_net.2.weight"], sd["mlp_extractor.value_net.2.bias"]),
                   (sd["value_net.weight"], sd["value_net.bias"])]
-        return cls(layers, "tanh", None, device)
+        return cls(layers, "tanh", None, device, cache_packed=cache_packed)
 
     @classmethod
     def sb3_actor_critic(cls, state_dict, device=None):

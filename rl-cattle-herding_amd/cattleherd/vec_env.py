@@ -2,7 +2,8 @@
 
 Drop-in for ``make_vec_env(CattleAviary, n_envs=..., vec_env_cls=SubprocVecEnv)``
 (simulator/CTDECattleHerder.py:91-97): ``CattleHerdVecEnv(n_envs, num_drones=..., num_cattle=...)``
-returns numpy observations ``(E, 12, 86)``, rewards ``(E,)``, dones ``(E,)`` and per-env infos with
+returns numpy observations ``(E, 12, 86)`` (valid until the step after next: two pinned host buffers are used in
+turn), rewards ``(E,)``, dones ``(E,)`` and per-env infos with
 SB3's ``terminal_observation`` / ``TimeLimit.truncated`` keys and, as the Monitor that ``make_vec_env``
 wraps around every env (CTDECattleHerder.py:91-99) adds, ``episode = {"r", "l", "t"}`` for each episode that
 ends, auto-resetting finished envs inside the step launch.  ``step_tensors`` is the zero-copy path for
@@ -40,6 +41,12 @@ class CattleHerdVecEnv(_VecEnvBase):
                        "CTRL_TIMESTEP": 1.0 / self.batch.cfg.ctrl_freq, "NUM_DRONES": num_drones,
                        "is_evaluating": False}
         self._t_start = time.time()
+        # host delivery: pinned buffers filled by one ch_outputs_to_host per step (two sets used in turn, so the
+        # observation array returned by a step stays valid through the next step, as SB3's collect_rollouts needs)
+        self._host = self.batch.host_outputs(ring=2, ended=True)
+        # one info dict per env, reused: only the envs that end in a step get (and next time lose) the extra keys
+        self._infos = [{"answer": 42} for _ in range(n_envs)]
+        self._dirty = []
         if _VecEnvBase is not object:  # SB3 bookkeeping
             _VecEnvBase.__init__(self, n_envs, self.observation_space, self.action_space)
 
@@ -49,36 +56,54 @@ class CattleHerdVecEnv(_VecEnvBase):
 
     # ---- VecEnv API --------------------------------------------------------------------------
     def reset(self):
+        for e in self._dirty:
+            for k in ("terminal_observation", "TimeLimit.truncated", "episode"):
+                self._infos[e].pop(k, None)
+        self._dirty = []
         return self.batch.reset().cpu().numpy()
 
     def step_async(self, actions):
         self._actions = actions
 
     def step_wait(self):
+        """SubprocVecEnv.step_wait over the batch: one launch, then one ch_outputs_to_host (the first num_drones rows
+        of every observation block, reward and flags, and the terminal observations / episode statistics of the
+        envs that auto-reset, compacted on the device) into pinned buffers and a stream sync."""
         a = self._actions
         torch = self.batch.torch
         if not isinstance(a, torch.Tensor):
-            a = np.asarray(a, np.float32).reshape(self.num_envs, -1, 4)[:, :self.num_drones]
-            a = torch.from_numpy(np.ascontiguousarray(a)).to(self.batch.device)
-        obs, rew, te, tr = self.batch.step(a, autoreset=True, terminal_obs=True)
-        obs_np = obs.cpu().numpy()
-        rew_np = rew[:, 0].cpu().numpy().astype(np.float32)
-        te_np = te[:, 0].cpu().numpy().astype(bool)
-        tr_np = tr[:, 0].cpu().numpy().astype(bool)
+            # numpy actions through a pinned staging buffer (the previous step's copy out of it has completed: the
+            # delivery below synchronises the stream)
+            if getattr(self, "_act_pin", None) is None:
+                self._act_pin = torch.zeros((self.num_envs, self.num_drones, 4), dtype=torch.float32).pin_memory()
+                self._act_np = self._act_pin.numpy()
+            np.copyto(self._act_np, np.asarray(a, np.float32).reshape(self.num_envs, -1, 4)[:, :self.num_drones])
+            a = self._act_pin.to(self.batch.device, non_blocking=True)
+        self.batch.step(a, autoreset=True, terminal_obs=True)
+        h = self._host.fetch()
+        rew_np = h["reward"][:, 0].copy()
+        te_np = h["terminated"][:, 0].astype(bool)
+        tr_np = h["truncated"][:, 0].astype(bool)
         dones = te_np | tr_np
-        infos = [{"answer": 42} for _ in range(self.num_envs)]
-        idx = np.nonzero(dones)[0]
+        infos = self._infos
+        for e in self._dirty:   # the keys the last step added
+            d = infos[e]
+            d.pop("terminal_observation", None)
+            d.pop("TimeLimit.truncated", None)
+            d.pop("episode", None)
+        idx = h["ended_env"]
+        self._dirty = idx.tolist()
         if len(idx):
-            term_obs = self.batch.terminal_obs[idx].cpu().numpy()
-            # Monitor.step: the episode's summed float64 reward and length, kept on the device by the step
-            # kernel (ch_step_io.episode_stats), and the wall time since the Monitor started
-            stats = self.batch.episode_stats[idx].cpu().numpy()
+            # Monitor.step: the episode's summed float64 reward and length, kept on the device by the step kernel
+            # (ch_step_io.episode_stats), and the wall time since the Monitor started
             t = round(time.time() - self._t_start, 6)
-            for k, e in enumerate(idx):
-                infos[e]["terminal_observation"] = term_obs[k]
-                infos[e]["TimeLimit.truncated"] = bool(tr_np[e] and not te_np[e])
-                infos[e]["episode"] = {"r": round(float(stats[k, 0]), 6), "l": int(stats[k, 1]), "t": t}
-        return obs_np, rew_np, dones, infos
+            term_obs, stats = h["ended_obs"], h["ended_stats"]
+            for k, e in enumerate(self._dirty):
+                d = infos[e]
+                d["terminal_observation"] = term_obs[k].copy()
+                d["TimeLimit.truncated"] = bool(tr_np[e] and not te_np[e])
+                d["episode"] = {"r": round(float(stats[k, 0]), 6), "l": int(stats[k, 1]), "t": t}
+        return h["obs"], rew_np, dones, list(infos)
 
     def step(self, actions):
         self.step_async(actions)

@@ -73,6 +73,18 @@ struct ch_handle {
     int* tv_count = nullptr;
     float* tv_val = nullptr;
     size_t tv_obs_n = 0, tv_val_n = 0;
+    // ch_rollout_collect's path (diagnostics / tests, ch__set_rollout_path): bit 0 copy every step's observation into
+    // the buffer instead of stepping into its slots, bit 1 the stand-alone store kernel instead of the forward epilogues
+    int rollout_path = 0;
+    // ch_outputs_to_host's device staging of the envs that auto-reset (allocated on first use): count, indices,
+    // episode statistics, terminal observation blocks; and the pinned host copy of the count
+    long long* st_count = nullptr;
+    long long* st_env = nullptr;
+    double* st_stats = nullptr;
+    float* st_obs = nullptr;
+    long long* st_count_host = nullptr;
+    // the device error word was reported to the caller (device_status) since it was last cleared
+    bool err_seen = false;
     std::string err;
 };
 
@@ -244,14 +256,17 @@ static void free_all(ch_handle* h) {
                     h->errw, h->mdev, h->stale, h->obs_tag, h->evald, h->rdn, h->rdv, h->pos64, h->cpos64, h->prev64};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
-    for (void* p : {(void*)h->tv_obs, (void*)h->tv_row, (void*)h->tv_count, (void*)h->tv_val})
+    for (void* p : {(void*)h->tv_obs, (void*)h->tv_row, (void*)h->tv_count, (void*)h->tv_val, (void*)h->st_count,
+                    (void*)h->st_env, (void*)h->st_stats, (void*)h->st_obs})
         if (p) (void)hipFree(p);
     if (h->mhost) (void)hipHostFree(h->mhost);
+    if (h->st_count_host) (void)hipHostFree(h->st_count_host);
 }
 
 // the sticky device error word as a status (call after the stream has drained)
 static int device_status(ch_handle* h, int word) {
     if (!word) return CH_OK;
+    h->err_seen = true;
     return fail(h, CH_ERR_DEVICE,
                 "device error word " + std::to_string(word) +
                     ((word & CH_DEVERR_HANDOFF) ? ": a step kernel's LDS hand-off timed out (ch_step.hip lds_wait); "
@@ -314,6 +329,11 @@ int ch_create(const ch_config* c, int64_t n_envs, int32_t device, ch_handle** ou
     h->rsize = c->precision == CH_PREC_F64 ? sizeof(double) : sizeof(float);
     h->P = h->M * (h->M - 1) / 2;
     (void)kLevelMin; (void)kLevelMax;
+    {   // ch_rollout_collect's path: the environment's choice, ch__set_rollout_path overrides it per handle
+        const char* v = getenv("CH_ROLLOUT_COPY");
+        const char* k = getenv("CH_ROLLOUT_STORE_KERNEL");
+        h->rollout_path = ((v && v[0] == '1') ? 1 : 0) | ((k && k[0] == '1') ? 2 : 0);
+    }
 
     auto cleanup = [&](int code) { free_all(h); std::string m = h->err; delete h; g_create_err = m; return code; };
 #define CTRY(expr)                                                                                  \
@@ -480,6 +500,24 @@ int ch_shape(const ch_handle* h, int64_t* n_envs, int32_t* obs_rows, int32_t* ob
     return CH_OK;
 }
 
+// A full reset rebuilds every env, so the results a failed hand-off spoiled are gone and the sticky device error word
+// is cleared.  The word is read first (a stream sync: full resets are rare): if it was set and no ch_sync /
+// ch_metrics / ch_get_state has reported it yet, the reset still happens but returns CH_ERR_DEVICE, so that the
+// failure of the steps before it is never lost silently.
+static int clear_error_word(ch_handle* h, hipStream_t st, const char* who) {
+    int word = 0;
+    HIP_TRY(h, hipStreamSynchronize(st));
+    HIP_TRY(h, hipMemcpy(&word, h->errw, sizeof(int), hipMemcpyDeviceToHost));
+    HIP_TRY(h, hipMemsetAsync(h->errw, 0, sizeof(int), st));
+    const bool unseen = word && !h->err_seen;
+    h->err_seen = false;
+    if (unseen)
+        return fail(h, CH_ERR_DEVICE, std::string(who) + ": the envs were reset, but the steps before it had set device "
+                                          "error word " + std::to_string(word) + " (never reported: the results of "
+                                          "those steps are wrong); the word is now cleared");
+    return CH_OK;
+}
+
 int ch_reset(ch_handle* h, const uint8_t* mask_dev, float* obs_dev, void* stream) {
     if (!h) return fail(nullptr, CH_ERR_INVALID, "ch_reset: NULL handle");
     if (!obs_dev) return fail(h, CH_ERR_INVALID, "ch_reset: obs is NULL");
@@ -498,10 +536,7 @@ int ch_reset(ch_handle* h, const uint8_t* mask_dev, float* obs_dev, void* stream
     if (e != hipSuccess) return fail(h, CH_ERR_DEVICE, std::string("ch_reset launch: ") + hipGetErrorString(e));
     if (!mask_dev) h->obs_zero_ptr = obs_dev;                    // every block written in full
     else if (h->obs_zero_ptr != obs_dev) h->obs_zero_ptr = nullptr;   // some blocks of obs_dev unknown
-    // a full reset rebuilds every env: the results a failed hand-off spoiled are gone, so the sticky device
-    // error word is cleared (the failure was reported by every ch_sync / ch_metrics / ch_get_state before it)
-    if (!mask_dev) HIP_TRY(h, hipMemsetAsync(h->errw, 0, sizeof(int), st));
-    return CH_OK;
+    return mask_dev ? CH_OK : clear_error_word(h, st, "ch_reset");
 }
 
 int ch_reset_with(ch_handle* h, const uint8_t* mask_dev, const int32_t* num_drones, const double* cow_vel,
@@ -537,11 +572,10 @@ int ch_reset_with(ch_handle* h, const uint8_t* mask_dev, const int32_t* num_dron
         e = launch_reset(p, h->team, st);
     }
     if (e != hipSuccess) return fail(h, CH_ERR_DEVICE, std::string("ch_reset_with launch: ") + hipGetErrorString(e));
-    if (!mask_dev) HIP_TRY(h, hipMemsetAsync(h->errw, 0, sizeof(int), st));   // as ch_reset
     HIP_TRY(h, hipStreamSynchronize(st));   // the host arrays may be reused as soon as this returns
     if (!mask_dev) h->obs_zero_ptr = obs_dev;
     else if (h->obs_zero_ptr != obs_dev) h->obs_zero_ptr = nullptr;
-    return CH_OK;
+    return mask_dev ? CH_OK : clear_error_word(h, st, "ch_reset_with");   // as ch_reset
 }
 
 int ch_step(ch_handle* h, const ch_step_io* io, void* stream) {
@@ -577,10 +611,11 @@ int ch_step(ch_handle* h, const ch_step_io* io, void* stream) {
     }
     if (e != hipSuccess) return fail(h, CH_ERR_DEVICE, std::string("ch_step launch: ") + hipGetErrorString(e));
     h->obs_zero_ptr = (h->phase_mask & 8) ? nullptr : io->obs;
-    // The per-env "constant obs bytes unknown" flags (stale row 1) describe one buffer: the one the last step
-    // wrote.  A step into a different buffer than the previous step's leaves the other buffer's blocks behind
-    // (rows a reset episode no longer uses), so the flags are raised again: whatever the next step writes --
-    // this buffer, or the first one from a HIP graph captured earlier -- it writes every block in full.
+    // Which buffer holds each env's constant-zero obs bytes is also tracked on the device, per env: the step kernels
+    // record the address they wrote (StepParams::obs_tag) and write an env's block in full when the buffer they are
+    // given is not that one (k_step2 and k_env compare p.obs_tag[e] with p.obs), so a HIP graph captured on one
+    // buffer and replayed after steps into another stays exact.  A new tensor at a recycled address is the caller's
+    // to flag (HerdBatch.step(obs_out=...) calls invalidate_obs when the tensor changes).
     return CH_OK;
 }
 
@@ -723,6 +758,14 @@ int ch__obs_invalidate(ch_handle* h, void* stream) {
 // diagnostics: k_mlp2 writes wave 0's phase clocks of every workgroup to dev[blockIdx][16] (NULL: off)
 extern "C" int ch__set_mlp_tstamp(long long* dev) {
     g_mlp_tstamp = dev;
+    return CH_OK;
+}
+
+/* Internal (tests / diagnostics): ch_rollout_collect's path, bit 0 copy each step's observation into the buffer
+ * (CH_ROLLOUT_COPY=1), bit 1 the stand-alone store kernel instead of the forward epilogues (CH_ROLLOUT_STORE_KERNEL=1). */
+int ch__set_rollout_path(ch_handle* h, int32_t bits) {
+    if (!h || bits < 0 || bits > 3) return CH_ERR_INVALID;
+    h->rollout_path = bits;
     return CH_OK;
 }
 
@@ -961,7 +1004,7 @@ int ch_rollout_collect(ch_handle* h, const ch_rollout* rb, const ch_rollout_io* 
     // holds at most kTvEvery * E rows).  Per step that leaves two launches with separate nets (forwards with the
     // store in their epilogues, step) and three with a fused net or CH_ROLLOUT_STORE_KERNEL=1 (forward, store, step).
     constexpr int kTvEvery = 8;
-    static const bool copy_each = [] { const char* v = getenv("CH_ROLLOUT_COPY"); return v && v[0] == '1'; }();
+    const bool copy_each = (h->rollout_path & 1) != 0;
     const size_t slot = (size_t)h->E * (size_t)ra.obs_dim;
     auto obs_at = [&](int32_t t) { return (t == 0 || t == rb->n_steps || copy_each) ? sio->obs : rb->obs + (size_t)t * slot; };
     MlpArgs fa, fc, ftv;
@@ -1009,7 +1052,7 @@ int ch_rollout_collect(ch_handle* h, const ch_rollout* rb, const ch_rollout_io* 
     };
     MlpArgs segs[2];
     segs[0] = fa; segs[1] = fc;
-    static const bool no_epi = [] { const char* v = getenv("CH_ROLLOUT_STORE_KERNEL"); return v && v[0] == '1'; }();
+    const bool no_epi = (h->rollout_path & 2) != 0;
     if (!fused && !no_epi && mlp_multi_fits(segs, 2)) {
         // Two launches per step: the actor and critic forwards with the store folded into their epilogues (the
         // actor's samples its actions, log-probabilities and env actions; the critic's writes the values, the
@@ -1100,6 +1143,72 @@ int ch_get_eval(ch_handle* h, double* host_out, void* stream) {
     HIP_TRY(h, hipSetDevice(h->device));
     HIP_TRY(h, hipStreamSynchronize((hipStream_t)stream));
     HIP_TRY(h, hipMemcpy(host_out, h->evald, sizeof(double) * h->E * h->NC, hipMemcpyDeviceToHost));
+    return CH_OK;
+}
+
+int ch_outputs_to_host(ch_handle* h, const ch_step_io* io, ch_host_out* out, void* stream) {
+    if (!h) return fail(nullptr, CH_ERR_INVALID, "ch_outputs_to_host: NULL handle");
+    if (!io || !out || !io->obs || !io->reward || !io->terminated || !io->truncated || !out->obs || !out->reward ||
+        !out->terminated || !out->truncated)
+        return fail(h, CH_ERR_INVALID, "ch_outputs_to_host: obs, reward, terminated and truncated are required on both sides");
+    if ((out->reset_happened || out->ended_env || out->ended_obs || out->ended_stats) && !io->reset_happened)
+        return fail(h, CH_ERR_INVALID, "ch_outputs_to_host: the reset list needs io->reset_happened");
+    if ((out->ended_obs && !io->terminal_obs) || (out->ended_stats && !io->episode_stats))
+        return fail(h, CH_ERR_INVALID, "ch_outputs_to_host: ended_obs needs io->terminal_obs, ended_stats io->episode_stats");
+    if (out->agent_active && !io->agent_active)
+        return fail(h, CH_ERR_INVALID, "ch_outputs_to_host: agent_active needs io->agent_active");
+    HIP_TRY(h, hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t E = h->E;
+    const size_t blk = (size_t)h->rows * 86, live = (size_t)h->NC * 86;   // floats per block / in its first NC rows
+    if (io->reset_happened) {
+        if (!h->st_count) {
+            HIP_TRY(h, hipMalloc(&h->st_count, sizeof(long long)));
+            HIP_TRY(h, hipMalloc(&h->st_env, sizeof(long long) * E));
+            HIP_TRY(h, hipMalloc(&h->st_stats, sizeof(double) * 2 * E));
+            HIP_TRY(h, hipMalloc(&h->st_obs, sizeof(float) * blk * E));
+            HIP_TRY(h, hipHostMalloc(&h->st_count_host, sizeof(long long), hipHostMallocDefault));
+        }
+        HIP_TRY(h, launch_stage_ended(E, io->reset_happened, out->ended_obs ? io->terminal_obs : nullptr,
+                                      out->ended_stats ? io->episode_stats : nullptr, (int)blk, h->st_count, h->st_env,
+                                      h->st_stats, h->st_obs, st));
+        HIP_TRY(h, hipMemcpyAsync(h->st_count_host, h->st_count, sizeof(long long), hipMemcpyDeviceToHost, st));
+    }
+    // the first NC rows of every block (CTDE: rows >= NC are always zero; MARL: R = NC, one contiguous copy)
+    if (live == blk)
+        HIP_TRY(h, hipMemcpyAsync(out->obs, io->obs, sizeof(float) * blk * E, hipMemcpyDeviceToHost, st));
+    else
+        HIP_TRY(h, hipMemcpy2DAsync(out->obs, sizeof(float) * blk, io->obs, sizeof(float) * blk, sizeof(float) * live, E,
+                                    hipMemcpyDeviceToHost, st));
+    const size_t K = (size_t)h->K;
+    HIP_TRY(h, hipMemcpyAsync(out->reward, io->reward, sizeof(float) * K * E, hipMemcpyDeviceToHost, st));
+    HIP_TRY(h, hipMemcpyAsync(out->terminated, io->terminated, K * E, hipMemcpyDeviceToHost, st));
+    HIP_TRY(h, hipMemcpyAsync(out->truncated, io->truncated, K * E, hipMemcpyDeviceToHost, st));
+    if (out->reset_happened) HIP_TRY(h, hipMemcpyAsync(out->reset_happened, io->reset_happened, E, hipMemcpyDeviceToHost, st));
+    if (out->agent_active)
+        HIP_TRY(h, hipMemcpyAsync(out->agent_active, io->agent_active, (size_t)h->NC * E, hipMemcpyDeviceToHost, st));
+    // the ended envs' lists: a speculative first part (the usual case: a few envs end per step), the rest after the count
+    const int64_t cap = std::min<int64_t>(E, 64);
+    auto copy_ended = [&](int64_t lo, int64_t hi) -> int {
+        if (hi <= lo) return CH_OK;
+        if (out->ended_env)
+            HIP_TRY(h, hipMemcpyAsync(out->ended_env + lo, h->st_env + lo, sizeof(long long) * (hi - lo), hipMemcpyDeviceToHost, st));
+        if (out->ended_stats)
+            HIP_TRY(h, hipMemcpyAsync(out->ended_stats + 2 * lo, h->st_stats + 2 * lo, sizeof(double) * 2 * (hi - lo),
+                                      hipMemcpyDeviceToHost, st));
+        if (out->ended_obs)
+            HIP_TRY(h, hipMemcpyAsync(out->ended_obs + blk * lo, h->st_obs + blk * lo, sizeof(float) * blk * (hi - lo),
+                                      hipMemcpyDeviceToHost, st));
+        return CH_OK;
+    };
+    int rc = CH_OK;
+    if (io->reset_happened && (rc = copy_ended(0, cap))) return rc;
+    HIP_TRY(h, hipStreamSynchronize(st));
+    out->ended_count = io->reset_happened ? *h->st_count_host : 0;
+    if (out->ended_count > cap) {
+        if ((rc = copy_ended(cap, out->ended_count))) return rc;
+        HIP_TRY(h, hipStreamSynchronize(st));
+    }
     return CH_OK;
 }
 

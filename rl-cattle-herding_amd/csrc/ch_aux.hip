@@ -147,6 +147,57 @@ __global__ void k_rollout_gae(RolloutArgs a) {
     }
 }
 
+// ---- host delivery (ch_outputs_to_host): the envs that auto-reset in a step, compacted in ascending env order ------
+// One workgroup: each chunk of 1024 envs is ranked by wave ballots (lane prefix) and a scan of the 16 wave totals, so
+// the slots follow the env order; then the terminal observation blocks of the listed envs are copied into the
+// staging buffer (float4, whole blocks) by the whole workgroup.
+constexpr int kStageThreads = 1024;
+__global__ __launch_bounds__(kStageThreads) void k_stage_ended(long long E, const uint8_t* reset, const float* term_obs,
+                                                               const double* stats, int blk_floats, long long* count,
+                                                               long long* env_out, double* stats_out, float* obs_out) {
+    __shared__ long long wsum[kStageThreads / 64 + 1];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    long long base = 0;
+    for (long long c0 = 0; c0 < E; c0 += kStageThreads) {
+        const long long e = c0 + t;
+        const bool f = e < E && reset[e] != 0;
+        const unsigned long long m = __ballot(f);
+        if (lane == 0) wsum[w] = __popcll(m);
+        __syncthreads();
+        if (t == 0) {
+            long long s = 0;
+            for (int k = 0; k < kStageThreads / 64; ++k) { const long long v = wsum[k]; wsum[k] = s; s += v; }
+            wsum[kStageThreads / 64] = s;
+        }
+        __syncthreads();
+        if (f) {
+            const long long slot = base + wsum[w] + __popcll(m & ((1ull << lane) - 1ull));
+            env_out[slot] = e;
+            if (stats) { stats_out[2 * slot] = stats[2 * e]; stats_out[2 * slot + 1] = stats[2 * e + 1]; }
+        }
+        base += wsum[kStageThreads / 64];
+        __syncthreads();
+    }
+    if (t == 0) *count = base;
+    if (!term_obs) return;
+    __threadfence_block();
+    __syncthreads();
+    const int q = blk_floats / 2;   // float2 per block (R * 86 is even, so every block starts 8-byte aligned)
+    for (long long i = t; i < base * q; i += kStageThreads) {
+        const long long s = i / q, k = i - s * q;
+        reinterpret_cast<float2*>(obs_out + s * blk_floats)[k] =
+            reinterpret_cast<const float2*>(term_obs + env_out[s] * blk_floats)[k];
+    }
+}
+
+hipError_t launch_stage_ended(long long E, const uint8_t* reset, const float* term_obs, const double* stats,
+                              int blk_floats, long long* count, long long* env_out, double* stats_out, float* obs_out,
+                              hipStream_t st) {
+    hipLaunchKernelGGL(k_stage_ended, dim3(1), dim3(kStageThreads), 0, st, E, reset, term_obs, stats, blk_floats, count,
+                       env_out, stats_out, obs_out);
+    return hipGetLastError();
+}
+
 hipError_t launch_rollout(const RolloutArgs& a, int which, hipStream_t st) {
     if (which == 0)
         hipLaunchKernelGGL(k_rollout_store, dim3((unsigned)((a.rows + kRollThreads / 64 - 1) / (kRollThreads / 64))),

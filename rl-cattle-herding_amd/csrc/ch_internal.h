@@ -203,7 +203,11 @@ struct RolloutArgs {
     float *env_actions, *obs, *actions, *rewards, *episode_starts, *values, *log_probs, *advantages, *returns,
         *last_episode_starts;
 };
-hipError_t launch_rollout(const RolloutArgs& a, int which, hipStream_t st);   // 0 store, 1 post, 2 gae, 3 apply (cap slots)
+hipError_t launch_rollout(const RolloutArgs& a, int which, hipStream_t st);
+// ch_aux.hip: ch_outputs_to_host's compaction of the envs that auto-reset (ascending env order)
+hipError_t launch_stage_ended(long long E, const uint8_t* reset, const float* term_obs, const double* stats,
+                              int blk_floats, long long* count, long long* env_out, double* stats_out, float* obs_out,
+                              hipStream_t st);   // 0 store, 1 post, 2 gae, 3 apply (cap slots)
 
 // up to three independent forwards in one launch (ch_policy.hip k_mlp2).  A segment's role folds the rollout
 // store into its last layer's epilogue (ch_rollout_collect): kRoleSample -- the actor's mean becomes the

@@ -98,8 +98,27 @@ class FakeBatch:
     def invalidate_obs(self):
         pass
 
+    def host_outputs(self, ring=2, ended=True, agents=False):
+        return _FakeHostOutputs(self)
+
     def metrics(self, reset=False):
         return np.zeros(8)
 
     def close(self):
         pass
+
+
+class _FakeHostOutputs:
+    """HostOutputs.fetch() of the CPU stand-in: the same dict of numpy arrays, the reset envs listed ascending."""
+
+    def __init__(self, batch):
+        self.b = batch
+
+    def fetch(self):
+        b = self.b
+        idx = np.nonzero(b.reset_happened.numpy())[0]
+        return {"obs": b.obs.numpy().astype(np.float32), "reward": b.reward.numpy().astype(np.float32),
+                "terminated": b.terminated.numpy().copy(), "truncated": b.truncated.numpy().copy(),
+                "reset_happened": b.reset_happened.numpy().copy(), "agent_active": b.agent_active.numpy().copy(),
+                "ended_env": idx.astype(np.int64), "ended_obs": b.terminal_obs.numpy()[idx].astype(np.float32),
+                "ended_stats": b.episode_stats.numpy()[idx].copy()}

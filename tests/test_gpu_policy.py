@@ -143,3 +143,65 @@ def test_masked_forward_computes_selected_rows_only(dims, rows):
     assert torch.equal(out[sel], full[sel])
     assert torch.all(out[~sel] == 123.0)
     assert torch.all(none == -7.0)
+
+
+def test_weight_updates_are_seen_by_forward_and_collect():
+    """DevicePolicy over nn.Linear parameters (used in place) sees every kind of weight update: an optimizer step
+    and a write through ``.data`` (which does not move the tensor's version counter) -- forward() and a rollout
+    collection both match the torch forward of the updated weights.  With cache_packed=True a ``.data`` write needs
+    an explicit pack() (documented), after which it matches too."""
+    import torch
+    from cattleherd.env import HerdBatch
+    from cattleherd.policy import DevicePolicy
+    from cattleherd.rollout import DeviceRolloutBuffer
+    torch.manual_seed(0)
+    dev = torch.device("cuda", 0)
+
+    def mlp(out):
+        return [torch.nn.Linear(1032, 128).to(dev), torch.nn.Linear(128, 128).to(dev), torch.nn.Linear(128, out).to(dev)]
+    la, lc = mlp(16), mlp(1)
+    actor = DevicePolicy([(l.weight, l.bias) for l in la], "tanh", None)
+    critic = DevicePolicy([(l.weight, l.bias) for l in lc], "tanh", None)
+    assert actor.weights[0] is la[0].weight
+    x = torch.randn(300, 1032, device=dev) * 0.3
+    y0 = actor.forward(x)
+    assert torch.allclose(y0, actor.reference(x), rtol=1e-5, atol=1e-5)
+    # 1. an optimizer step on the parameters
+    opt = torch.optim.SGD([p for l in la for p in l.parameters()], lr=0.5)
+    h = x
+    for i, l in enumerate(la):
+        h = l(h)
+        if i < 2:
+            h = torch.tanh(h)
+    h.square().sum().backward()
+    opt.step()
+    y1 = actor.forward(x)
+    assert not torch.allclose(y1, y0, rtol=1e-3, atol=1e-3)
+    assert torch.allclose(y1, actor.reference(x), rtol=1e-5, atol=1e-5)
+    # 2. a write through .data (no version bump)
+    v0 = la[1].weight._version
+    la[1].weight.data.copy_(torch.randn_like(la[1].weight) * 0.05)
+    assert la[1].weight._version == v0
+    y2 = actor.forward(x)
+    assert not torch.allclose(y2, y1, rtol=1e-3, atol=1e-3)
+    assert torch.allclose(y2, actor.reference(x), rtol=1e-5, atol=1e-5)
+    # 3. a collection after a .data write into the critic: the stored values are V under the new weights
+    E, T = 256, 6
+    b = HerdBatch(E, 4, 16, mode="ctde")
+    b.reset()
+    rb = DeviceRolloutBuffer(b, T, act_dim=16)
+    log_std = torch.full((16,), -1.0, device=dev)
+    rb.collect(actor, critic, log_std, seed=3)
+    lc[0].weight.data.mul_(1.5)
+    rb.collect(actor, critic, log_std, seed=4)
+    torch.cuda.synchronize()
+    want = critic.reference(rb.obs.view(T * E, -1)).view(T, E)
+    assert torch.allclose(rb.values, want, rtol=1e-5, atol=1e-5)
+    # 4. cache_packed=True: packed once; a .data write is seen after pack()
+    cached = DevicePolicy([(l.weight, l.bias) for l in la], "tanh", None, cache_packed=True)
+    y3 = cached.forward(x)
+    la[2].weight.data.mul_(-1.0)
+    cached.pack()
+    assert torch.allclose(cached.forward(x), cached.reference(x), rtol=1e-5, atol=1e-5)
+    assert not torch.allclose(cached.forward(x), y3, rtol=1e-3, atol=1e-3)
+    b.close()

@@ -99,20 +99,27 @@ def test_rollout_buffer_matches_sb3_semantics(E, n, m, compat, level):
     b2.close()
 
 
-def test_native_collect_equals_python_loop():
+@pytest.mark.parametrize("T", [5, 13, 24])
+@pytest.mark.parametrize("path", [0, 2, 1], ids=["epilogues", "store_kernel", "copy_each"])
+def test_native_collect_equals_python_loop(T, path):
     """ch_rollout_collect (the loop in C++) and collect_steps (the same kernels launched from Python) fill
-    identical buffers, across auto-resets and truncation bootstraps."""
+    identical buffers, across auto-resets and truncation bootstraps: rollouts shorter than the deferred bootstrap's
+    8-step flush window and not a multiple of it, on each of the collection's paths (the store folded into the
+    forward epilogues, the stand-alone store kernel, every observation copied into the buffer)."""
+    import ctypes
     import torch
+    from cattleherd import _lib
     from cattleherd.env import HerdBatch
     from cattleherd.policy import DevicePolicy
     from cattleherd.rollout import DeviceRolloutBuffer
-    E, T, n, m = 256, 24, 4, 16
-    sc = 4800 - 12 + (np.arange(E) % 24)
+    E, n, m = 256, 4, 16
+    sc = 4800 - T // 2 + (np.arange(E) % T)   # truncations at every step of the rollout
     bufs = []
     for native in (True, False):
         b = HerdBatch(E, n, m, mode="ctde", curriculum_level=2)
         b.reset()
         b.set_state({"step_counter": sc})
+        assert _lib.lib().ch__set_rollout_path(b.handle, ctypes.c_int32(path)) == 0
         actor = DevicePolicy(DevicePolicy.random_layers([12 * 86, 128, 128, 4 * n], seed=1), "tanh", None)
         critic = DevicePolicy(DevicePolicy.random_layers([12 * 86, 128, 128, 1], seed=2), "tanh", None)
         rb = DeviceRolloutBuffer(b, T)

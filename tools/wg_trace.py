@@ -15,7 +15,9 @@ from cattleherd import _lib  # noqa: E402
 from cattleherd.env import HerdBatch  # noqa: E402
 
 
-def trace(mode, E, n, m, prec, G=None, B=None, steps=4):
+def trace(mode, E, n, m, prec, G=None, B=None, steps=4, summary=None):
+    """Print the phase table of `steps` launches; `summary` (a list) receives one dict per launch with the numbers
+    bench.py's latency roofline quotes (drone chain and workgroup cycles)."""
     L = _lib.lib()
     b = HerdBatch(E, n, m, mode=mode, precision=prec)
     if G is not None:
@@ -127,6 +129,13 @@ def trace(mode, E, n, m, prec, G=None, B=None, steps=4):
               f" | resetting WGs {int(res.sum())}: cycles mean {cyc[res].mean() if res.any() else 0:.0f} vs "
               f"{cyc[~res].mean():.0f} | chain q50/q90/max {np.percentile(chain, 50):.0f}/{np.percentile(chain, 90):.0f}/"
               f"{chain.max():.0f}")
+        if summary is not None:
+            summary.append({"wg_cycles_q50": float(np.percentile(cyc, 50)), "wg_cycles_q90": float(np.percentile(cyc, 90)),
+                            "wg_cycles_max": float(cyc.max()), "chain_cycles_q50": float(np.percentile(chain, 50)),
+                            "chain_start": float(rel(3)), "chain_done": float(rel(4)), "drone_terms_done": float(rel(5)),
+                            "h_received": float(rel(6)), "reset_list": float(rel(15)), "reward_done": float(rel(19)),
+                            "drone_wave_end": float(rel(35)), "span_us": float(span_us), "clock_ghz": float(clk),
+                            "flocking_envs_per_wg": float(nfv.mean()), "resetting_wgs": int(res.sum())})
         slow = np.argsort(cyc)[-5:]
         nfv = t[:, 31]
         print(f"   flocking envs per WG: mean {nfv.mean():.2f} | slow WGs' nf {nfv[slow].tolist()} | cycles by nf: " +
@@ -141,6 +150,17 @@ def trace(mode, E, n, m, prec, G=None, B=None, steps=4):
 
 
 def main():
+    if len(sys.argv) >= 2 and sys.argv[1] == "--json":   # --json mode E n m: 8 launches, then one JSON summary line
+        a = sys.argv[2:]
+        rows = []
+        trace(a[0], int(a[1]), int(a[2]), int(a[3]), "f64", steps=8, summary=rows)
+        out = {k: float(np.mean([r[k] for r in rows])) for k in rows[0]}
+        out["launches"] = len(rows)
+        out["chain_over_wg"] = out["chain_cycles_q50"] / out["wg_cycles_q50"]
+        out["post_chain_cycles"] = out["drone_wave_end"] - out["chain_done"]
+        import json
+        print(json.dumps(out), flush=True)
+        return
     if len(sys.argv) >= 5:   # one config: mode E n m [G B]
         a = sys.argv[1:]
         geom = (int(a[4]), int(a[5])) if len(a) >= 6 else (None, None)
