@@ -185,6 +185,35 @@ def ppo_rollout(b, d, T=32, fused=False):
     return out
 
 
+def marl_ppo_rollout(b, T=32):
+    """configs[4]'s training use: RLlib PPO sampling with one shared policy over every agent (DTDECattleHerder.py:
+    62-97; the RLlib default model, 86 -> 256 -> 256 -> 8 tanh = DiagGaussian mean and log_std, and a separate value
+    branch 86 -> 256 -> 256 -> 1, random-initialised) on the device (cattleherd.rollout.DeviceMarlRolloutBuffer): per
+    step the two forwards (f32 MFMA), the per-agent sample / log-prob / store, the env step with the wrapper's
+    drop-out; then per-agent GAE.  env-steps/s (and agent-steps/s) of one whole T-step collection after an untimed
+    one."""
+    import torch
+    from cattleherd.policy import DevicePolicy
+    from cattleherd.rollout import DeviceMarlRolloutBuffer
+    policy = DevicePolicy(DevicePolicy.random_layers([86, 256, 256, 8], seed=1), "tanh", None)
+    value = DevicePolicy(DevicePolicy.random_layers([86, 256, 256, 1], seed=2), "tanh", None)
+    rb = DeviceMarlRolloutBuffer(b, T)
+    b.reset()
+    rb.collect(policy, value, seed=1)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rb.collect(policy, value, seed=2)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    out = {"env_steps_per_s": b.n_envs * T / dt, "agent_steps_per_s": b.n_envs * b.num_drones * T / dt,
+           "ms_per_step": dt / T * 1000.0, "n_steps": T,
+           "policy": "RLlib default model 86-256-256-8 (mean, log_std) + value 86-256-256-1, tanh, random init, f32",
+           "gae": "per agent, gamma 0.99, lambda 1.0 (RLlib PPO default)",
+           "buffer_GB": sum(t.numel() * t.element_size() for t in (rb.obs, rb.actions)) / 1e9}
+    del rb
+    return out
+
+
 def marl_vec_rollout(n, m, E, steps, warmup, burn_in):
     """configs[4] through the batched RLlib multi-agent surface (cattleherd.marl_vec_env): random actions,
     the wrapper semantics and in-launch resets; env-steps/s of the zero-copy tensor path (one launch plus the
@@ -523,6 +552,8 @@ def main():
                                                                          "source") if k in fr} or fr_why
         if args.policy and mode == "ctde":
             out["policy_rollout"] = policy_rollout(b, n, args.steps, args.warmup)
+        if args.policy and mode == "marl":
+            out["marl_ppo_rollout"] = marl_ppo_rollout(b)
         if args.marl_vec and mode == "marl":
             b.close()
             out["marl_vec_env"] = marl_vec_rollout(n, m, E, args.steps, args.warmup, args.burn_in)

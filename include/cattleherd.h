@@ -334,6 +334,48 @@ int ch_rollout_collect(ch_handle* h, const ch_rollout* rb, const ch_rollout_io* 
                        const ch_mlp* critic, const float* log_std, uint64_t seed, float gamma, float gae_lambda,
                        int32_t bootstrap_truncated, void* stream);
 
+/* ---- On-device rollout collection for the DTDE (RLlib) driver ----------------------------------------------
+ * Replaces: RLlib PPO's sampling of RLlibMultiAgentWrapper envs with one shared policy over every agent
+ * (DTDECattleHerder.py:62-97: policies = {"shared_policy"}, gamma 0.99, train_batch_size 4096; the wrapper's
+ * agent drop-out and "__all__", marl_wrapper.py:77-119) and its GAE postprocessing.  MARL handles only.  Rows are
+ * agents: rows = n_envs * num_drones, row e * num_drones + i = agent_i of env e.  Per step t < n_steps:
+ *   the policy (output [rows][2 * act_dim]: RLlib's DiagGaussian inputs, the mean then log_std) and the value net
+ *   on the agents' observations (obs[t] = [rows][86]); for every agent live at the step's start (the wrapper's
+ *   self.agents: agent i < NUM_DRONES, not dropped out) a Gaussian sample a = mean + exp(log_std) eps (Philox keyed
+ *   by seed, counter (t, action, row), Box-Muller), stored unclipped with its summed Normal log-probability, the
+ *   value and agent_mask = 1; the env gets the samples clipped to [-1, 1] (RLlib's unsquash for Box(-1, 1)) and 0
+ *   for the other agents (ignored by the env); ch_step with auto-reset; the step's reward / terminated / truncated
+ *   per agent (0 where agent_mask is 0).
+ * Then last_values = V(obs after the last step) and GAE(gamma, gae_lambda) per agent backwards in float32: an
+ * agent's trajectory ends where it terminates (bootstrap 0; the env resets only once every agent has terminated, so
+ * a live agent that did not terminate is live at the next step of the same episode); rows with agent_mask 0 get
+ * advantage and return 0; truncation does not end a trajectory (the wrapper keeps truncated agents acting).
+ * RLlib is not installed here: these semantics are restated from its PPO defaults ("parity unpinned" to its
+ * source).  All arrays are caller-owned device memory. */
+typedef struct ch_marl_rollout {
+    int32_t n_steps;           /* T */
+    int32_t act_dim;           /* 4 (the VEL action of one agent) */
+    float* obs;                /* [T][rows][86] */
+    float* actions;            /* [T][rows][act_dim] unclipped samples (0 where not live) */
+    float* log_probs;          /* [T][rows] */
+    float* values;             /* [T][rows] */
+    float* rewards;            /* [T][rows] */
+    uint8_t* agent_mask;       /* [T][rows]: the agent was live at the start of step t */
+    uint8_t* terminated;       /* [T][rows] */
+    uint8_t* truncated;        /* [T][rows] */
+    float* advantages;         /* [T][rows] */
+    float* returns;            /* [T][rows] (advantages + values) */
+    float* last_values;        /* [rows] */
+} ch_marl_rollout;
+typedef struct ch_marl_rollout_io {
+    const ch_step_io* step;    /* the env's step buffers: obs, reward, terminated, truncated (actions are env_actions) */
+    float* policy_out;         /* scratch [rows][2 * act_dim] */
+    float* value_out;          /* scratch [rows] */
+    float* env_actions;        /* scratch [n_envs][num_drones][4] */
+} ch_marl_rollout_io;
+int ch_marl_rollout_collect(ch_handle* h, const ch_marl_rollout* rb, const ch_marl_rollout_io* io, const ch_mlp* policy,
+                            const ch_mlp* value, uint64_t seed, float gamma, float gae_lambda, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

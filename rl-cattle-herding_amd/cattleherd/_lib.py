@@ -25,7 +25,7 @@ EXPORTS = ("ch_default_config", "ch_create", "ch_destroy", "ch_last_error", "ch_
            "ch_state_size", "ch_get_state", "ch_set_state", "ch_metrics", "ch_metrics_device", "ch_sync",
            "ch_get_eval", "ch_builtin_spawn_table", "ch_rollout_store", "ch_rollout_post", "ch_rollout_gae", "ch_rollout_collect",
            "ch_spawn_table", "ch_mlp_forward", "ch_mlp_forward_masked", "ch_policy_forward", "ch_mlp_packed_size",
-           "ch_mlp_pack", "ch_outputs_to_host")
+           "ch_mlp_pack", "ch_outputs_to_host", "ch_marl_rollout_collect")
 CH_ACT_NONE, CH_ACT_TANH, CH_ACT_RELU = 0, 1, 2
 
 

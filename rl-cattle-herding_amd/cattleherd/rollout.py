@@ -130,3 +130,77 @@ class DeviceRolloutBuffer:
         L.check(lib.ch_rollout_gae(b.handle, rb, self.value.data_ptr(), self.gamma, self.gae_lambda, b._stream()),
                 b.handle)
         return self
+
+
+class ChMarlRollout(ctypes.Structure):
+    _fields_ = [("n_steps", ctypes.c_int32), ("act_dim", ctypes.c_int32)] + \
+        [(k, ctypes.c_void_p) for k in ("obs", "actions", "log_probs", "values", "rewards", "agent_mask", "terminated",
+                                        "truncated", "advantages", "returns", "last_values")]
+
+
+class ChMarlRolloutIO(ctypes.Structure):
+    _fields_ = [("step", ctypes.POINTER(L.ChStepIO))] + \
+        [(k, ctypes.c_void_p) for k in ("policy_out", "value_out", "env_actions")]
+
+
+class DeviceMarlRolloutBuffer:
+    """On-device rollout collection for the DTDE driver (SURVEY §8(f)2's RLlib half): RLlib PPO with one shared
+    policy over every agent of every ``RLlibMultiAgentWrapper`` env (simulator/DTDECattleHerder.py:62-97:
+    ``policies = {"shared_policy"}``, gamma 0.99; GAE lambda is RLlib PPO's default 1.0), the wrapper's agent
+    drop-out and ``"__all__"`` (rllib_envs/marl_wrapper.py:77-119) handled per agent row.
+
+    Rows are agents (``E * N``, row ``e * N + i`` = ``agent_i`` of env ``e``); every buffer is ``[T, rows, ...]``:
+    ``obs`` (86 floats), ``actions`` (unclipped samples), ``log_probs``, ``values``, ``rewards``, ``agent_mask``
+    (the agent was live at the step's start: its key was in the wrapper's dicts), ``terminated``, ``truncated``,
+    ``advantages``, ``returns``; ``last_values`` = V(obs after the last step).  ``collect`` is one native call
+    (ch_marl_rollout_collect): per step the policy and value forwards (f32 MFMA), the Gaussian sample /
+    log-probability / store, ch_step with auto-reset; then GAE per agent (a trajectory ends where the agent
+    terminates).  RLlib is not installed: its defaults are restated ("parity unpinned" to its source)."""
+
+    def __init__(self, batch, n_steps, act_dim=4, gamma=0.99, gae_lambda=1.0):
+        if batch.mode != L.CH_MODE_MARL:
+            raise ValueError("the per-agent rollout buffer is for MARL batches")
+        torch = batch.torch
+        self.batch, self.T, self.gamma, self.gae_lambda = batch, int(n_steps), float(gamma), float(gae_lambda)
+        self.act_dim = int(act_dim)
+        self.rows = rows = batch.n_envs * batch.num_drones
+        f32, u8 = dict(dtype=torch.float32, device=batch.device), dict(dtype=torch.uint8, device=batch.device)
+        self.obs = torch.zeros((self.T, rows, 86), **f32)
+        self.actions = torch.zeros((self.T, rows, self.act_dim), **f32)
+        for k in ("log_probs", "values", "rewards", "advantages", "returns"):
+            setattr(self, k, torch.zeros((self.T, rows), **f32))
+        for k in ("agent_mask", "terminated", "truncated"):
+            setattr(self, k, torch.zeros((self.T, rows), **u8))
+        self.last_values = torch.zeros(rows, **f32)
+        self.policy_out = torch.zeros((rows, 2 * self.act_dim), **f32)
+        self.value_out = torch.zeros((rows, 1), **f32)
+        self.env_actions = torch.zeros((batch.n_envs, batch.num_drones, 4), **f32)
+        rb = ChMarlRollout()
+        rb.n_steps, rb.act_dim = self.T, self.act_dim
+        for k in ("obs", "actions", "log_probs", "values", "rewards", "agent_mask", "terminated", "truncated",
+                  "advantages", "returns", "last_values"):
+            setattr(rb, k, getattr(self, k).data_ptr())
+        self._rb = rb
+        lib = L.lib()
+        vp = ctypes.c_void_p
+        lib.ch_marl_rollout_collect.argtypes = [vp, ctypes.POINTER(ChMarlRollout), ctypes.POINTER(ChMarlRolloutIO),
+                                                ctypes.POINTER(L.ChMlp), ctypes.POINTER(L.ChMlp), ctypes.c_uint64,
+                                                ctypes.c_float, ctypes.c_float, vp]
+        lib.ch_marl_rollout_collect.restype = ctypes.c_int
+        self._lib = lib
+
+    def collect(self, policy, value, seed=0):
+        """RLlib PPO sampling for n_steps steps of every env and agent, on the device, in one native call.
+        ``policy``: DevicePolicy 86 -> ... -> 2 * act_dim (mean, log_std: RLlib's DiagGaussian inputs), ``value``:
+        DevicePolicy 86 -> ... -> 1 (RLlib PPO's separate value branch, vf_share_layers=False)."""
+        b = self.batch
+        for net in (policy, value):
+            net._ensure_packed()
+        io = ChMarlRolloutIO()
+        io.step = ctypes.pointer(b._io)
+        io.policy_out, io.value_out, io.env_actions = (self.policy_out.data_ptr(), self.value_out.data_ptr(),
+                                                       self.env_actions.data_ptr())
+        L.check(self._lib.ch_marl_rollout_collect(b.handle, ctypes.byref(self._rb), ctypes.byref(io),
+                                                  ctypes.byref(policy._net), ctypes.byref(value._net), int(seed),
+                                                  self.gamma, self.gae_lambda, b._stream()), b.handle)
+        return self

@@ -1118,6 +1118,67 @@ int ch_rollout_collect(ch_handle* h, const ch_rollout* rb, const ch_rollout_io* 
     return CH_OK;
 }
 
+int ch_marl_rollout_collect(ch_handle* h, const ch_marl_rollout* rb, const ch_marl_rollout_io* io, const ch_mlp* policy,
+                            const ch_mlp* value, uint64_t seed, float gamma, float gae_lambda, void* stream) {
+    if (!h) return fail(nullptr, CH_ERR_INVALID, "ch_marl_rollout_collect: NULL handle");
+    if (h->cfg.mode != CH_MODE_MARL)
+        return fail(h, CH_ERR_UNSUPPORTED, "ch_marl_rollout_collect: the per-agent rollout is for MARL handles");
+    if (!rb || !io || !io->step || !policy || !value || !io->policy_out || !io->value_out || !io->env_actions)
+        return fail(h, CH_ERR_INVALID, "ch_marl_rollout_collect: NULL argument");
+    if (rb->n_steps < 1 || rb->act_dim != 4)
+        return fail(h, CH_ERR_INVALID, "ch_marl_rollout_collect: n_steps >= 1 and act_dim = 4 (one VEL action per agent)");
+    if (!rb->obs || !rb->actions || !rb->log_probs || !rb->values || !rb->rewards || !rb->agent_mask || !rb->terminated ||
+        !rb->truncated || !rb->advantages || !rb->returns || !rb->last_values)
+        return fail(h, CH_ERR_INVALID, "ch_marl_rollout_collect: NULL rollout buffer array");
+    const ch_step_io* sio = io->step;
+    if (!sio->obs || !sio->reward || !sio->terminated || !sio->truncated)
+        return fail(h, CH_ERR_INVALID, "ch_marl_rollout_collect: the step buffers obs, reward, terminated, truncated are required");
+    if ((reinterpret_cast<uintptr_t>(sio->obs) | reinterpret_cast<uintptr_t>(rb->obs)) & 15)
+        return fail(h, CH_ERR_INVALID, "ch_marl_rollout_collect: obs buffers must be 16-byte aligned");
+    if (policy->dims[policy->n_layers] != 2 * rb->act_dim || value->dims[value->n_layers] != 1)
+        return fail(h, CH_ERR_INVALID, "ch_marl_rollout_collect: the policy must output 2 * act_dim (mean, log_std), the value net 1");
+    int rc;
+    MlpArgs fp, fv;
+    if ((rc = policy_args(h, policy, sio->obs, io->policy_out, fp, "ch_marl_rollout_collect (policy)"))) return rc;
+    if ((rc = policy_args(h, value, sio->obs, io->value_out, fv, "ch_marl_rollout_collect (value)"))) return rc;
+    HIP_TRY(h, hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    MarlArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.T = rb->n_steps; a.A = rb->act_dim; a.N = h->NC; a.E = h->E; a.rows = h->E * h->NC;
+    a.env_n = h->envi; a.env_active = h->envi + 7 * h->E;
+    a.pol = io->policy_out; a.val = io->value_out; a.seed = seed; a.post_prev = 1;
+    a.reward = sio->reward; a.term = sio->terminated; a.trunc = sio->truncated;
+    a.gamma = gamma; a.gamma_lambda = (float)((double)gamma * (double)gae_lambda);
+    a.obs = rb->obs; a.actions = rb->actions; a.log_probs = rb->log_probs; a.values = rb->values; a.rewards = rb->rewards;
+    a.advantages = rb->advantages; a.returns = rb->returns; a.last_values = rb->last_values; a.env_actions = io->env_actions;
+    a.mask = rb->agent_mask; a.terminated = rb->terminated; a.truncated = rb->truncated;
+    // the step writes its observations straight into the buffer's next slot (a step into a buffer other than the one
+    // it wrote last writes every block in full); the last step into the env's own buffer.  No terminal observations:
+    // an agent's trajectory ends only where it terminates (no bootstrap), so the reset path needs no copy.
+    ch_step_io s = *sio;
+    s.actions = io->env_actions; s.actions_out = nullptr; s.terminal_obs = nullptr;
+    s.flags = (s.flags & ~CH_STEP_RANDOM_ACTIONS) | CH_STEP_AUTORESET;
+    const size_t slot = (size_t)a.rows * 86;
+    MlpArgs segs[2];
+    for (int32_t t = 0; t < rb->n_steps; ++t) {
+        const float* x = t == 0 ? sio->obs : rb->obs + (size_t)t * slot;
+        segs[0] = fp; segs[1] = fv;
+        segs[0].x = segs[1].x = x;
+        HIP_TRY(h, launch_mlp_multi(segs, 2, st));
+        a.t = t;
+        a.obs_now = t == 0 ? sio->obs : nullptr;
+        HIP_TRY(h, launch_marl_rollout(a, 0, st));
+        s.obs = t + 1 < rb->n_steps ? rb->obs + (size_t)(t + 1) * slot : sio->obs;
+        if ((rc = ch_step(h, &s, stream))) return rc;
+    }
+    // V(obs after the last step) -> last_values, the last step's post, GAE
+    fv.x = sio->obs;
+    HIP_TRY(h, launch_mlp_multi(&fv, 1, st));
+    HIP_TRY(h, launch_marl_rollout(a, 1, st));
+    return CH_OK;
+}
+
 int ch_metrics(ch_handle* h, double* out, int32_t reset_after, void* stream) {
     if (!h || !out) return fail(h, CH_ERR_INVALID, "ch_metrics: NULL argument");
     HIP_TRY(h, hipSetDevice(h->device));

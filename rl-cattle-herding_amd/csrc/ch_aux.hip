@@ -147,6 +147,106 @@ __global__ void k_rollout_gae(RolloutArgs a) {
     }
 }
 
+// ---- the DTDE (RLlib) per-agent rollout (ch_marl_rollout_collect; DTDECattleHerder.py:62-97, marl_wrapper.py:77-119)
+// RLlib PPO with one shared policy over every agent row (RLlib is not in this image: its defaults restated, "parity
+// unpinned"): the policy output is DiagGaussian's (mean, log_std), actions a = mean + exp(log_std) eps stored
+// unclipped, the env gets them clipped to Box(-1, 1); the log-probability is summed in action order.
+
+// after the env step t - 1: the agent's reward / terminated / truncated into the buffer (0 where it was not live)
+__device__ __forceinline__ void marl_post(const MarlArgs& a, int t, long long r) {
+    const long long row = (long long)t * a.rows + r;
+    const bool m = a.mask[row] != 0;
+    a.rewards[row] = m ? a.reward[r] : 0.0f;
+    a.terminated[row] = m ? a.term[r] : 0;
+    a.truncated[row] = m ? a.trunc[r] : 0;
+}
+
+// one thread per agent row: the previous step's post, then step t's mask (the wrapper's self.agents: agent i <
+// NUM_DRONES and not dropped out, read from the env state the step starts from), the samples, log-probability,
+// value and clipped env action; at t == 0 the batch's observation row into obs[0]
+__global__ __launch_bounds__(256) void k_marl_store(MarlArgs a) {
+    const long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= a.rows) return;
+    if (a.post_prev && a.t > 0) marl_post(a, a.t - 1, r);
+    if (a.post_only) return;
+    const long long e = r / a.N;
+    const int i = (int)(r - e * a.N);
+    const bool live = i < a.env_n[e] && ((a.env_active[e] >> i) & 1);
+    const long long row = (long long)a.t * a.rows + r;
+    if (a.obs_now) {
+        const float2* src = reinterpret_cast<const float2*>(a.obs_now + r * 86);
+        float2* dst = reinterpret_cast<float2*>(a.obs + row * 86);
+#pragma unroll 1
+        for (int k = 0; k < 43; ++k) dst[k] = src[k];
+    }
+    a.mask[row] = live;
+    float lps = 0.0f;
+    for (int k = 0; k < a.A; ++k) {
+        float act = 0.0f;
+        if (live) {
+            uint32_t c[4] = {(uint32_t)a.t, (uint32_t)k, (uint32_t)r, (uint32_t)(r >> 32)};
+            philox_k(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+            const float u1 = ((float)(c[0] >> 8) + 1.0f) * (1.0f / 16777216.0f);   // (0, 1]
+            const float u2 = (float)(c[1] >> 8) * (1.0f / 16777216.0f);
+            const float eps = sqrtf(-2.0f * logf(u1)) * cosf(6.2831853071795865f * u2);
+            const float mu = a.pol[r * 2 * a.A + k], ls = a.pol[r * 2 * a.A + a.A + k], sd = expf(ls);
+            act = mu + sd * eps;
+            const float d = act - mu, var = sd * sd;
+            lps += -(d * d) / (2.0f * var) - ls - 0.91893853320467274f;
+        }
+        a.actions[row * a.A + k] = act;
+        a.env_actions[r * 4 + k] = live ? fminf(fmaxf(act, -1.0f), 1.0f) : 0.0f;
+    }
+    a.log_probs[row] = lps;
+    a.values[row] = live ? a.val[r] : 0.0f;
+}
+
+// the last step's post, then GAE per agent row backwards in float32: a trajectory ends where the agent terminates;
+// rows the agent was not live in get 0 (include/cattleherd.h ch_marl_rollout)
+constexpr int kMarlGaeChunk = 16;
+__global__ __launch_bounds__(256) void k_marl_gae(MarlArgs a) {
+    const long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= a.rows) return;
+    if (a.post_prev) marl_post(a, a.T - 1, r);
+    const float g = a.gamma, gl = a.gamma_lambda;
+    const float lv = a.val[r];
+    a.last_values[r] = lv;
+    float last = 0.0f, nv = lv;
+    for (int s1 = a.T; s1 > 0; s1 -= kMarlGaeChunk) {
+        const int s0 = s1 > kMarlGaeChunk ? s1 - kMarlGaeChunk : 0;
+        float rw[kMarlGaeChunk], vl[kMarlGaeChunk];
+        uint8_t mk[kMarlGaeChunk], te[kMarlGaeChunk];
+#pragma unroll
+        for (int i = 0; i < kMarlGaeChunk; ++i) {
+            const long long row = (long long)min(s0 + i, s1 - 1) * a.rows + r;
+            rw[i] = a.rewards[row]; vl[i] = a.values[row]; mk[i] = a.mask[row]; te[i] = a.terminated[row];
+        }
+#pragma unroll
+        for (int i = kMarlGaeChunk - 1; i >= 0; --i) {
+            if (s0 + i >= s1) continue;
+            const long long row = (long long)(s0 + i) * a.rows + r;
+            if (!mk[i]) {
+                a.advantages[row] = 0.0f; a.returns[row] = 0.0f;
+                last = 0.0f; nv = 0.0f;
+                continue;
+            }
+            const float nnt = te[i] ? 0.0f : 1.0f;
+            const float delta = (rw[i] + (g * nv) * nnt) - vl[i];
+            last = delta + (gl * nnt) * last;
+            a.advantages[row] = last;
+            a.returns[row] = last + vl[i];
+            nv = vl[i];
+        }
+    }
+}
+
+hipError_t launch_marl_rollout(const MarlArgs& a, int which, hipStream_t st) {
+    const unsigned g = (unsigned)((a.rows + 255) / 256);
+    if (which == 0) hipLaunchKernelGGL(k_marl_store, dim3(g), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(k_marl_gae, dim3(g), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
 // ---- host delivery (ch_outputs_to_host): the envs that auto-reset in a step, compacted in ascending env order ------
 // One workgroup: each chunk of 1024 envs is ranked by wave ballots (lane prefix) and a scan of the 16 wave totals, so
 // the slots follow the env order; then the terminal observation blocks of the listed envs are copied into the

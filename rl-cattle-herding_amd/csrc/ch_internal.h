@@ -204,6 +204,25 @@ struct RolloutArgs {
         *last_episode_starts;
 };
 hipError_t launch_rollout(const RolloutArgs& a, int which, hipStream_t st);
+// ch_aux.hip: the DTDE (RLlib) per-agent rollout (ch_marl_rollout_collect); rows = E * N agents
+struct MarlArgs {
+    int T, t, A, N;
+    long long E, rows;
+    const int* env_n;          // handle envi row 0 (NUM_DRONES) and row 7 (the live-agent mask) at the step's start
+    const int* env_active;
+    const float* pol;          // [rows][2A] policy output: mean, log_std
+    const float* val;          // [rows] value output
+    const float* obs_now;      // t == 0: the batch's observations, copied into obs[0]
+    unsigned long long seed;
+    int post_prev, post_only;
+    const float* reward;       // the last step's outputs [rows]
+    const uint8_t *term, *trunc;
+    float gamma, gamma_lambda;
+    float *obs, *actions, *log_probs, *values, *rewards, *advantages, *returns, *last_values, *env_actions;
+    uint8_t *mask, *terminated, *truncated;
+};
+hipError_t launch_marl_rollout(const MarlArgs& a, int which, hipStream_t st);   // 0 store (+ post of t - 1), 1 gae
+
 // ch_aux.hip: ch_outputs_to_host's compaction of the envs that auto-reset (ascending env order)
 hipError_t launch_stage_ended(long long E, const uint8_t* reset, const float* term_obs, const double* stats,
                               int blk_floats, long long* count, long long* env_out, double* stats_out, float* obs_out,

