@@ -36,13 +36,17 @@ def _make(E, n, m, near):
     b = HerdBatch(E, n, m, mode="marl", curriculum_level=2, min_drones=n, max_drones=n)
     b.reset()
     s = b.get_state()
-    # a third of the envs start with their drones around the herd centroid: at level 2 their agents terminate
-    # (episode end and reset, or single agents dropping out when the curriculum level moves on between the calls)
+    # the `near` envs start with their drone centroid 0.45 m from the herd centroid: at level 2 (approach_min 0.6,
+    # curriculum_learning.py) every agent terminates and the env ends; half of them are one success short of level 3
+    # (approach_min 0.3, tally 99 of 100), so agent 0's success moves the env to level 3 and the other agents go on:
+    # agent 0 alone drops out (marl_wrapper.py:112-113)
     c = s["cow_pos"].mean(1)
     for k in range(n):
         s["drone_pos"][near, k, 0] = c[near, 0] + 0.5 * (k - (n - 1) / 2)
-        s["drone_pos"][near, k, 1] = c[near, 1]
-    b.set_state({"drone_pos": s["drone_pos"]})
+        s["drone_pos"][near, k, 1] = c[near, 1] + 0.45
+    tally = s["tally"].copy()
+    tally[near & (np.arange(E) % 2 == 0)] = 99
+    b.set_state({"drone_pos": s["drone_pos"], "tally": tally})
     return b
 
 
