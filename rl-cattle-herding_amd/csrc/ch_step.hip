@@ -386,17 +386,50 @@ __device__ __forceinline__ void alpha_cheap(V2Smem<R>& S, int* fl, int M, int P,
     }
 }
 
+// The full evaluation of the queued pairs.  Streamed (default; CH_NO_STREAM_FULL for the barrier form): a wave
+// that runs out of cheap-pass chunks starts on the queue at once instead of waiting at a pass-wide barrier for
+// the other waves' last cheap chunks.  Every queue slot starts as kQEmpty (phase 0); a chunk of 64 slots is taken
+// when all of them are reserved (Q_LEN) or the cheap pass is complete (F_C counts the waves done with it, so
+// Q_LEN is then final), and each lane waits for its own slot's pair index to be written -- a per-slot ready mark.
+constexpr uint16_t kQEmpty = 0xFFFF;
 template <class R>
-__device__ __forceinline__ void alpha_full(V2Smem<R>& S, int* fl, int M, int P, bool skip) {
+__device__ __forceinline__ void alpha_full(V2Smem<R>& S, int* fl, int M, int P, bool skip, int W1, int* err) {
     const R ra = sigma_norm_n(R(1.2)), da = ra;
-    const int qn = lds_peek(fl + Q_LEN);   // final: every cow wave's cheap pass is done (F_C)
     const float rP = 1.0f / (float)P;
     const int lane = threadIdx.x & 63;
+#ifdef CH_NO_STREAM_FULL
+    (void)W1; (void)err;
+    const int qn = lds_peek(fl + Q_LEN);   // final: every cow wave's cheap pass is done (F_C)
+#endif
     for (;;) {
         const int b = grab(fl + C_QUEUE, 64, skip);
+#ifndef CH_NO_STREAM_FULL
+        if (b >= (1 << 28)) break;   // (skip)
+        int qn = 0;
+        bool done = false;
+        for (int spins = 0;; ++spins) {
+            done = lds_peek(fl + F_C) >= W1;      // F_C before Q_LEN: once every wave is done, Q_LEN is final
+            qn = lds_peek(fl + Q_LEN);
+            if (done || qn >= b + 64) break;
+            if (spins >= (1 << 22)) { handoff_failed(err); done = true; break; }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (b >= qn) break;   // done: no slot of this chunk was ever reserved
+#else
         if (b >= qn) break;
+#endif
         if (b + lane < qn) {
+#ifndef CH_NO_STREAM_FULL
+            int gi = kQEmpty;
+            for (int spins = 0; spins < (1 << 22); ++spins) {
+                gi = *reinterpret_cast<volatile const uint16_t*>(&S.queue[b + lane]);
+                if (gi != kQEmpty) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (gi == kQEmpty) { handoff_failed(err); gi = 0; }
+#else
             const int gi = S.queue[b + lane];
+#endif
             const int g = qdiv(gi, P, rP), r = gi - g * P;
             const uint32_t pr = S.pl[r];
             const int bi = g * M + (pr & 0xff), bj = g * M + (pr >> 8);
@@ -801,6 +834,10 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             S.hasnb[k] = 0; S.nbm[k] = 0;
             if (sep) S.cnt[k] = 0;
         }
+#ifndef CH_NO_STREAM_FULL
+        if constexpr (!PW)   // the shared queue's per-slot ready marks (alpha_full)
+            for (int k = ct; k < G * P; k += CW) S.queue[k] = kQEmpty;
+#endif
         if (ct < 64) {   // the first cow wave: env scalars, one env per lane
         const int g = ct;
         bool flk = false;
@@ -1544,9 +1581,11 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             alpha_cheap(S, fl, M, P, nf, flist, skip_pre);
             if (ct == 0) TS(38, (long long)clock64());
             lds_signal(fl + F_C);
+#ifdef CH_NO_STREAM_FULL
             lds_wait(fl + F_C, W1, p.err);   // the queue is complete
+#endif
             if (ct == 0) { TS(39, (long long)clock64()); TS(29, (long long)lds_peek(fl + Q_LEN)); }
-            alpha_full(S, fl, M, P, skip_pre);
+            alpha_full(S, fl, M, P, skip_pre, W1, p.err);
         }
         if (ct == 0) TS(18, (long long)clock64());
 #pragma unroll

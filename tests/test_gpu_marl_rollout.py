@@ -37,15 +37,16 @@ def _make(E, n, m, near):
     b.reset()
     s = b.get_state()
     # the `near` envs start with their drone centroid 0.45 m from the herd centroid: at level 2 (approach_min 0.6,
-    # curriculum_learning.py) every agent terminates and the env ends; half of them are one success short of level 3
-    # (approach_min 0.3, tally 99 of 100), so agent 0's success moves the env to level 3 and the other agents go on:
-    # agent 0 alone drops out (marl_wrapper.py:112-113)
+    # curriculum_learning.py) every agent terminates and the env ends.  Half of them are n + 2 successes short of level
+    # 3 (approach_min 0.3, 100 successes): env.step's n reward calls and the wrapper's reward call for agent 0 count
+    # n + 1 (MARLCattleAviary._computeReward counts a success per call), agent 0's terminated call is still at level 2,
+    # agent 1's reward call moves the env to level 3 -- agent 0 alone drops out (marl_wrapper.py:104-113)
     c = s["cow_pos"].mean(1)
     for k in range(n):
         s["drone_pos"][near, k, 0] = c[near, 0] + 0.5 * (k - (n - 1) / 2)
         s["drone_pos"][near, k, 1] = c[near, 1] + 0.45
     tally = s["tally"].copy()
-    tally[near & (np.arange(E) % 2 == 0)] = 99
+    tally[near & (np.arange(E) % 2 == 0)] = 100 - n - 2
     b.set_state({"drone_pos": s["drone_pos"], "tally": tally})
     return b
 
