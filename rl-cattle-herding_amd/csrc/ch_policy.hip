@@ -275,10 +275,12 @@ constexpr int kD2 = 4;         // K pairs in flight per wave
 constexpr int kMaxPair0 = 36;  // first-layer live width <= 1152 (else k_mlp)
 constexpr int kLdsMax2 = 160 * 1024 - 1024;   // k_mlp2 dynamic LDS cap (the static kmax word included)
 
-template <int TW>
+// D pairs in flight (kD2; 2 when a pair's MFMAs already take ~1 k cycles: TW x RT >= 8 tiles per wave)
+template <int TW, int D = kD2>
 struct Ring2 {
-    float4 v[kD2][TW][2];
+    float4 v[D][TW][2];
 };
+template <int TW, int RT> constexpr int ring_depth() { return TW * RT >= 8 ? 2 : kD2; }
 
 __device__ __host__ __forceinline__ int pad_pairs(int k) { return ((k + 31) / 32 + kD2 - 1) / kD2 * kD2; }
 
@@ -291,8 +293,8 @@ struct WSrc {
 
 // request pair p into ring slot S (S a literal: the ring stays in registers).  MODE 0: packed; 1: raw rows,
 // K % 8 == 0 and 16-B aligned (two float4 at min(k, K - 8)); 2: raw rows, element loads at min(k + q, K - 1)
-template <int S, int TW, int MODE>
-__device__ __forceinline__ void mlp2_fetch(Ring2<TW>& r, const WSrc<TW>& ws, int p, int g) {
+template <int S, int TW, int MODE, int D>
+__device__ __forceinline__ void mlp2_fetch(Ring2<TW, D>& r, const WSrc<TW>& ws, int p, int g) {
 #pragma unroll
     for (int j = 0; j < TW; ++j) {
         if constexpr (MODE == 0) {
@@ -315,43 +317,56 @@ __device__ __forceinline__ float f4_at(const float4& v, int i) {
     return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
 }
 
-// pair p from ring slot S: the lane's 8 A values from LDS, 8 MFMAs per tile; then (FETCH) refill the slot with
-// pair p + D
-template <int S, int NT, int TW, int MODE, bool FETCH>
-__device__ __forceinline__ void mlp2_pair(f32x4 (&acc)[TW], Ring2<TW>& r, const WSrc<TW>& ws, const float* A, int lda,
+// pair p from ring slot S: the lane's 8 A values of each of the RT row tiles from LDS, 8 MFMAs per (row tile, column
+// tile); then (FETCH) refill the slot with pair p + D.  One weight pair feeds RT row tiles: a workgroup of 16 RT rows
+// streams each weight once for all of them.
+template <int S, int NT, int TW, int MODE, bool FETCH, int RT, int D>
+__device__ __forceinline__ void mlp2_pair(f32x4 (&acc)[RT][TW], Ring2<TW, D>& r, const WSrc<TW>& ws, const float* A, int lda,
                                           int p, int lane) {
     const int g = lane >> 4;
-    const float* ap = A + (lane & 15) * lda + 32 * p + 8 * g;
-    const float4 a0 = *reinterpret_cast<const float4*>(ap);
-    const float4 a1 = *reinterpret_cast<const float4*>(ap + 4);
+    float4 a0[RT], a1[RT];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+        const float* ap = A + (16 * t + (lane & 15)) * lda + 32 * p + 8 * g;
+        a0[t] = *reinterpret_cast<const float4*>(ap);
+        a1[t] = *reinterpret_cast<const float4*>(ap + 4);
+    }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-        const float av = f4_at(e < 4 ? a0 : a1, e & 3);
 #pragma unroll
-        for (int j = 0; j < NT; ++j)
-            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, f4_at(r.v[S][j][e >> 2], e & 3), acc[j], 0, 0, 0);
+        for (int t = 0; t < RT; ++t) {
+            const float av = f4_at(e < 4 ? a0[t] : a1[t], e & 3);
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+                acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, f4_at(r.v[S][j][e >> 2], e & 3), acc[t][j], 0, 0, 0);
+        }
     }
-    if constexpr (FETCH) mlp2_fetch<S, TW, MODE>(r, ws, p + kD2, g);
+    if constexpr (FETCH) mlp2_fetch<S, TW, MODE>(r, ws, p + D, g);
     // keep the refill here: left alone, the scheduler sinks all four refills below the group's last MFMAs, and
     // the next group then waits for loads issued a moment earlier
     __builtin_amdgcn_sched_barrier(0);
 }
 
 // npad (a multiple of D) pairs: the steady state refills every slot it drains, the last D pairs only drain
-template <int NT, int TW, int MODE>
-__device__ __forceinline__ void mlp2_loop(f32x4 (&acc)[TW], Ring2<TW>& r, const WSrc<TW>& ws, const float* A, int lda,
+template <int NT, int TW, int MODE, int RT, int D>
+__device__ __forceinline__ void mlp2_loop(f32x4 (&acc)[RT][TW], Ring2<TW, D>& r, const WSrc<TW>& ws, const float* A, int lda,
                                           int npad, int lane) {
+    static_assert(D == 2 || D == 4, "ring depth");
     int p0 = 0;
-    for (; p0 < npad - kD2; p0 += kD2) {
-        mlp2_pair<0, NT, TW, MODE, true>(acc, r, ws, A, lda, p0 + 0, lane);
-        mlp2_pair<1, NT, TW, MODE, true>(acc, r, ws, A, lda, p0 + 1, lane);
-        mlp2_pair<2, NT, TW, MODE, true>(acc, r, ws, A, lda, p0 + 2, lane);
-        mlp2_pair<3, NT, TW, MODE, true>(acc, r, ws, A, lda, p0 + 3, lane);
+    for (; p0 < npad - D; p0 += D) {
+        mlp2_pair<0, NT, TW, MODE, true, RT>(acc, r, ws, A, lda, p0 + 0, lane);
+        mlp2_pair<1, NT, TW, MODE, true, RT>(acc, r, ws, A, lda, p0 + 1, lane);
+        if constexpr (D == 4) {
+            mlp2_pair<2, NT, TW, MODE, true, RT>(acc, r, ws, A, lda, p0 + 2, lane);
+            mlp2_pair<3, NT, TW, MODE, true, RT>(acc, r, ws, A, lda, p0 + 3, lane);
+        }
     }
-    mlp2_pair<0, NT, TW, MODE, false>(acc, r, ws, A, lda, p0 + 0, lane);
-    mlp2_pair<1, NT, TW, MODE, false>(acc, r, ws, A, lda, p0 + 1, lane);
-    mlp2_pair<2, NT, TW, MODE, false>(acc, r, ws, A, lda, p0 + 2, lane);
-    mlp2_pair<3, NT, TW, MODE, false>(acc, r, ws, A, lda, p0 + 3, lane);
+    mlp2_pair<0, NT, TW, MODE, false, RT>(acc, r, ws, A, lda, p0 + 0, lane);
+    mlp2_pair<1, NT, TW, MODE, false, RT>(acc, r, ws, A, lda, p0 + 1, lane);
+    if constexpr (D == 4) {
+        mlp2_pair<2, NT, TW, MODE, false, RT>(acc, r, ws, A, lda, p0 + 2, lane);
+        mlp2_pair<3, NT, TW, MODE, false, RT>(acc, r, ws, A, lda, p0 + 3, lane);
+    }
 }
 
 template <int TW>
@@ -380,7 +395,7 @@ __device__ __forceinline__ Plan2 mlp2_plan(const MlpArgs& a, int li, int wave, i
         pl.pb = hi ? a.split_in[li] / 32 : 0;
         pl.npad = pad_pairs(hi ? K - a.split_in[li] : a.split_in[li]);
     } else {
-        pl.ntw = (wave < nt) + (TW > 1 && wave + NW < nt);
+        pl.ntw = wave < nt ? min(TW, (nt - wave + NW - 1) / NW) : 0;   // tiles wave, wave + NW, ... below nt
         pl.pb = 0;
         pl.npad = li == 0 ? np0 : pad_pairs(K);
     }
@@ -394,8 +409,8 @@ __device__ __forceinline__ int mlp2_tile(const Plan2& pl, int wave, int j) {
 
 // the wave's weight source for layer li (tiles past the layer width clamped to its last tile / row: computed,
 // never stored), starting at pair pl.pb, and the loads of its first D pairs
-template <int NW, int TW>
-__device__ __forceinline__ void mlp2_prologue(const MlpArgs& a, int li, const Plan2& pl, Ring2<TW>& r, WSrc<TW>& ws,
+template <int NW, int TW, int D>
+__device__ __forceinline__ void mlp2_prologue(const MlpArgs& a, int li, const Plan2& pl, Ring2<TW, D>& r, WSrc<TW>& ws,
                                               int wave, int lane) {
     // the layer's scalars read together and pinned in scalar registers here: read where each is first used
     // (inside a branch, after another field's use) they would cost a chain of dependent scalar-cache round
@@ -417,7 +432,7 @@ __device__ __forceinline__ void mlp2_prologue(const MlpArgs& a, int li, const Pl
     const int g = lane >> 4;
 #define CH_MLP2_PRO(M)                                                                                              \
     mlp2_fetch<0, TW, M>(r, ws, 0, g); mlp2_fetch<1, TW, M>(r, ws, 1, g);                                            \
-    mlp2_fetch<2, TW, M>(r, ws, 2, g); mlp2_fetch<3, TW, M>(r, ws, 3, g)
+    if constexpr (D == 4) { mlp2_fetch<2, TW, M>(r, ws, 2, g); mlp2_fetch<3, TW, M>(r, ws, 3, g); }
     if (mode == 0) { CH_MLP2_PRO(0); } else if (mode == 1) { CH_MLP2_PRO(1); } else { CH_MLP2_PRO(2); }
 #undef CH_MLP2_PRO
 }
@@ -434,19 +449,22 @@ __device__ __forceinline__ void mlp2_lds_barrier() {
 // accumulator chains; <8, 2>: <= 256 wide).  lda / ldh: LDS row strides (floats) of the staged input rows and of
 // the hidden activations, both = 4 mod 64 (conflict-free 16-B operand reads), wide enough for the padded pair
 // counts.
-template <int NW, int TW>
+// RT row tiles of 16 per workgroup (RT > 1: the hidden buffer of odd layers reuses the input rows' region, which is
+// dead after layer 0 -- see mlp2_lds_floats).
+template <int NW, int TW, int RT>
 __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int lda, int ldh, int role,
                                           const RolloutArgs& ro) {
     extern __shared__ __align__(16) float sm[];
-    float* xa = sm;                    // [16][lda]
-    float* hb0 = xa + kTM * lda;       // [16][ldh]
-    float* hb1 = hb0 + kTM * ldh;
+    constexpr int TMR = kTM * RT;      // rows of the workgroup
+    float* xa = sm;                    // [TMR][lda]
+    float* hb0 = RT == 1 ? xa + kTM * lda : xa + TMR * (lda > ldh ? lda : ldh);   // [TMR][ldh]
+    float* hb1 = RT == 1 ? hb0 + kTM * ldh : xa;
     __shared__ int kmax;
-    __shared__ int qslot[kTM];         // kRoleValue: each row's slot in the deferred-bootstrap queue (-1: none)
+    __shared__ int qslot[TMR];         // kRoleValue: each row's slot in the deferred-bootstrap queue (-1: none)
     constexpr int kT = 64 * NW;        // threads
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const long long row0 = blk * kTM;
+    const long long row0 = blk * TMR;
     // the arguments the tile's start needs, read together (see mlp2_prologue)
     const int* rows_dev = a.rows_dev;
     const int* env_n = a.env_n;
@@ -457,7 +475,7 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
     if (rows_dev && row0 >= *rows_dev) return;   // (uniform: every thread reads the same count)
     if (tid == 0) kmax = 0;
     __syncthreads();
-    if (tid < kTM && row0 + tid < rows) {
+    if (tid < TMR && row0 + tid < rows) {
         int k = d0;
         if (env_n) {
             const long long r = row0 + tid, e = r / rpe;
@@ -467,7 +485,7 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
         }
         atomicMax(&kmax, k);
     }
-    const bool any = __syncthreads_or(row_mask && tid < kTM && row0 + tid < rows && row_mask[row0 + tid] != 0);
+    const bool any = __syncthreads_or(row_mask && tid < TMR && row0 + tid < rows && row_mask[row0 + tid] != 0);
     if (row_mask && !any) return;
     const int kloop = min(kmax, a.kcap);   // (the host sized the tile for kcap)
     const int np0 = min(pad_pairs(max(kloop, 1)), kMaxPair0);
@@ -476,40 +494,41 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
 
     // the first layer's first weight pairs (L2 hits), then the tile's input rows (from HBM): thread t owns row
     // t / (4 NW) and float4 columns t % (4 NW) + 4 NW i, i < nld, of the padded width 32 np0
-    Ring2<TW> ring;
+    Ring2<TW, ring_depth<TW, RT>()> ring;
     WSrc<TW> ws;
     Plan2 pl = mlp2_plan<NW, TW>(a, 0, wave, np0);
     mlp2_prologue<NW, TW>(a, 0, pl, ring, ws, wave, lane);
     if (ts) ts[1] = clock64();
+    // rows srow + 16 rt; as many row tiles per pass as the kQ registers hold (RT nld <= kQ for the reference's nets)
     constexpr int kTPR = 4 * NW, kQ = 8 * kMaxPair0 / kTPR;
     const int K0 = a.dims[0], srow = tid / kTPR, sc = 4 * (tid % kTPR), nld = (8 * np0 + kTPR - 1) / kTPR;
-    const bool srv = row0 + srow < a.rows;
-    const float* xs = a.x + min(row0 + srow, a.rows - 1) * K0;
-    float4 xr[kQ];
-    if ((a.vec_w >> 7) & 1) {
+    const int rper = max(1, min(RT, kQ / nld));
+    for (int rb = 0; rb < RT; rb += rper) {
+        float4 xr[kQ];
+        const long long rr0 = row0 + 16 * rb + srow;
 #pragma unroll
-        for (int i = 0; i < kQ; ++i)
-            if (i < nld) xr[i] = *reinterpret_cast<const float4*>(xs + min(sc + 4 * kTPR * i, K0 - 4));
-    } else {
-#pragma unroll
-        for (int i = 0; i < kQ; ++i) {
-            const int c = sc + 4 * kTPR * i;
-            if (i < nld)
-                xr[i] = make_float4(xs[min(c, K0 - 1)], xs[min(c + 1, K0 - 1)], xs[min(c + 2, K0 - 1)], xs[min(c + 3, K0 - 1)]);
+        for (int q = 0; q < kQ; ++q) {
+            const int t = q / nld, i = q - t * nld, c = sc + 4 * kTPR * i;
+            if (t < rper && rb + t < RT) {
+                const float* xs = a.x + min(rr0 + 16 * t, a.rows - 1) * K0;
+                if ((a.vec_w >> 7) & 1) xr[q] = *reinterpret_cast<const float4*>(xs + min(c, K0 - 4));
+                else xr[q] = make_float4(xs[min(c, K0 - 1)], xs[min(c + 1, K0 - 1)], xs[min(c + 2, K0 - 1)], xs[min(c + 3, K0 - 1)]);
+            }
         }
-    }
-    __builtin_amdgcn_sched_barrier(0);   // every load above issued before the first wait
-    if (ts) ts[2] = clock64();
+        __builtin_amdgcn_sched_barrier(0);   // every load above issued before the first wait
+        if (ts && rb == 0) ts[2] = clock64();
 #pragma unroll
-    for (int i = 0; i < kQ; ++i) {
-        const int c = sc + 4 * kTPR * i;
-        if (i < nld && c < 32 * np0) {
-            float4 v = xr[i];
-            v.x = srv && c < kloop ? v.x : 0.0f;
-            v.y = srv && c + 1 < kloop ? v.y : 0.0f;
-            v.z = srv && c + 2 < kloop ? v.z : 0.0f;
-            v.w = srv && c + 3 < kloop ? v.w : 0.0f;
-            *reinterpret_cast<float4*>(xa + srow * lda + c) = v;
+        for (int q = 0; q < kQ; ++q) {
+            const int t = q / nld, i = q - t * nld, c = sc + 4 * kTPR * i;
+            if (t < rper && rb + t < RT && c < 32 * np0) {
+                const bool srv = rr0 + 16 * t < a.rows;
+                float4 v = xr[q];
+                v.x = srv && c < kloop ? v.x : 0.0f;
+                v.y = srv && c + 1 < kloop ? v.y : 0.0f;
+                v.z = srv && c + 2 < kloop ? v.z : 0.0f;
+                v.w = srv && c + 3 < kloop ? v.w : 0.0f;
+                *reinterpret_cast<float4*>(xa + (16 * (rb + t) + srow) * lda + c) = v;
+            }
         }
     }
     if (ts) ts[3] = clock64();
@@ -530,14 +549,18 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
             const int col = mlp2_tile<NW, TW>(pl, wave, j) * 16 + (lane & 15);
             bcol[j] = a.b[li] && col < N ? a.b[li][col] : 0.0f;
         }
-        f32x4 acc[TW];
+        f32x4 acc[RT][TW];
 #pragma unroll
-        for (int j = 0; j < TW; ++j) acc[j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+            for (int j = 0; j < TW; ++j) acc[t][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #define CH_MLP2_LOOP(NT_)                                                                                           \
-        if (mode == 0) mlp2_loop<NT_, TW, 0>(acc, ring, ws, A, ldc, pl.npad, lane);                                  \
-        else if (mode == 1) mlp2_loop<NT_, TW, 1>(acc, ring, ws, A, ldc, pl.npad, lane);                             \
-        else mlp2_loop<NT_, TW, 2>(acc, ring, ws, A, ldc, pl.npad, lane)
-        if (ntw == TW) { CH_MLP2_LOOP(TW); } else if (ntw > 0) { CH_MLP2_LOOP(1); }
+        if (mode == 0) mlp2_loop<NT_, TW, 0, RT>(acc, ring, ws, A, ldc, pl.npad, lane);                              \
+        else if (mode == 1) mlp2_loop<NT_, TW, 1, RT>(acc, ring, ws, A, ldc, pl.npad, lane);                         \
+        else mlp2_loop<NT_, TW, 2, RT>(acc, ring, ws, A, ldc, pl.npad, lane)
+        if (ntw == TW) { CH_MLP2_LOOP(TW); }
+        else if constexpr (TW >= 4) { if (ntw == 3) { CH_MLP2_LOOP(3); } else if (ntw == 2) { CH_MLP2_LOOP(2); } else if (ntw == 1) { CH_MLP2_LOOP(1); } }
+        else if (ntw > 0) { CH_MLP2_LOOP(1); }
 #undef CH_MLP2_LOOP
         if (ts && li < 3) ts[5 + 2 * li] = clock64();
         // the next layer's first pairs, in flight during this epilogue and barrier
@@ -548,15 +571,17 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
             mlp2_prologue<NW, TW>(a, li + 1, pl, ring, ws, wave, lane);
         }
         float* out = li & 1 ? hb1 : hb0;
-        // epilogue: C/D map col = lane & 15, row = 4 (lane >> 4) + r
+        // epilogue: C/D map col = lane & 15, row = 16 t + 4 (lane >> 4) + r
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
 #pragma unroll
         for (int j = 0; j < TW; ++j) {
             if (j >= ntw) continue;
             const int col = mlp2_tile<NW, TW>(cpl, wave, j) * 16 + (lane & 15);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int row = (lane >> 4) * 4 + r;
-                float v = acc[j][r] + bcol[j];
+                const int row = 16 * t + (lane >> 4) * 4 + r;
+                float v = acc[t][j][r] + bcol[j];
                 if (!last) {
                     if (col < N) out[row * ldh + col] = act_fn(v, a.hidden_act);
                 } else if (col < N && row0 + row < a.rows && (!a.row_mask || a.row_mask[row0 + row])) {
@@ -569,7 +594,7 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
         if (last) break;
         // columns [N, 32 npn) of the activations: zero for the next layer's padded pairs
         const int zc = 32 * npn - N;
-        for (int idx = tid; idx < kTM * zc; idx += kT) {
+        for (int idx = tid; idx < TMR * zc; idx += kT) {
             const int r = idx / zc;
             out[r * ldh + N + idx - r * zc] = 0.0f;
         }
@@ -585,7 +610,7 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
         // terms are summed in action order by one lane (k_rollout_store's order)
         float* lp = a.layers & 1 ? hb0 : hb1;
         const int NA = a.dims[a.layers];
-        const int nrow = (int)min((long long)kTM, a.rows - row0);
+        const int nrow = (int)min((long long)TMR, a.rows - row0);
         mlp2_lds_barrier();
         for (int idx = tid; idx < nrow * NA; idx += kT) {
             const int r = idx / NA, k = idx - r * NA;
@@ -603,7 +628,7 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
         // observation rows into obs[0]
         const float* vl = a.layers & 1 ? hb0 : hb1;
         mlp2_lds_barrier();
-        if (tid < kTM) {
+        if (tid < TMR) {
             const long long e = row0 + tid;
             int slot = -1;
             if (e < a.rows) {
@@ -620,7 +645,7 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
         }
         mlp2_lds_barrier();
         const int nq4 = ro.obs_dim / 4;
-        for (int r = 0; r < kTM; ++r) {
+        for (int r = 0; r < TMR; ++r) {
             const int slot = qslot[r];
             if (slot < 0) continue;
             const float4* src = reinterpret_cast<const float4*>(ro.term_obs + (row0 + r) * ro.obs_dim);
@@ -628,7 +653,7 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
             for (int k = tid; k < nq4; k += kT) dst[k] = src[k];
         }
         if (ro.copy_obs) {
-            const int nr = (int)min((long long)kTM, a.rows - row0);
+            const int nr = (int)min((long long)TMR, a.rows - row0);
             for (int k = tid; k < nr * nq4; k += kT) {
                 const int r = k / nq4, c = k - r * nq4;
                 reinterpret_cast<float4*>(ro.obs + ((long long)ro.t * ro.rows + row0 + r) * ro.obs_dim)[c] =
@@ -643,12 +668,14 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
 // other's matrix work -- the rollout's actor, critic and terminal-value critic in one launch.
 // SHARE: registers capped at 128 per lane (4 waves per SIMD) so that two 8-wave workgroups fit a CU -- the
 // multi-segment launches; a single forward runs without the cap (fewer, faster waves: 17-18 vs 19.7 us alone)
-template <int NW, int TW, bool SHARE = false>
+// RT: row tiles of 16 per workgroup (launch_mlp_multi picks 2 or 4 for row counts that fill the chip anyway: each
+// weight pair then feeds RT x more MFMAs, the 256-wide RLlib nets' forward is otherwise bound by the weight stream)
+template <int NW, int TW, bool SHARE = false, int RT = 1>
 __global__ __launch_bounds__(64 * NW, SHARE ? 4 : 1) void k_mlp2(MlpMulti m) {
     int sg = 0;
     if (m.nseg > 1 && (int)blockIdx.x >= m.start[1]) sg = 1;
     if (m.nseg > 2 && (int)blockIdx.x >= m.start[2]) sg = 2;
-    mlp2_body<NW, TW>(m.seg[sg], (long long)blockIdx.x - m.start[sg], m.lda, m.ldh, m.role[sg], m.ro);
+    mlp2_body<NW, TW, RT>(m.seg[sg], (long long)blockIdx.x - m.start[sg], m.lda, m.ldh, m.role[sg], m.ro);
 }
 
 // ch_mlp_pack: layer li's weights into the [tile][pair][half][lane][4] layout (zero past N and K)
@@ -704,7 +731,10 @@ static hipError_t mlp_attrs() {
             if (e != hipSuccess) return e;
         }
         for (const void* f : {reinterpret_cast<const void*>(&k_mlp2<4, 2>), reinterpret_cast<const void*>(&k_mlp2<8, 2>),
-                              reinterpret_cast<const void*>(&k_mlp2<8, 1>), reinterpret_cast<const void*>(&k_mlp2<8, 1, true>)}) {
+                              reinterpret_cast<const void*>(&k_mlp2<8, 1>), reinterpret_cast<const void*>(&k_mlp2<8, 1, true>),
+                              reinterpret_cast<const void*>(&k_mlp2<4, 4, false, 2>),
+                              reinterpret_cast<const void*>(&k_mlp2<4, 4, false, 4>),
+                              reinterpret_cast<const void*>(&k_mlp2<8, 1, false, 2>)}) {
             e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax2);
             if (e != hipSuccess) return e;
         }
@@ -715,6 +745,12 @@ static hipError_t mlp_attrs() {
 
 // k_mlp2's shape for one net: widest layer, LDS strides (the live input width rounded to whole K pairs, rows
 // padded to 4 mod 64 floats); false when the net does not fit it (then k_mlp)
+// LDS floats of k_mlp2's tile: RT == 1 input rows and two hidden buffers; RT > 1 the odd layers' hidden buffer in the
+// input rows' region (dead after layer 0)
+static size_t mlp2_lds_floats(int rt, int lda, int ldh) {
+    return rt == 1 ? (size_t)kTM * (lda + 2 * ldh) : (size_t)kTM * rt * ((lda > ldh ? lda : ldh) + ldh);
+}
+
 static bool mlp2_shape(const MlpArgs& a, int& maxw, int& lda, int& ldh) {
     int maxhid = 32;
     maxw = 0;
@@ -725,7 +761,7 @@ static bool mlp2_shape(const MlpArgs& a, int& maxw, int& lda, int& ldh) {
     const int np0 = pad_pairs(std::max(a.kcap, 1));
     lda = (32 * np0 + 63) / 64 * 64 + 4;
     ldh = (std::max(maxhid, 32 * kD2) + 32 * kD2 - 1) / (32 * kD2) * (32 * kD2) + 4;
-    return np0 <= kMaxPair0 && sizeof(float) * (size_t)kTM * (lda + 2 * ldh) <= (size_t)kLdsMax2;
+    return np0 <= kMaxPair0 && sizeof(float) * mlp2_lds_floats(1, lda, ldh) <= (size_t)kLdsMax2;
 }
 
 bool mlp_multi_fits(const MlpArgs* segs, int nseg) {
@@ -745,32 +781,57 @@ hipError_t launch_mlp_multi(const MlpArgs* segs, int nseg, hipStream_t st, const
     if (nseg < 1 || nseg > 3) return hipErrorInvalidValue;
     hipError_t e = mlp_attrs();
     if (e != hipSuccess) return e;
-    MlpMulti m;
-    std::memset(&m, 0, sizeof(m));
-    int maxw = 0, fits = !v1, grid = 0, n = 0;
+    // row tiles per workgroup: 4 (64 rows) when every segment still gives >= 256 workgroups and a net is 256 wide (the
+    // RLlib per-agent nets: the weight stream per workgroup is what the forward waits on), else 1; CH_MLP_RT overrides
+    static const int rt_env = [] { const char* v = getenv("CH_MLP_RT"); return v ? atoi(v) : 0; }();
+    int maxw0 = 0;
+    long long minrows = -1;
     for (int s = 0; s < nseg; ++s) {
-        const long long g = (segs[s].rows + kTM - 1) / kTM;
-        if (g == 0) continue;
-        int w, la, lh;
-        fits &= mlp2_shape(segs[s], w, la, lh);
-        maxw = std::max(maxw, w); m.lda = std::max(m.lda, la); m.ldh = std::max(m.ldh, lh);
-        m.seg[n] = segs[s];
-        m.seg[n].tstamp = g_mlp_tstamp;
-        m.role[n] = roles ? roles[s] : kRoleNone;
-        m.start[n] = grid;
-        grid += (int)g;
-        ++n;
+        for (int i = 1; i <= segs[s].layers; ++i) maxw0 = std::max(maxw0, segs[s].dims[i]);
+        if (segs[s].rows > 0) minrows = minrows < 0 ? segs[s].rows : std::min(minrows, segs[s].rows);
+    }
+    int rt = rt_env == 1 || rt_env == 2 || rt_env == 4 ? rt_env : (maxw0 > 128 && minrows >= 256LL * 64 ? 4 : 1);
+    rt = std::min(rt, maxw0 > 128 ? 4 : (nw4 || nseg > 1 ? 1 : 2));   // the instantiations below
+    MlpMulti m;
+    int maxw = 0, fits = 0, grid = 0, n = 0;
+    for (;;) {   // the largest rt <= the chosen one whose tile fits the LDS
+        std::memset(&m, 0, sizeof(m));
+        maxw = 0; fits = !v1; grid = 0; n = 0;
+        for (int s = 0; s < nseg; ++s) {
+            const long long g = (segs[s].rows + kTM * rt - 1) / (kTM * rt);
+            if (g == 0) continue;
+            int w, la, lh;
+            fits &= mlp2_shape(segs[s], w, la, lh);
+            maxw = std::max(maxw, w); m.lda = std::max(m.lda, la); m.ldh = std::max(m.ldh, lh);
+            m.seg[n] = segs[s];
+            m.seg[n].tstamp = g_mlp_tstamp;
+            m.role[n] = roles ? roles[s] : kRoleNone;
+            m.start[n] = grid;
+            grid += (int)g;
+            ++n;
+        }
+        if (rt == 1 || sizeof(float) * mlp2_lds_floats(rt, m.lda, m.ldh) <= (size_t)kLdsMax2) break;
+        rt >>= 1;
     }
     if (n == 0) return hipSuccess;
     if (ro) m.ro = *ro;
     m.nseg = n;
     m.start[n] = grid;
-    const size_t lds2 = sizeof(float) * (size_t)kTM * (m.lda + 2 * m.ldh);
+    const size_t lds2 = sizeof(float) * mlp2_lds_floats(rt, m.lda, m.ldh);
     if (fits && lds2 <= (size_t)kLdsMax2) {
-        if (maxw > 128) hipLaunchKernelGGL((k_mlp2<8, 2>), dim3((unsigned)grid), dim3(512), lds2, st, m);
-        else if (nw4) hipLaunchKernelGGL((k_mlp2<4, 2>), dim3((unsigned)grid), dim3(256), lds2, st, m);
-        else if (n > 1) hipLaunchKernelGGL((k_mlp2<8, 1, true>), dim3((unsigned)grid), dim3(512), lds2, st, m);
-        else hipLaunchKernelGGL((k_mlp2<8, 1>), dim3((unsigned)grid), dim3(512), lds2, st, m);
+        if (maxw > 128) {
+            // RT > 1: four waves of 64 columns each, one per SIMD (the 512-register budget of a lone wave holds the
+            // 4 x 4 accumulators and the 4 x 4 weight ring)
+            if (rt == 4) hipLaunchKernelGGL((k_mlp2<4, 4, false, 4>), dim3((unsigned)grid), dim3(256), lds2, st, m);
+            else if (rt == 2) hipLaunchKernelGGL((k_mlp2<4, 4, false, 2>), dim3((unsigned)grid), dim3(256), lds2, st, m);
+            else hipLaunchKernelGGL((k_mlp2<8, 2>), dim3((unsigned)grid), dim3(512), lds2, st, m);
+        } else if (nw4) hipLaunchKernelGGL((k_mlp2<4, 2>), dim3((unsigned)grid), dim3(256), lds2, st, m);
+        else if (n > 1) {
+            hipLaunchKernelGGL((k_mlp2<8, 1, true>), dim3((unsigned)grid), dim3(512), lds2, st, m);
+        } else {
+            if (rt >= 2) hipLaunchKernelGGL((k_mlp2<8, 1, false, 2>), dim3((unsigned)grid), dim3(512), lds2, st, m);
+            else hipLaunchKernelGGL((k_mlp2<8, 1>), dim3((unsigned)grid), dim3(512), lds2, st, m);
+        }
         return hipGetLastError();
     }
     // the round-2 kernel, one launch per net (no rollout epilogues: callers check mlp_multi_fits first)

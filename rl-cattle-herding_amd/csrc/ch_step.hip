@@ -511,6 +511,43 @@ __device__ __forceinline__ void alpha_cheap_pw(V2Smem<R>& S, int M, int P, int g
     }
 }
 
+// The same pass for a geometry-specialised herd (NC = the pass's 64-pair chunks, a compile-time count): the lane's
+// pair words come from registers (prw, read from LDS once per kernel) and every chunk's position loads are issued
+// before any chunk's test, so the pass costs about one LDS round trip instead of one per chunk.  The queue and
+// masks are filled in the same (chunk, lane) order as alpha_cheap_pw.
+template <class R, int NC>
+__device__ __forceinline__ void alpha_cheap_pw_b(V2Smem<R>& S, int M, int P, int g, uint16_t* qu, int& qn,
+                                                 const uint32_t (&prw)[NC]) {
+    const int lane = threadIdx.x & 63;
+    R n2[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const uint32_t pr = prw[c];
+        const int bi = g * M + (pr & 0xff), bj = g * M + (pr >> 8);
+        const R zx = S.cx[bj] - S.cx[bi], zy = S.cy[bj] - S.cy[bi];
+        n2[c] = zx * zx + zy * zy;
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const int r = 64 * c + lane;
+        bool cand = false;
+        if (r < P) {
+            const uint32_t pr = prw[c];
+            const int li = pr & 0xff, hi = pr >> 8;
+            const int bi = g * M + li, bj = g * M + hi;
+            if (in_sensing(n2[c])) { S.hasnb[bi] = 1; S.hasnb[bj] = 1; }
+            cand = n2[c] <= R(kAlphaSupport2);
+            if (cand) {
+                atomicOr(&S.nbm[bi], 1ull << hi);
+                atomicOr(&S.nbm[bj], 1ull << li);
+            }
+        }
+        const unsigned long long m = __ballot(cand);
+        if (cand) qu[qn + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)r;
+        qn += __popcll(m);
+    }
+}
+
 template <class R>
 __device__ __forceinline__ void alpha_full_pw(V2Smem<R>& S, int M, int P, int g, int q0, int qn, R* tb,
                                               const uint16_t* qu) {
@@ -1502,6 +1539,15 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         uint16_t* qu = nullptr;
         int f_cur = -1, ch = 0, qn = 0, qd = 0;
         const int NCH = (P + 63) >> 6;
+        // PW with a compile-time herd: this lane's pair words (i | j << 8) of every 64-pair chunk, read from the
+        // staged pair list once (pairs past P repeat pair 0, whose test is masked out by r < P)
+        constexpr int NCHC = MT > 0 ? (MT * (MT - 1) / 2 + 63) / 64 : 1;
+        uint32_t prw[NCHC];
+#pragma unroll
+        for (int c = 0; c < NCHC; ++c) {
+            const int r = 64 * c + (tid & 63);
+            prw[c] = (PW && MT > 0) ? S.pl[r < P ? r : 0] : 0u;
+        }
         // one unit of PW alpha work (a cheap-pass chunk or an expensive-pass wave of queued pairs, plus the
         // env's rows after its last unit); false when no flocking env is left.  The state is wave-uniform
         // (grab is readfirstlane'd, the queue length a ballot count).
@@ -1557,7 +1603,12 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             CHUNK_T0;
             const int g = flist[f_cur];
             if (ch < NCH) {
+#ifndef CH_NO_BATCHED_CHEAP
+                if constexpr (PW && MT > 0) alpha_cheap_pw_b<R, NCHC>(S, M, P, g, qu, qn, prw);
+                else alpha_cheap_pw(S, M, P, g, qu, qn);
+#else
                 alpha_cheap_pw(S, M, P, g, qu, qn);
+#endif
                 ch = NCH;
                 wave_sync();   // the queue
             } else if (qd < qn) {
