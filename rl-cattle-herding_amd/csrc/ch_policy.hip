@@ -781,17 +781,26 @@ hipError_t launch_mlp_multi(const MlpArgs* segs, int nseg, hipStream_t st, const
     if (nseg < 1 || nseg > 3) return hipErrorInvalidValue;
     hipError_t e = mlp_attrs();
     if (e != hipSuccess) return e;
-    // row tiles per workgroup: 4 (64 rows) when every segment still gives >= 256 workgroups and a net is 256 wide (the
-    // RLlib per-agent nets: the weight stream per workgroup is what the forward waits on), else 1; CH_MLP_RT overrides
+    // row tiles per workgroup: the most (1, 2 or 4 tiles of 16 rows) that still leave a workgroup for every CU across
+    // the launch's segments -- each weight pair a workgroup streams then feeds RT times the MFMAs, and the forward of
+    // a chip-filling batch waits on that stream, not on the matrix cores; CH_MLP_RT overrides
     static const int rt_env = [] { const char* v = getenv("CH_MLP_RT"); return v ? atoi(v) : 0; }();
-    int maxw0 = 0;
-    long long minrows = -1;
+    int maxw0 = 0, cus = 256;
+    long long rows_all = 0;
     for (int s = 0; s < nseg; ++s) {
         for (int i = 1; i <= segs[s].layers; ++i) maxw0 = std::max(maxw0, segs[s].dims[i]);
-        if (segs[s].rows > 0) minrows = minrows < 0 ? segs[s].rows : std::min(minrows, segs[s].rows);
+        rows_all += segs[s].rows;
     }
-    int rt = rt_env == 1 || rt_env == 2 || rt_env == 4 ? rt_env : (maxw0 > 128 && minrows >= 256LL * 64 ? 4 : 1);
-    rt = std::min(rt, maxw0 > 128 ? 4 : (nw4 || nseg > 1 ? 1 : 2));   // the instantiations below
+    {
+        int dev = 0;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    }
+    int rt = 1;
+    if (rt_env == 1 || rt_env == 2 || rt_env == 4) rt = rt_env;
+    else
+        for (int r : {4, 2})
+            if (rows_all >= (long long)kTM * r * cus) { rt = r; break; }
+    rt = std::min(rt, maxw0 > 128 ? 4 : (nw4 ? 1 : 2));   // the instantiations below
     MlpMulti m;
     int maxw = 0, fits = 0, grid = 0, n = 0;
     for (;;) {   // the largest rt <= the chosen one whose tile fits the LDS
@@ -826,7 +835,7 @@ hipError_t launch_mlp_multi(const MlpArgs* segs, int nseg, hipStream_t st, const
             else if (rt == 2) hipLaunchKernelGGL((k_mlp2<4, 4, false, 2>), dim3((unsigned)grid), dim3(256), lds2, st, m);
             else hipLaunchKernelGGL((k_mlp2<8, 2>), dim3((unsigned)grid), dim3(512), lds2, st, m);
         } else if (nw4) hipLaunchKernelGGL((k_mlp2<4, 2>), dim3((unsigned)grid), dim3(256), lds2, st, m);
-        else if (n > 1) {
+        else if (n > 1 && rt == 1) {   // two workgroups per CU (128 registers)
             hipLaunchKernelGGL((k_mlp2<8, 1, true>), dim3((unsigned)grid), dim3(512), lds2, st, m);
         } else {
             if (rt >= 2) hipLaunchKernelGGL((k_mlp2<8, 1, false, 2>), dim3((unsigned)grid), dim3(512), lds2, st, m);
