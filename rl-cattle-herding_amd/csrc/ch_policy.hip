@@ -37,8 +37,22 @@ constexpr int kWMax = 256;         // widest layer
 
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 
+// tanh(v) = 1 - 2 / (exp(2v) + 1) on the hardware exp2 and reciprocal: an absolute error of a few 1e-8 (the relative
+// error of a small |v| is larger -- the tests hold the forward's outputs, i.e. absolute errors of the hidden units
+// summed through the next layer, to 1e-5 and 2e-5), about 8 instructions instead of ocml's tanhf.  A 64-row tile
+// applies it to 64 values per lane and layer, which made the epilogues as long as the matrix loops.
+// CH_OCML_TANH: ocml's tanhf.
+__device__ __forceinline__ float tanh_fast(float v) {
+#ifdef CH_OCML_TANH
+    return tanhf(v);
+#else
+    const float e = __builtin_amdgcn_exp2f(v * 2.8853900817779268f);   // 2^(2 v log2 e) = e^(2v)
+    return 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
+#endif
+}
+
 __device__ __forceinline__ float act_fn(float v, int act) {
-    if (act == CH_ACT_TANH) return tanhf(v);
+    if (act == CH_ACT_TANH) return tanh_fast(v);
     if (act == CH_ACT_RELU) return v > 0.0f ? v : 0.0f;
     return v;
 }
@@ -409,7 +423,9 @@ __device__ __forceinline__ int mlp2_tile(const Plan2& pl, int wave, int j) {
 
 // the wave's weight source for layer li (tiles past the layer width clamped to its last tile / row: computed,
 // never stored), starting at pair pl.pb, and the loads of its first D pairs
-template <int NW, int TW, int D>
+// PKO: packed weights only (the host launches such a kernel only with ch_mlp.packed set): the raw-row fetch paths
+// and their address registers are not compiled in
+template <int NW, int TW, int D, bool PKO = false>
 __device__ __forceinline__ void mlp2_prologue(const MlpArgs& a, int li, const Plan2& pl, Ring2<TW, D>& r, WSrc<TW>& ws,
                                               int wave, int lane) {
     // the layer's scalars read together and pinned in scalar registers here: read where each is first used
@@ -421,7 +437,7 @@ __device__ __forceinline__ void mlp2_prologue(const MlpArgs& a, int li, const Pl
     long long pko = a.pk_off[li];
     asm volatile("" : "+s"(N), "+s"(K), "+s"(pkp), "+s"(vw), "+s"(pk), "+s"(wl), "+s"(pko));
     const int nt = (N + 15) >> 4;
-    const int mode = pk ? 0 : (((vw >> li) & 1) ? 1 : 2);
+    const int mode = (PKO || pk) ? 0 : (((vw >> li) & 1) ? 1 : 2);
     ws.K = K - 32 * pl.pb;
 #pragma unroll
     for (int j = 0; j < TW; ++j) {
@@ -433,7 +449,7 @@ __device__ __forceinline__ void mlp2_prologue(const MlpArgs& a, int li, const Pl
 #define CH_MLP2_PRO(M)                                                                                              \
     mlp2_fetch<0, TW, M>(r, ws, 0, g); mlp2_fetch<1, TW, M>(r, ws, 1, g);                                            \
     if constexpr (D == 4) { mlp2_fetch<2, TW, M>(r, ws, 2, g); mlp2_fetch<3, TW, M>(r, ws, 3, g); }
-    if (mode == 0) { CH_MLP2_PRO(0); } else if (mode == 1) { CH_MLP2_PRO(1); } else { CH_MLP2_PRO(2); }
+    if (PKO || mode == 0) { CH_MLP2_PRO(0); } else if (mode == 1) { CH_MLP2_PRO(1); } else { CH_MLP2_PRO(2); }
 #undef CH_MLP2_PRO
 }
 
@@ -465,6 +481,7 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const long long row0 = blk * TMR;
+    constexpr bool PKO = NW == 4 && RT > 1;   // packed weights only (launch_mlp_multi)
     // the arguments the tile's start needs, read together (see mlp2_prologue)
     const int* rows_dev = a.rows_dev;
     const int* env_n = a.env_n;
@@ -497,10 +514,10 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
     Ring2<TW, ring_depth<TW, RT>()> ring;
     WSrc<TW> ws;
     Plan2 pl = mlp2_plan<NW, TW>(a, 0, wave, np0);
-    mlp2_prologue<NW, TW>(a, 0, pl, ring, ws, wave, lane);
+    mlp2_prologue<NW, TW, ring_depth<TW, RT>(), PKO>(a, 0, pl, ring, ws, wave, lane);
     if (ts) ts[1] = clock64();
     // rows srow + 16 rt; as many row tiles per pass as the kQ registers hold (RT nld <= kQ for the reference's nets)
-    constexpr int kTPR = 4 * NW, kQ = 8 * kMaxPair0 / kTPR;
+    constexpr int kTPR = 4 * NW, kQ = RT > 1 && NW < 8 ? 8 : 8 * kMaxPair0 / kTPR;   // (RT > 1: more passes, fewer registers)
     const int K0 = a.dims[0], srow = tid / kTPR, sc = 4 * (tid % kTPR), nld = (8 * np0 + kTPR - 1) / kTPR;
     const int rper = max(1, min(RT, kQ / nld));
     for (int rb = 0; rb < RT; rb += rper) {
@@ -540,7 +557,7 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
     for (int li = 0; li < a.layers; ++li) {
         const bool last = li == a.layers - 1;
         const int N = a.dims[li + 1];
-        const int mode = layer_mode<TW>(a, li);
+        const int mode = PKO ? 0 : layer_mode<TW>(a, li);
         const int ntw = pl.ntw;
         const float* A = cur + 32 * pl.pb;
         float bcol[TW];
@@ -555,9 +572,11 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
 #pragma unroll
             for (int j = 0; j < TW; ++j) acc[t][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #define CH_MLP2_LOOP(NT_)                                                                                           \
-        if (mode == 0) mlp2_loop<NT_, TW, 0, RT>(acc, ring, ws, A, ldc, pl.npad, lane);                              \
-        else if (mode == 1) mlp2_loop<NT_, TW, 1, RT>(acc, ring, ws, A, ldc, pl.npad, lane);                         \
-        else mlp2_loop<NT_, TW, 2, RT>(acc, ring, ws, A, ldc, pl.npad, lane)
+        if (PKO || mode == 0) mlp2_loop<NT_, TW, 0, RT>(acc, ring, ws, A, ldc, pl.npad, lane);                       \
+        else if constexpr (!PKO) {                                                                                   \
+            if (mode == 1) mlp2_loop<NT_, TW, 1, RT>(acc, ring, ws, A, ldc, pl.npad, lane);                          \
+            else mlp2_loop<NT_, TW, 2, RT>(acc, ring, ws, A, ldc, pl.npad, lane);                                    \
+        }
         if (ntw == TW) { CH_MLP2_LOOP(TW); }
         else if constexpr (TW >= 4) { if (ntw == 3) { CH_MLP2_LOOP(3); } else if (ntw == 2) { CH_MLP2_LOOP(2); } else if (ntw == 1) { CH_MLP2_LOOP(1); } }
         else if (ntw > 0) { CH_MLP2_LOOP(1); }
@@ -568,7 +587,7 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
         const int npn = last ? 0 : pad_pairs(N);
         if (!last) {
             pl = mlp2_plan<NW, TW>(a, li + 1, wave, 0);
-            mlp2_prologue<NW, TW>(a, li + 1, pl, ring, ws, wave, lane);
+            mlp2_prologue<NW, TW, ring_depth<TW, RT>(), PKO>(a, li + 1, pl, ring, ws, wave, lane);
         }
         float* out = li & 1 ? hb1 : hb0;
         // epilogue: C/D map col = lane & 15, row = 16 t + 4 (lane >> 4) + r
@@ -591,6 +610,7 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
                 }
             }
         }
+        if (ts && li < 2) ts[11 + li] = clock64();
         if (last) break;
         // columns [N, 32 npn) of the activations: zero for the next layer's padded pairs
         const int zc = 32 * npn - N;
@@ -669,9 +689,10 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
 // SHARE: registers capped at 128 per lane (4 waves per SIMD) so that two 8-wave workgroups fit a CU -- the
 // multi-segment launches; a single forward runs without the cap (fewer, faster waves: 17-18 vs 19.7 us alone)
 // RT: row tiles of 16 per workgroup (launch_mlp_multi picks 2 or 4 for row counts that fill the chip anyway: each
-// weight pair then feeds RT x more MFMAs, the 256-wide RLlib nets' forward is otherwise bound by the weight stream)
+// weight pair then feeds RT x more MFMAs, the 256-wide RLlib nets' forward is otherwise bound by the weight stream).
+// <4, 4, *, 2> is held to 256 registers so that two workgroups share a CU (one's epilogue beside the other's MFMAs)
 template <int NW, int TW, bool SHARE = false, int RT = 1>
-__global__ __launch_bounds__(64 * NW, SHARE ? 4 : 1) void k_mlp2(MlpMulti m) {
+__global__ __launch_bounds__(64 * NW, SHARE ? 4 : ((NW == 4 && RT == 2) ? 2 : 1)) void k_mlp2(MlpMulti m) {
     int sg = 0;
     if (m.nseg > 1 && (int)blockIdx.x >= m.start[1]) sg = 1;
     if (m.nseg > 2 && (int)blockIdx.x >= m.start[2]) sg = 2;
@@ -801,6 +822,8 @@ hipError_t launch_mlp_multi(const MlpArgs* segs, int nseg, hipStream_t st, const
         for (int r : {4, 2})
             if (rows_all >= (long long)kTM * r * cus) { rt = r; break; }
     rt = std::min(rt, maxw0 > 128 ? 4 : (nw4 ? 1 : 2));   // the instantiations below
+    for (int s = 0; s < nseg; ++s)
+        if (maxw0 > 128 && !segs[s].packed) rt = 1;          // the wide row-tiled kernels read packed weights only
     MlpMulti m;
     int maxw = 0, fits = 0, grid = 0, n = 0;
     for (;;) {   // the largest rt <= the chosen one whose tile fits the LDS

@@ -53,9 +53,9 @@ def main():
     lib.ch__set_mlp_tstamp(None)
     t = ts.view(-1, 16).cpu().numpy().astype(np.float64)
     t = t[t[:, 0] > 0]
-    d = t[:, :11] - t[:, :1]
+    d = t[:, :13] - t[:, :1]
     names = ["start", "w issued", "x issued", "x stored", "staged", "L0 loop", "L0 done", "L1 loop", "L1 done",
-             "L2 loop", "end"]
+             "L2 loop", "end", "L0 stored", "L1 stored"]
     out["workgroups"] = int(len(t))
     out["phases_mean"] = {nm: float(np.mean(d[:, i])) for i, nm in enumerate(names)}
     out["phases_max"] = {nm: float(np.max(d[:, i])) for i, nm in enumerate(names)}
