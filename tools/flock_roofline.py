@@ -12,9 +12,10 @@ velocity update on every cow.  FLOP per unit (~31 FLOP + 2 sqrt 
 3 sqrt + 1 cos per cow-drone pair; sqrt and cos counted as one FLOP each, the convention that undercounts):
     cheap pair test 5, full alpha pair 34, cow-drone pair 64, gamma + velocity update + speed clip per cow 28.
 Bytes: SURVEY.md 8(d) B_flock = 24 M + 8 N per flocking env.  Peak: 78.6 TFLOP/s fp64 vector FMA (wave64 FMA in 4
-cycles per SIMD = 32 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz); ridge 78.6 / 8 TB/s = 9.8 FLOP/B, while the flock
-carries ~28-49 FLOP/B: an fp64 flock at the FMA roof moves at most ~35 % of HBM bandwidth, so the north_star's 40 %
-of HBM is out of reach in fp64 and the compute roofline is the one it can be held to.
+cycles per SIMD = 32 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz); ridge 78.6 / 8 TB/s = 9.8 FLOP/B.  The flock carries
+~16-17 useful FLOP/B by this count (~28 by SURVEY's, which folds in the transcendental costs), so it is compute-side of
+the ridge: the north_star's 40 % of HBM would need ~2/3 of the fp64 FMA peak in useful FLOP, and the compute roofline is
+the one it is held to.
 
   python tools/flock_roofline.py --out profiles/counters        # C4, C5 and 262144 x (4, 16)
 """
@@ -125,8 +126,8 @@ def main():
     out = {"code_object": code_object_hash(), "records": recs, "flop_model": FLOP, "peak_tflops": PEAK_TFLOPS,
            "note": "flock phase = launch time under phase mask 13 (flock only) minus mask 15 (skeleton), per launch, "
                    "from one burnt-in state; useful FLOP counted on the host from the state each launch starts from "
-                   "(tools/flock_roofline.py docstring); peak = fp64 vector FMA rate; ridge 9.8 FLOP/B, so 40 % of HBM "
-                   "is out of reach for an fp64 flock (~28-49 FLOP/B)"}
+                   "(tools/flock_roofline.py docstring); peak = fp64 vector FMA rate; ridge 9.8 FLOP/B; the flock carries "
+                   "~16.5 FLOP/B, so 40 % of HBM would need ~2/3 of the fp64 FMA peak in useful FLOP"}
     os.makedirs(a.out, exist_ok=True)
     with open(os.path.join(a.out, "flock_roofline.json"), "w") as fh:
         json.dump(out, fh, indent=1)
