@@ -75,7 +75,9 @@ class CattleHerdVecEnv(_VecEnvBase):
             # numpy actions through a pinned staging buffer (the previous step's copy out of it has completed: the
             # delivery below synchronises the stream)
             if getattr(self, "_act_pin", None) is None:
-                self._act_pin = torch.zeros((self.num_envs, self.num_drones, 4), dtype=torch.float32).pin_memory()
+                self._act_pin = torch.zeros((self.num_envs, self.num_drones, 4), dtype=torch.float32)
+                if str(self.batch.device).startswith("cuda"):   # (the CPU tests' stand-in batch has no device)
+                    self._act_pin = self._act_pin.pin_memory()
                 self._act_np = self._act_pin.numpy()
             np.copyto(self._act_np, np.asarray(a, np.float32).reshape(self.num_envs, -1, 4)[:, :self.num_drones])
             a = self._act_pin.to(self.batch.device, non_blocking=True)
