@@ -1043,10 +1043,20 @@ int ch_rollout_collect(ch_handle* h, const ch_rollout* rb, const ch_rollout_io* 
         ap.rows = cap;
         ap.terminal_value = h->tv_val + (fused ? rb->act_dim : 0);
         ap.tv_ld = fused ? out_w : 1;   // the value net's output width
+        ap.v_col = fused ? rb->act_dim : 0;
     }
+    // the flush: V over the queue with the reward update in the forward's epilogue (kRoleTvApply), or (a net k_mlp2
+    // does not take) the forward into tv_val and k_rollout_apply; then the queue is emptied
+    const bool tv_epi = bootstrap_truncated && mlp_multi_fits(&ftv, 1) && !(h->rollout_path & 2);
     auto flush = [&]() -> hipError_t {
-        hipError_t e = launch_mlp_multi(&ftv, 1, st);
-        if (e == hipSuccess) e = launch_rollout(ap, 3, st);
+        hipError_t e;
+        if (tv_epi) {
+            const int role = kRoleTvApply;
+            e = launch_mlp_multi(&ftv, 1, st, &role, &ap);
+        } else {
+            e = launch_mlp_multi(&ftv, 1, st);
+            if (e == hipSuccess) e = launch_rollout(ap, 3, st);
+        }
         if (e == hipSuccess) e = hipMemsetAsync(h->tv_count, 0, sizeof(int), st);
         return e;
     };

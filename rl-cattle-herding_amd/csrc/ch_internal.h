@@ -191,6 +191,7 @@ struct RolloutArgs {
     // gamma V to those rows (the same f32 fma the immediate path does)
     int defer;
     int post_only;                  // store: only the previous step's post (the last step's, before GAE)
+    int v_col;                      // kRoleTvApply: the value's column in the value net's output
     const float* term_obs;
     float* tv_obs;
     int* tv_count;
@@ -233,7 +234,9 @@ hipError_t launch_stage_ended(long long E, const uint8_t* reset, const float* te
 // Gaussian sample, its log-probability and the env actions (k_rollout_store's action half); kRoleValue -- the
 // critic's value goes into the buffer together with the previous step's post and the episode start (its
 // other half).  `ro` holds the rollout buffer for both.
-enum { kRoleNone = 0, kRoleSample = 1, kRoleValue = 2 };
+// kRoleTvApply -- the deferred truncation bootstrap's flush: the value of queued terminal observation q is added,
+// times gamma, to its rewards row tv_row[q] (k_rollout_apply's fma) straight from the epilogue.
+enum { kRoleNone = 0, kRoleSample = 1, kRoleValue = 2, kRoleTvApply = 3 };
 struct MlpMulti {
     MlpArgs seg[3];
     int nseg;

@@ -361,7 +361,10 @@ __device__ __forceinline__ void mlp2_pair(f32x4 (&acc)[RT][TW], Ring2<TW, D>& r,
     __builtin_amdgcn_sched_barrier(0);
 }
 
-// npad (a multiple of D) pairs: the steady state refills every slot it drains, the last D pairs only drain
+// npad >= 1 pairs: the steady state refills every slot it drains, the last (up to D) pairs only drain.  The loads
+// are those of the padded count (a multiple of D, in bounds: packed layers hold their padded pairs, raw fetches
+// clamp); a count that is not a multiple of D -- the first layer's live pairs -- skips the drain's all-zero tail
+// (+0 products: the outputs are bit-identical)
 template <int NT, int TW, int MODE, int RT, int D>
 __device__ __forceinline__ void mlp2_loop(f32x4 (&acc)[RT][TW], Ring2<TW, D>& r, const WSrc<TW>& ws, const float* A, int lda,
                                           int npad, int lane) {
@@ -376,10 +379,10 @@ __device__ __forceinline__ void mlp2_loop(f32x4 (&acc)[RT][TW], Ring2<TW, D>& r,
         }
     }
     mlp2_pair<0, NT, TW, MODE, false, RT>(acc, r, ws, A, lda, p0 + 0, lane);
-    mlp2_pair<1, NT, TW, MODE, false, RT>(acc, r, ws, A, lda, p0 + 1, lane);
+    if (p0 + 1 < npad) mlp2_pair<1, NT, TW, MODE, false, RT>(acc, r, ws, A, lda, p0 + 1, lane);
     if constexpr (D == 4) {
-        mlp2_pair<2, NT, TW, MODE, false, RT>(acc, r, ws, A, lda, p0 + 2, lane);
-        mlp2_pair<3, NT, TW, MODE, false, RT>(acc, r, ws, A, lda, p0 + 3, lane);
+        if (p0 + 2 < npad) mlp2_pair<2, NT, TW, MODE, false, RT>(acc, r, ws, A, lda, p0 + 2, lane);
+        if (p0 + 3 < npad) mlp2_pair<3, NT, TW, MODE, false, RT>(acc, r, ws, A, lda, p0 + 3, lane);
     }
 }
 
@@ -395,6 +398,7 @@ __device__ __forceinline__ int layer_mode(const MlpArgs& a, int li) {
 struct Plan2 {
     int ntw, pb, npad;
     bool contig;
+    int rs, tile0;   // row-split output layer (mlp2_plan_out): the wave's row tile (-1: not split) and its column tile
 };
 
 template <int NW, int TW>
@@ -413,12 +417,31 @@ __device__ __forceinline__ Plan2 mlp2_plan(const MlpArgs& a, int li, int wave, i
         pl.pb = 0;
         pl.npad = li == 0 ? np0 : pad_pairs(K);
     }
+    pl.rs = -1;
+    pl.tile0 = 0;
+    return pl;
+}
+
+// the output layer li > 0 of a row-tiled workgroup (RT > 1) whose column tiles x row tiles fit the waves (and not
+// block-diagonal): wave w computes column tile w % nt of row tile w / nt alone, instead of the first nt waves each
+// running all RT row tiles while the rest wait -- each output's fma chain is the same (bit-identical)
+template <int NW, int TW, int RT>
+__device__ __forceinline__ Plan2 mlp2_plan_out(const MlpArgs& a, int li, int wave) {
+    Plan2 pl = mlp2_plan<NW, TW>(a, li, wave, 0);
+    const int nt = (a.dims[li + 1] + 15) >> 4;
+    // (not <4, 4, *, 2>, held to 256 registers for two workgroups per CU: the split's accumulators spill there)
+    if (RT > 1 && !(NW == 4 && RT == 2) && !pl.contig && nt * RT <= NW) {
+        const bool has = wave < nt * RT;
+        pl.ntw = has ? 1 : 0;
+        pl.rs = has ? wave / nt : 0;
+        pl.tile0 = has ? wave - (wave / nt) * nt : 0;
+    }
     return pl;
 }
 
 template <int NW, int TW>
 __device__ __forceinline__ int mlp2_tile(const Plan2& pl, int wave, int j) {
-    return pl.contig ? TW * wave + j : wave + NW * j;
+    return pl.rs >= 0 ? pl.tile0 : (pl.contig ? TW * wave + j : wave + NW * j);
 }
 
 // the wave's weight source for layer li (tiles past the layer width clamped to its last tile / row: computed,
@@ -453,6 +476,58 @@ __device__ __forceinline__ void mlp2_prologue(const MlpArgs& a, int li, const Pl
 #undef CH_MLP2_PRO
 }
 
+// a hidden layer's epilogue: bias + activation of the wave's NT tiles into the LDS activations, straight-line.
+// Written per element with the activation switch and the bounds inside (act_fn, col < N), the 64-row tile's
+// epilogue compiled to ~1000 scalar branches and took as long as the layer's matrix loop (17.6 k cycles,
+// tools/mlp_marl_probe.py).  Columns past the layer width land in [N, 32 npn), which the caller zeroes next.
+template <int ACT, int NT, int NW, int TW, int RT>
+__device__ __forceinline__ void mlp2_epi_hidden(const f32x4 (&acc)[RT][TW], const float (&bcol)[TW], float* out, int ldh,
+                                                const Plan2& pl, int wave, int lane) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int col = mlp2_tile<NW, TW>(pl, wave, j) * 16 + (lane & 15);
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float v = acc[t][j][r] + bcol[j];
+                if constexpr (ACT == CH_ACT_TANH) v = tanh_fast(v);
+                else if constexpr (ACT == CH_ACT_RELU) v = v > 0.0f ? v : 0.0f;
+                out[(16 * t + (lane >> 4) * 4 + r) * ldh + col] = v;
+            }
+    }
+}
+
+// the output layer's epilogue: bias, optional clip, into y (or, STAGE, the LDS buffer the rollout epilogue reads);
+// each lane's row bound and row mask are read once per row, not per element
+template <bool STAGE, int NT, int NW, int TW, int RT>
+__device__ __forceinline__ void mlp2_epi_out(const MlpArgs& a, const f32x4 (&acc)[RT][TW], const float (&bcol)[TW],
+                                             float* out, int ldh, const Plan2& pl, int wave, int lane, long long row0,
+                                             int N) {
+    const bool clip = a.clip != 0;
+    const float lo = a.lo, hi = a.hi;
+    const long long rows = a.rows;
+    const uint8_t* mask = a.row_mask;
+    float* y = a.y;
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = 16 * t + (lane >> 4) * 4 + r;
+            const bool ok = row0 + row < rows && (!mask || mask[row0 + row]);
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                const int col = mlp2_tile<NW, TW>(pl, wave, j) * 16 + (lane & 15);
+                float v = acc[t][j][r] + bcol[j];
+                if (clip) v = fminf(fmaxf(v, lo), hi);
+                if (ok && col < N) {
+                    if constexpr (STAGE) out[row * ldh + col] = v;
+                    else y[(row0 + row) * (long long)N + col] = v;
+                }
+            }
+        }
+}
+
 // a workgroup barrier ordering LDS only: the weight loads in flight stay in flight (__syncthreads' release fence
 // would wait for every outstanding global load)
 __device__ __forceinline__ void mlp2_lds_barrier() {
@@ -472,10 +547,11 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
                                           const RolloutArgs& ro) {
     extern __shared__ __align__(16) float sm[];
     constexpr int TMR = kTM * RT;      // rows of the workgroup
+    static_assert(TMR <= 64, "the live-width scan reduces the rows in wave 0");
     float* xa = sm;                    // [TMR][lda]
     float* hb0 = RT == 1 ? xa + kTM * lda : xa + TMR * (lda > ldh ? lda : ldh);   // [TMR][ldh]
     float* hb1 = RT == 1 ? hb0 + kTM * ldh : xa;
-    __shared__ int kmax;
+    __shared__ int kmax, kany;
     __shared__ int qslot[TMR];         // kRoleValue: each row's slot in the deferred-bootstrap queue (-1: none)
     constexpr int kT = 64 * NW;        // threads
     const int tid = threadIdx.x, lane = tid & 63;
@@ -490,50 +566,66 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
     int d0 = a.dims[0], ku = a.k_unit;
     asm volatile("" : "+s"(rows_dev), "+s"(env_n), "+s"(row_mask), "+s"(rows), "+s"(rpe), "+s"(d0), "+s"(ku));
     if (rows_dev && row0 >= *rows_dev) return;   // (uniform: every thread reads the same count)
-    if (tid == 0) kmax = 0;
-    __syncthreads();
+    long long* ts = a.tstamp && tid == 0 ? a.tstamp + blk * 16 : nullptr;
+    if (ts) ts[0] = clock64();
+    // the tile's live input width (the drones of each row's env) and row mask: the rows are all in wave 0 (TMR <= 64);
+    // requested first, reduced after the loads below are in flight
+    int kr = 0, mr = 0;
     if (tid < TMR && row0 + tid < rows) {
-        int k = d0;
+        kr = d0;
         if (env_n) {
             const long long r = row0 + tid, e = r / rpe;
             const int j = (int)(r - e * rpe), n = env_n[e];
-            k = rpe == 1 ? n * ku : (j < n ? ku : 0);
-            k = min(k, d0);
+            kr = rpe == 1 ? n * ku : (j < n ? ku : 0);
+            kr = min(kr, d0);
         }
-        atomicMax(&kmax, k);
+        if (row_mask) mr = row_mask[row0 + tid];
     }
-    const bool any = __syncthreads_or(row_mask && tid < TMR && row0 + tid < rows && row_mask[row0 + tid] != 0);
-    if (row_mask && !any) return;
-    const int kloop = min(kmax, a.kcap);   // (the host sized the tile for kcap)
-    const int np0 = min(pad_pairs(max(kloop, 1)), kMaxPair0);
-    long long* ts = a.tstamp && tid == 0 ? a.tstamp + blk * 16 : nullptr;
-    if (ts) ts[0] = clock64();
 
-    // the first layer's first weight pairs (L2 hits), then the tile's input rows (from HBM): thread t owns row
-    // t / (4 NW) and float4 columns t % (4 NW) + 4 NW i, i < nld, of the padded width 32 np0
+    // the first layer's first weight pairs (L2 hits), then the first pass of the tile's input rows (from HBM) at the
+    // host's cap width kcap (zeroed past the live width when stored): thread t owns row t / (4 NW) and float4 columns
+    // t % (4 NW) + 4 NW i, i < nld, of the padded width 32 np0.  Both are in flight while wave 0 reduces the live width.
     Ring2<TW, ring_depth<TW, RT>()> ring;
     WSrc<TW> ws;
-    Plan2 pl = mlp2_plan<NW, TW>(a, 0, wave, np0);
+    Plan2 pl = mlp2_plan<NW, TW>(a, 0, wave, 1);   // (its pair count follows the scan)
     mlp2_prologue<NW, TW, ring_depth<TW, RT>(), PKO>(a, 0, pl, ring, ws, wave, lane);
     if (ts) ts[1] = clock64();
+    const int np0 = min(pad_pairs(max(a.kcap, 1)), kMaxPair0);
     // rows srow + 16 rt; as many row tiles per pass as the kQ registers hold (RT nld <= kQ for the reference's nets)
     constexpr int kTPR = 4 * NW, kQ = RT > 1 && NW < 8 ? 8 : 8 * kMaxPair0 / kTPR;   // (RT > 1: more passes, fewer registers)
     const int K0 = a.dims[0], srow = tid / kTPR, sc = 4 * (tid % kTPR), nld = (8 * np0 + kTPR - 1) / kTPR;
     const int rper = max(1, min(RT, kQ / nld));
-    for (int rb = 0; rb < RT; rb += rper) {
-        float4 xr[kQ];
+    const bool vec_x = (a.vec_w >> 7) & 1;
+    float4 xr[kQ];
+    auto load_pass = [&](int rb) {
         const long long rr0 = row0 + 16 * rb + srow;
 #pragma unroll
         for (int q = 0; q < kQ; ++q) {
             const int t = q / nld, i = q - t * nld, c = sc + 4 * kTPR * i;
             if (t < rper && rb + t < RT) {
                 const float* xs = a.x + min(rr0 + 16 * t, a.rows - 1) * K0;
-                if ((a.vec_w >> 7) & 1) xr[q] = *reinterpret_cast<const float4*>(xs + min(c, K0 - 4));
+                if (vec_x) xr[q] = *reinterpret_cast<const float4*>(xs + min(c, K0 - 4));
                 else xr[q] = make_float4(xs[min(c, K0 - 1)], xs[min(c + 1, K0 - 1)], xs[min(c + 2, K0 - 1)], xs[min(c + 3, K0 - 1)]);
             }
         }
         __builtin_amdgcn_sched_barrier(0);   // every load above issued before the first wait
-        if (ts && rb == 0) ts[2] = clock64();
+    };
+    load_pass(0);
+    if (ts) ts[2] = clock64();
+    if (wave == 0) {
+        int km = kr;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) km = max(km, __shfl_xor(km, o));
+        const bool anyr = __ballot(mr != 0) != 0;
+        if (lane == 0) { kmax = km; kany = anyr ? 1 : 0; }
+    }
+    mlp2_lds_barrier();   // (LDS only: the loads stay in flight)
+    if (row_mask && !kany) return;
+    const int kloop = min(kmax, a.kcap);   // (the host sized the tile for kcap)
+    pl.npad = min((max(kloop, 1) + 31) / 32, np0);   // the first layer multiplies its live pairs only
+    for (int rb = 0; rb < RT; rb += rper) {
+        if (rb > 0) load_pass(rb);
+        const long long rr0 = row0 + 16 * rb + srow;
 #pragma unroll
         for (int q = 0; q < kQ; ++q) {
             const int t = q / nld, i = q - t * nld, c = sc + 4 * kTPR * i;
@@ -566,6 +658,27 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
             const int col = mlp2_tile<NW, TW>(pl, wave, j) * 16 + (lane & 15);
             bcol[j] = a.b[li] && col < N ? a.b[li][col] : 0.0f;
         }
+        if (RT > 1 && !(NW == 4 && RT == 2) && pl.rs >= 0) {
+            // the row-split output layer (mlp2_plan_out): one row tile of one column tile per wave
+            f32x4 acc1[1][TW];
+#pragma unroll
+            for (int j = 0; j < TW; ++j) acc1[0][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+            const float* A1 = A + 16 * pl.rs * ldc;
+            if (ntw > 0) {
+                if (PKO || mode == 0) mlp2_loop<1, TW, 0, 1>(acc1, ring, ws, A1, ldc, pl.npad, lane);
+                else if constexpr (!PKO) {
+                    if (mode == 1) mlp2_loop<1, TW, 1, 1>(acc1, ring, ws, A1, ldc, pl.npad, lane);
+                    else mlp2_loop<1, TW, 2, 1>(acc1, ring, ws, A1, ldc, pl.npad, lane);
+                }
+            }
+            if (ts && li < 3) ts[5 + 2 * li] = clock64();
+            float* out = (li & 1 ? hb1 : hb0) + 16 * pl.rs * ldh;
+            if (ntw > 0) {
+                if (role != kRoleNone) mlp2_epi_out<true, 1, NW>(a, acc1, bcol, out, ldh, pl, wave, lane, row0 + 16 * pl.rs, N);
+                else mlp2_epi_out<false, 1, NW>(a, acc1, bcol, out, ldh, pl, wave, lane, row0 + 16 * pl.rs, N);
+            }
+            break;
+        }
         f32x4 acc[RT][TW];
 #pragma unroll
         for (int t = 0; t < RT; ++t)
@@ -586,29 +699,30 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
         const Plan2 cpl = pl;
         const int npn = last ? 0 : pad_pairs(N);
         if (!last) {
-            pl = mlp2_plan<NW, TW>(a, li + 1, wave, 0);
+            pl = li + 2 == a.layers ? mlp2_plan_out<NW, TW, RT>(a, li + 1, wave) : mlp2_plan<NW, TW>(a, li + 1, wave, 0);
             mlp2_prologue<NW, TW, ring_depth<TW, RT>(), PKO>(a, li + 1, pl, ring, ws, wave, lane);
         }
         float* out = li & 1 ? hb1 : hb0;
         // epilogue: C/D map col = lane & 15, row = 16 t + 4 (lane >> 4) + r
-#pragma unroll
-        for (int t = 0; t < RT; ++t)
-#pragma unroll
-        for (int j = 0; j < TW; ++j) {
-            if (j >= ntw) continue;
-            const int col = mlp2_tile<NW, TW>(cpl, wave, j) * 16 + (lane & 15);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = 16 * t + (lane >> 4) * 4 + r;
-                float v = acc[t][j][r] + bcol[j];
-                if (!last) {
-                    if (col < N) out[row * ldh + col] = act_fn(v, a.hidden_act);
-                } else if (col < N && row0 + row < a.rows && (!a.row_mask || a.row_mask[row0 + row])) {
-                    if (a.clip) v = fminf(fmaxf(v, a.lo), a.hi);
-                    if (role != kRoleNone) out[row * ldh + col] = v;   // (the rollout epilogue below)
-                    else a.y[(row0 + row) * (long long)N + col] = v;
-                }
-            }
+        if (!last) {
+            const int act = a.hidden_act;
+#define CH_MLP2_EPI(NT_)                                                                                            \
+            if (act == CH_ACT_TANH) mlp2_epi_hidden<CH_ACT_TANH, NT_, NW>(acc, bcol, out, ldh, cpl, wave, lane);       \
+            else if (act == CH_ACT_RELU) mlp2_epi_hidden<CH_ACT_RELU, NT_, NW>(acc, bcol, out, ldh, cpl, wave, lane);  \
+            else mlp2_epi_hidden<CH_ACT_NONE, NT_, NW>(acc, bcol, out, ldh, cpl, wave, lane);
+            if (ntw == TW) { CH_MLP2_EPI(TW); }
+            else if constexpr (TW >= 4) { if (ntw == 3) { CH_MLP2_EPI(3); } else if (ntw == 2) { CH_MLP2_EPI(2); } else if (ntw == 1) { CH_MLP2_EPI(1); } }
+            else if (ntw > 0) { CH_MLP2_EPI(1); }
+#undef CH_MLP2_EPI
+        } else if (ntw > 0) {
+            // the output layer (narrow: one or a few tiles); a rollout role stages it in LDS for the epilogue below
+#define CH_MLP2_OUT(NT_)                                                                                            \
+            if (role != kRoleNone) mlp2_epi_out<true, NT_, NW>(a, acc, bcol, out, ldh, cpl, wave, lane, row0, N);    \
+            else mlp2_epi_out<false, NT_, NW>(a, acc, bcol, out, ldh, cpl, wave, lane, row0, N);
+            if (ntw == TW) { CH_MLP2_OUT(TW); }
+            else if constexpr (TW >= 4) { if (ntw == 3) { CH_MLP2_OUT(3); } else if (ntw == 2) { CH_MLP2_OUT(2); } else { CH_MLP2_OUT(1); } }
+            else { CH_MLP2_OUT(1); }
+#undef CH_MLP2_OUT
         }
         if (ts && li < 2) ts[11 + li] = clock64();
         if (last) break;
@@ -678,6 +792,18 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
                 const int r = k / nq4, c = k - r * nq4;
                 reinterpret_cast<float4*>(ro.obs + ((long long)ro.t * ro.rows + row0 + r) * ro.obs_dim)[c] =
                     reinterpret_cast<const float4*>(a.x + (row0 + r) * (long long)ro.obs_dim)[c];
+            }
+        }
+    } else if (role == kRoleTvApply) {
+        // ch_rollout_collect's flush of the deferred truncation bootstrap: rewards[tv_row[q]] += gamma V(terminal obs
+        // q) for the tile's queue rows, k_rollout_apply's fma without its launch
+        const float* vl = a.layers & 1 ? hb0 : hb1;
+        mlp2_lds_barrier();
+        if (tid < TMR) {
+            const long long q = row0 + tid;
+            if (q < (a.rows_dev ? (long long)*a.rows_dev : a.rows)) {
+                const long long row = ro.tv_row[q];
+                ro.rewards[row] = fmaf(ro.gamma, vl[tid * ldh + ro.v_col], ro.rewards[row]);
             }
         }
     }
