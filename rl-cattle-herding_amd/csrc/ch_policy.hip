@@ -42,12 +42,17 @@ using f32x4 = __attribute__((ext_vector_type(4))) float;
 // summed through the next layer, to 1e-5 and 2e-5), about 8 instructions instead of ocml's tanhf.  A 64-row tile
 // applies it to 64 values per lane and layer, which made the epilogues as long as the matrix loops.
 // CH_OCML_TANH: ocml's tanhf.
+constexpr float kTanhScale = 2.8853900817779268f;   // 2 log2(e): 2^(kTanhScale v) = e^(2v)
+// tanh from s = kTanhScale v (the hidden epilogue folds its bias into the fma that forms s): 5 instructions, two of
+// them transcendental, with the bias add
+__device__ __forceinline__ float tanh_fast_scaled(float s) {
+    return fmaf(-2.0f, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(s) + 1.0f), 1.0f);
+}
 __device__ __forceinline__ float tanh_fast(float v) {
 #ifdef CH_OCML_TANH
     return tanhf(v);
 #else
-    const float e = __builtin_amdgcn_exp2f(v * 2.8853900817779268f);   // 2^(2 v log2 e) = e^(2v)
-    return 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
+    return tanh_fast_scaled(v * kTanhScale);
 #endif
 }
 
@@ -448,17 +453,11 @@ __device__ __forceinline__ int mlp2_tile(const Plan2& pl, int wave, int j) {
 // never stored), starting at pair pl.pb, and the loads of its first D pairs
 // PKO: packed weights only (the host launches such a kernel only with ch_mlp.packed set): the raw-row fetch paths
 // and their address registers are not compiled in
+// (the layer's scalars given: the tile's start reads layer 0's with its own, in one scalar round trip)
 template <int NW, int TW, int D, bool PKO = false>
-__device__ __forceinline__ void mlp2_prologue(const MlpArgs& a, int li, const Plan2& pl, Ring2<TW, D>& r, WSrc<TW>& ws,
-                                              int wave, int lane) {
-    // the layer's scalars read together and pinned in scalar registers here: read where each is first used
-    // (inside a branch, after another field's use) they would cost a chain of dependent scalar-cache round
-    // trips (~0.5 k cycles each at kernel start) before the first weight load
-    int N = a.dims[li + 1], K = a.dims[li], pkp = a.pk_pairs[li], vw = a.vec_w;
-    const float* pk = a.packed;
-    const float* wl = a.w[li];
-    long long pko = a.pk_off[li];
-    asm volatile("" : "+s"(N), "+s"(K), "+s"(pkp), "+s"(vw), "+s"(pk), "+s"(wl), "+s"(pko));
+__device__ __forceinline__ void mlp2_prologue_s(int N, int K, int pkp, int vw, const float* pk, const float* wl,
+                                                long long pko, int li, const Plan2& pl, Ring2<TW, D>& r, WSrc<TW>& ws,
+                                                int wave, int lane) {
     const int nt = (N + 15) >> 4;
     const int mode = (PKO || pk) ? 0 : (((vw >> li) & 1) ? 1 : 2);
     ws.K = K - 32 * pl.pb;
@@ -476,6 +475,20 @@ __device__ __forceinline__ void mlp2_prologue(const MlpArgs& a, int li, const Pl
 #undef CH_MLP2_PRO
 }
 
+template <int NW, int TW, int D, bool PKO = false>
+__device__ __forceinline__ void mlp2_prologue(const MlpArgs& a, int li, const Plan2& pl, Ring2<TW, D>& r, WSrc<TW>& ws,
+                                              int wave, int lane) {
+    // the layer's scalars read together and pinned in scalar registers here: read where each is first used
+    // (inside a branch, after another field's use) they would cost a chain of dependent scalar-cache round
+    // trips (~0.5 k cycles each at kernel start) before the first weight load
+    int N = a.dims[li + 1], K = a.dims[li], pkp = a.pk_pairs[li], vw = a.vec_w;
+    const float* pk = a.packed;
+    const float* wl = a.w[li];
+    long long pko = a.pk_off[li];
+    asm volatile("" : "+s"(N), "+s"(K), "+s"(pkp), "+s"(vw), "+s"(pk), "+s"(wl), "+s"(pko));
+    mlp2_prologue_s<NW, TW, D, PKO>(N, K, pkp, vw, pk, wl, pko, li, pl, r, ws, wave, lane);
+}
+
 // a hidden layer's epilogue: bias + activation of the wave's NT tiles into the LDS activations, straight-line.
 // Written per element with the activation switch and the bounds inside (act_fn, col < N), the 64-row tile's
 // epilogue compiled to ~1000 scalar branches and took as long as the layer's matrix loop (17.6 k cycles,
@@ -486,13 +499,19 @@ __device__ __forceinline__ void mlp2_epi_hidden(const f32x4 (&acc)[RT][TW], cons
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
         const int col = mlp2_tile<NW, TW>(pl, wave, j) * 16 + (lane & 15);
+        const float bs = bcol[j] * kTanhScale;   // tanh: the bias folded into the exponent's fma
 #pragma unroll
         for (int t = 0; t < RT; ++t)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                float v = acc[t][j][r] + bcol[j];
-                if constexpr (ACT == CH_ACT_TANH) v = tanh_fast(v);
-                else if constexpr (ACT == CH_ACT_RELU) v = v > 0.0f ? v : 0.0f;
+                float v;
+#ifdef CH_OCML_TANH
+                if constexpr (ACT == CH_ACT_TANH) v = tanhf(acc[t][j][r] + bcol[j]);
+#else
+                if constexpr (ACT == CH_ACT_TANH) v = tanh_fast_scaled(fmaf(acc[t][j][r], kTanhScale, bs));
+#endif
+                else if constexpr (ACT == CH_ACT_RELU) { v = acc[t][j][r] + bcol[j]; v = v > 0.0f ? v : 0.0f; }
+                else v = acc[t][j][r] + bcol[j];
                 out[(16 * t + (lane >> 4) * 4 + r) * ldh + col] = v;
             }
     }
@@ -558,26 +577,36 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const long long row0 = blk * TMR;
     constexpr bool PKO = NW == 4 && RT > 1;   // packed weights only (launch_mlp_multi)
-    // the arguments the tile's start needs, read together (see mlp2_prologue)
+    // the arguments the tile's start needs -- the live-width scan's and the first layer's (plan, weight fetch, input
+    // rows) -- read together and pinned (see mlp2_prologue): one scalar round trip before the first loads (read where
+    // each is used, the start of a tile was ~5 k cycles of dependent scalar reads, tools/mlp_marl_probe.py --ctde)
     const int* rows_dev = a.rows_dev;
     const int* env_n = a.env_n;
     const uint8_t* row_mask = a.row_mask;
     long long rows = a.rows, rpe = a.rows_per_env;
     int d0 = a.dims[0], ku = a.k_unit;
-    asm volatile("" : "+s"(rows_dev), "+s"(env_n), "+s"(row_mask), "+s"(rows), "+s"(rpe), "+s"(d0), "+s"(ku));
+    int d1 = a.dims[1], pkp0 = a.pk_pairs[0], vw = a.vec_w, kcap = a.kcap;
+    const float* pk = a.packed;
+    const float* w0 = a.w[0];
+    const float* x = a.x;
+    long long pko0 = a.pk_off[0];
+    asm volatile("" : "+s"(rows_dev), "+s"(env_n), "+s"(row_mask), "+s"(rows), "+s"(rpe), "+s"(d0), "+s"(ku), "+s"(d1),
+                 "+s"(pkp0), "+s"(vw), "+s"(kcap), "+s"(pk), "+s"(w0), "+s"(x), "+s"(pko0));
     if (rows_dev && row0 >= *rows_dev) return;   // (uniform: every thread reads the same count)
     long long* ts = a.tstamp && tid == 0 ? a.tstamp + blk * 16 : nullptr;
     if (ts) ts[0] = clock64();
     // the tile's live input width (the drones of each row's env) and row mask: the rows are all in wave 0 (TMR <= 64);
     // requested first, reduced after the loads below are in flight
-    int kr = 0, mr = 0;
-    if (tid < TMR && row0 + tid < rows) {
-        kr = d0;
+    // (only the loads here: the width is formed after the weight and row loads below are issued, so that waiting for
+    // these does not hold them back; 32-bit row arithmetic, rows < 2^31)
+    const bool rl = tid < TMR && row0 + tid < rows;
+    int n_env = 0, jr = 0, mr = 0;
+    if (rl) {
         if (env_n) {
-            const long long r = row0 + tid, e = r / rpe;
-            const int j = (int)(r - e * rpe), n = env_n[e];
-            kr = rpe == 1 ? n * ku : (j < n ? ku : 0);
-            kr = min(kr, d0);
+            const int ri = (int)(row0 + tid), rp = (int)rpe;
+            const int e = rp == 1 ? ri : ri / rp;
+            jr = ri - e * rp;
+            n_env = env_n[e];
         }
         if (row_mask) mr = row_mask[row0 + tid];
     }
@@ -587,33 +616,65 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
     // t % (4 NW) + 4 NW i, i < nld, of the padded width 32 np0.  Both are in flight while wave 0 reduces the live width.
     Ring2<TW, ring_depth<TW, RT>()> ring;
     WSrc<TW> ws;
-    Plan2 pl = mlp2_plan<NW, TW>(a, 0, wave, 1);   // (its pair count follows the scan)
-    mlp2_prologue<NW, TW, ring_depth<TW, RT>(), PKO>(a, 0, pl, ring, ws, wave, lane);
+    Plan2 pl;   // layer 0 (mlp2_plan; its pair count follows the scan)
+    {
+        const int nt = (d1 + 15) >> 4;
+        pl.contig = false;
+        pl.ntw = wave < nt ? min(TW, (nt - wave + NW - 1) / NW) : 0;
+        pl.pb = 0;
+        pl.npad = 1;
+        pl.rs = -1;
+        pl.tile0 = 0;
+    }
+    mlp2_prologue_s<NW, TW, ring_depth<TW, RT>(), PKO>(d1, d0, pkp0, vw, pk, w0, pko0, 0, pl, ring, ws, wave, lane);
     if (ts) ts[1] = clock64();
-    const int np0 = min(pad_pairs(max(a.kcap, 1)), kMaxPair0);
+    const int np0 = min(pad_pairs(max(kcap, 1)), kMaxPair0);
     // rows srow + 16 rt; as many row tiles per pass as the kQ registers hold (RT nld <= kQ for the reference's nets)
     constexpr int kTPR = 4 * NW, kQ = RT > 1 && NW < 8 ? 8 : 8 * kMaxPair0 / kTPR;   // (RT > 1: more passes, fewer registers)
-    const int K0 = a.dims[0], srow = tid / kTPR, sc = 4 * (tid % kTPR), nld = (8 * np0 + kTPR - 1) / kTPR;
+    const int K0 = d0, srow = tid / kTPR, sc = 4 * (tid % kTPR), nld = (8 * np0 + kTPR - 1) / kTPR;
     const int rper = max(1, min(RT, kQ / nld));
-    const bool vec_x = (a.vec_w >> 7) & 1;
+    const bool vec_x = (vw >> 7) & 1, vec2_x = !vec_x && (K0 & 1) == 0 && K0 >= 2 && (reinterpret_cast<uintptr_t>(x) & 7) == 0;
     float4 xr[kQ];
+    // (the vector / element choice outside the unrolled loop: inside it, every iteration's two paths wrote the same
+    // registers and the compiler drained the loads in flight at each join -- one memory round trip per float4)
     auto load_pass = [&](int rb) {
         const long long rr0 = row0 + 16 * rb + srow;
+        if (vec_x) {
 #pragma unroll
-        for (int q = 0; q < kQ; ++q) {
-            const int t = q / nld, i = q - t * nld, c = sc + 4 * kTPR * i;
-            if (t < rper && rb + t < RT) {
-                const float* xs = a.x + min(rr0 + 16 * t, a.rows - 1) * K0;
-                if (vec_x) xr[q] = *reinterpret_cast<const float4*>(xs + min(c, K0 - 4));
-                else xr[q] = make_float4(xs[min(c, K0 - 1)], xs[min(c + 1, K0 - 1)], xs[min(c + 2, K0 - 1)], xs[min(c + 3, K0 - 1)]);
+            for (int q = 0; q < kQ; ++q) {
+                const int t = q / nld, i = q - t * nld, c = sc + 4 * kTPR * i;
+                if (t < rper && rb + t < RT)
+                    xr[q] = *reinterpret_cast<const float4*>(x + min(rr0 + 16 * t, rows - 1) * K0 + min(c, K0 - 4));
+            }
+        } else if (vec2_x) {   // even rows (the RLlib agents' 86 floats): two float2 (past the row: clamped, zeroed below)
+#pragma unroll
+            for (int q = 0; q < kQ; ++q) {
+                const int t = q / nld, i = q - t * nld, c = sc + 4 * kTPR * i;
+                if (t < rper && rb + t < RT) {
+                    const float* xs = x + min(rr0 + 16 * t, rows - 1) * K0;
+                    const float2 lo = *reinterpret_cast<const float2*>(xs + min(c, K0 - 2));
+                    const float2 hi = *reinterpret_cast<const float2*>(xs + min(c + 2, K0 - 2));
+                    xr[q] = make_float4(lo.x, lo.y, hi.x, hi.y);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < kQ; ++q) {
+                const int t = q / nld, i = q - t * nld, c = sc + 4 * kTPR * i;
+                if (t < rper && rb + t < RT) {
+                    const float* xs = x + min(rr0 + 16 * t, rows - 1) * K0;
+                    xr[q] = make_float4(xs[min(c, K0 - 1)], xs[min(c + 1, K0 - 1)], xs[min(c + 2, K0 - 1)], xs[min(c + 3, K0 - 1)]);
+                }
             }
         }
         __builtin_amdgcn_sched_barrier(0);   // every load above issued before the first wait
     };
     load_pass(0);
+    asm volatile("" : "+v"(mr), "+v"(n_env));   // (the row mask and width used from here: their wait lands here)
     if (ts) ts[2] = clock64();
     if (wave == 0) {
-        int km = kr;
+        int km = 0;
+        if (rl) km = env_n ? min(rpe == 1 ? n_env * ku : (jr < n_env ? ku : 0), d0) : d0;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) km = max(km, __shfl_xor(km, o));
         const bool anyr = __ballot(mr != 0) != 0;
@@ -621,7 +682,7 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
     }
     mlp2_lds_barrier();   // (LDS only: the loads stay in flight)
     if (row_mask && !kany) return;
-    const int kloop = min(kmax, a.kcap);   // (the host sized the tile for kcap)
+    const int kloop = min(kmax, kcap);   // (the host sized the tile for kcap)
     pl.npad = min((max(kloop, 1) + 31) / 32, np0);   // the first layer multiplies its live pairs only
     for (int rb = 0; rb < RT; rb += rper) {
         if (rb > 0) load_pass(rb);
@@ -630,7 +691,7 @@ __device__ __forceinline__ void mlp2_body(const MlpArgs& a, long long blk, int l
         for (int q = 0; q < kQ; ++q) {
             const int t = q / nld, i = q - t * nld, c = sc + 4 * kTPR * i;
             if (t < rper && rb + t < RT && c < 32 * np0) {
-                const bool srv = rr0 + 16 * t < a.rows;
+                const bool srv = rr0 + 16 * t < rows;
                 float4 v = xr[q];
                 v.x = srv && c < kloop ? v.x : 0.0f;
                 v.y = srv && c + 1 < kloop ? v.y : 0.0f;

@@ -3,6 +3,7 @@
 tiles per workgroup come from CH_MLP_RT (read once per process: run one process per setting).
 
   CH_MLP_RT=4 python tools/mlp_marl_probe.py
+  python tools/mlp_marl_probe.py --ctde      # the SB3 actor (model-v16-6) on 8192 CTDE envs: the PPO forward's kernel
 """
 import ctypes
 import json
@@ -34,14 +35,24 @@ def timed(fn, k=100):
 
 def main():
     rt = int(os.environ.get("CH_MLP_RT", "0") or 0)
-    b = HerdBatch(4096, 4, 32, mode="marl")
-    b.reset()
-    pol = DevicePolicy(DevicePolicy.random_layers([86, 256, 256, 8], seed=1), "tanh", None, cache_packed=True)
-    val = DevicePolicy(DevicePolicy.random_layers([86, 256, 256, 1], seed=2), "tanh", None, cache_packed=True)
-    rows = 4096 * 4
-    yp = torch.empty(rows, 8, device=b.device)
+    ctde = "--ctde" in sys.argv
+    if ctde:
+        b = HerdBatch(8192, 4, 16, mode="ctde")
+        b.reset()
+        d = np.load(os.path.join(ROOT, "tests", "golden", "policy_ctde_v16_6.npz"))
+        sd = {k.replace("__", "."): torch.tensor(d[k]) for k in d.files if "__" in k}
+        pol = DevicePolicy.sb3_actor(sd, clip=False, cache_packed=True)
+        val = DevicePolicy.sb3_critic(sd, cache_packed=True)
+        rows, na, flops_row = 8192, 48, 2.0 * (344 * 128 + 128 * 128 + 128 * 48)
+    else:
+        b = HerdBatch(4096, 4, 32, mode="marl")
+        b.reset()
+        pol = DevicePolicy(DevicePolicy.random_layers([86, 256, 256, 8], seed=1), "tanh", None, cache_packed=True)
+        val = DevicePolicy(DevicePolicy.random_layers([86, 256, 256, 1], seed=2), "tanh", None, cache_packed=True)
+        rows, na, flops_row = 4096 * 4, 8, 2.0 * (86 * 256 + 256 * 256 + 256 * 8)
+    yp = torch.empty(rows, na, device=b.device)
     yv = torch.empty(rows, 1, device=b.device)
-    out = {"rt_env": rt, "policy_us": timed(lambda: pol.forward_batch(b, yp)),
+    out = {"net": "ctde actor" if ctde else "marl policy", "rt_env": rt, "policy_us": timed(lambda: pol.forward_batch(b, yp)),
            "value_us": timed(lambda: val.forward_batch(b, yv))}
     # phase clocks of one policy forward (wave 0 of each workgroup, cycles from its start)
     lib = _lib.lib()
@@ -59,7 +70,7 @@ def main():
     out["workgroups"] = int(len(t))
     out["phases_mean"] = {nm: float(np.mean(d[:, i])) for i, nm in enumerate(names)}
     out["phases_max"] = {nm: float(np.max(d[:, i])) for i, nm in enumerate(names)}
-    flops = 2.0 * rows * (86 * 256 + 256 * 256 + 256 * 8)
+    flops = rows * flops_row
     out["policy_tflops"] = flops / (out["policy_us"] * 1e-6) / 1e12
     print(json.dumps(out), flush=True)
     b.close()
