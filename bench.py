@@ -156,6 +156,18 @@ def policy_rollout(b, n, steps, warmup):
     return out
 
 
+PPO_BURN_IN = 300
+
+
+def burn_in(b, steps=PPO_BURN_IN):
+    """Reset, then random-action steps with auto-reset before a timed collection: a training run's rollouts see the
+    envs' episode phases spread by their resets (half of them flocking on any step, BaseAviary.py:454), not the
+    lock-step phases of a batch that has just been reset (every env flocking on the same steps)."""
+    b.reset()
+    for _ in range(steps):
+        b.step(None, random_actions=True, autoreset=True, terminal_obs=False)
+
+
 def ppo_rollout(b, d, T=32, fused=False):
     """SB3 collect_rollouts on the device (cattleherd.rollout): per step the actor and critic forwards (fused=True:
     one launch of the two heads packed as one net, DevicePolicy.sb3_actor_critic, bit-identical to the separate
@@ -171,7 +183,7 @@ def ppo_rollout(b, d, T=32, fused=False):
     nets = (DevicePolicy.sb3_actor_critic(sd), None) if fused else (actor, critic)
     log_std = torch.full((actor.dims[-1],), -1.0, device=b.device)   # log_std_init (CTDECattleHerder.py:122)
     rb = DeviceRolloutBuffer(b, T, act_dim=actor.dims[-1])
-    b.reset()
+    burn_in(b)
     rb.collect(*nets, log_std, seed=1)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -179,6 +191,7 @@ def ppo_rollout(b, d, T=32, fused=False):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     out = {"env_steps_per_s": b.n_envs * T / dt, "ms_per_step": dt / T * 1000.0, "n_steps": T,
+           "burn_in": PPO_BURN_IN,
            "policy": "actor + critic fused (one forward per step)" if fused else "actor and critic separately",
            "buffer_GB": sum(t.numel() * 4 for t in (rb.obs, rb.actions)) / 1e9}
     del rb
@@ -198,7 +211,7 @@ def marl_ppo_rollout(b, T=32):
     policy = DevicePolicy(DevicePolicy.random_layers([86, 256, 256, 8], seed=1), "tanh", None)
     value = DevicePolicy(DevicePolicy.random_layers([86, 256, 256, 1], seed=2), "tanh", None)
     rb = DeviceMarlRolloutBuffer(b, T)
-    b.reset()
+    burn_in(b)
     rb.collect(policy, value, seed=1)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -206,7 +219,7 @@ def marl_ppo_rollout(b, T=32):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     out = {"env_steps_per_s": b.n_envs * T / dt, "agent_steps_per_s": b.n_envs * b.num_drones * T / dt,
-           "ms_per_step": dt / T * 1000.0, "n_steps": T,
+           "ms_per_step": dt / T * 1000.0, "n_steps": T, "burn_in": PPO_BURN_IN,
            "policy": "RLlib default model 86-256-256-8 (mean, log_std) + value 86-256-256-1, tanh, random init, f32",
            "gae": "per agent, gamma 0.99, lambda 1.0 (RLlib PPO default)",
            "buffer_GB": sum(t.numel() * t.element_size() for t in (rb.obs, rb.actions)) / 1e9}

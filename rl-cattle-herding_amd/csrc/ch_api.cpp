@@ -1003,7 +1003,9 @@ int ch_rollout_collect(ch_handle* h, const ch_rollout* rb, const ch_rollout_io* 
     // every kTvEvery steps one forward over the queue gives their values, added to those rewards rows (the queue
     // holds at most kTvEvery * E rows).  Per step that leaves two launches with separate nets (forwards with the
     // store in their epilogues, step) and three with a fused net or CH_ROLLOUT_STORE_KERNEL=1 (forward, store, step).
-    constexpr int kTvEvery = 8;
+    // (the period: 16 steps, fewer when the queue would pass 1 GiB -- one flush is a whole forward's latency, ~20 us
+    // at configs[2]'s size, whatever the queue holds)
+    const int kTvEvery = (int)std::min<long long>(16, std::max<long long>(1, (1LL << 30) / ((long long)h->E * ra.obs_dim * 4)));
     const bool copy_each = (h->rollout_path & 1) != 0;
     const size_t slot = (size_t)h->E * (size_t)ra.obs_dim;
     auto obs_at = [&](int32_t t) { return (t == 0 || t == rb->n_steps || copy_each) ? sio->obs : rb->obs + (size_t)t * slot; };
