@@ -13,37 +13,29 @@ namespace ch {
 // curriculum_learning.py:200-219
 __device__ __forceinline__ void curriculum_success(const Level* LT, int& level, int& tally) {
     tally += 1;
-    if (tally >= LT[level].required_tally) {
-        tally = 0;
-        level += 1;
-        if (level >= 8) level = 7;
-    }
+    const bool up = tally >= LT[level].required_tally;   // (selects: the env lanes of a wave differ)
+    tally = up ? 0 : tally;
+    level = up ? min(level + 1, 7) : level;
 }
 
 // _computeTerminated (CattleAviary.py:422-492; MARLCattleAviary.py:246-321)
+// Branch-free: every level's test is evaluated and the level selects (the same operations; the env lanes of a
+// wave sit at different levels, so the if-chain ran most of its arms anyway, plus the exec-mask bookkeeping).
 template <class R>
 __device__ __forceinline__ bool term_call_L(const Level& L, int level, R& clock, R clock_inc, R min_spacing, R cent,
                                             R eff) {
-    if (level == 0 || level == 1) {
-        R up = R(L.desired) + R(L.desired) * R(L.tol), lo = R(L.desired) - R(L.desired) * R(L.tol);
-        if (min_spacing < up && min_spacing > lo) {
-            clock += clock_inc;
-            if (clock >= R(L.hold)) return true;
-        } else {
-            clock = 0;
-        }
-    } else if (level == 2 || level == 3) {
-        if (cent < R(L.approach_min)) return true;
-    } else if (level == 4 || level == 6) {
-        if (eff > R(L.min_eff)) return true;
-    } else if (level == 5) {
-        if (eff > R(L.min_eff)) {
-            R up = R(L.cattle_desired) + R(L.cattle_desired) * R(L.cattle_tol);
-            R lo = R(L.cattle_desired) - R(L.cattle_desired) * R(L.cattle_tol);
-            if (min_spacing < up && min_spacing > lo) return true;
-        }
-    }
-    return false;
+    const R up = R(L.desired) + R(L.desired) * R(L.tol), lo = R(L.desired) - R(L.desired) * R(L.tol);
+    const bool l01 = level == 0 || level == 1;
+    const bool in01 = min_spacing < up && min_spacing > lo;
+    const R held = clock + clock_inc;
+    const bool t01 = l01 && in01 && held >= R(L.hold);
+    clock = l01 ? (in01 ? held : R(0)) : clock;
+    const bool t23 = (level == 2 || level == 3) && cent < R(L.approach_min);
+    const bool t46 = (level == 4 || level == 6) && eff > R(L.min_eff);
+    const R cup = R(L.cattle_desired) + R(L.cattle_desired) * R(L.cattle_tol);
+    const R clo = R(L.cattle_desired) - R(L.cattle_desired) * R(L.cattle_tol);
+    const bool t5 = level == 5 && eff > R(L.min_eff) && min_spacing < cup && min_spacing > clo;
+    return t01 || t23 || t46 || t5;
 }
 template <class R>
 __device__ __forceinline__ bool term_call(const Level* LT, int level, R& clock, R clock_inc, R min_spacing, R cent, R eff) {

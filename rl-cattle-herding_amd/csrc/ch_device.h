@@ -631,20 +631,24 @@ __device__ __forceinline__ R pair_terms_n(R n, R zx, R zy, R pix, R piy, R pjx, 
 }
 
 // ---- spacing rewards: CattleAviary.py:572-679 -------------------------------------------------
+// (both spacing terms branch-free: each candidate is evaluated and one selected, the same operations as the
+// reference's if-chain -- the drone lanes of a wave take different branches, so a branchy form ran every branch
+// anyway, plus the exec-mask bookkeeping)
 template <class R> __device__ __forceinline__ R simple_spacing(R r, const Level& L) {
     R desired = R(L.desired), tol = desired * R(L.tol);
     R lb = desired - tol, ub = desired + tol;
-    if (lb <= r && r <= ub) return R(1.0);
-    if (r < lb) return R(-1) + (r / lb) * R(2);
-    if (r > ub) return R(1) - ((r - ub) / (R(7.0) - ub)) * R(2);
-    return R(-1.0);
+    const R below = R(-1) + (r / lb) * R(2);
+    const R above = R(1) - ((r - ub) / (R(7.0) - ub)) * R(2);
+    return (lb <= r && r <= ub) ? R(1.0) : (r < lb ? below : (r > ub ? above : R(-1.0)));
 }
 template <class R> __device__ __forceinline__ R complex_spacing(R r, const Level& L) {
     R ds = R(L.desired);
     R t = divc(r - ds, R(0.4 + 1e-9));
     R gauss = m_exp(R(-0.5) * (t * t));
-    R coll = r < R(0.3) ? R(-1.0) * (R(1.0) - divc(r, R(0.3 + 1e-9))) : R(0.0);
-    R pull = r > R(1.5) ? divc(R(-0.3) * (r - R(1.5)), R(5.0 - 1.5)) : R(0.0);
+    const R coll_v = R(-1.0) * (R(1.0) - divc(r, R(0.3 + 1e-9)));
+    const R pull_v = divc(R(-0.3) * (r - R(1.5)), R(5.0 - 1.5));
+    R coll = r < R(0.3) ? coll_v : R(0.0);
+    R pull = r > R(1.5) ? pull_v : R(0.0);
     R rew = gauss + coll + pull;
     rew += R(0.1) * (R(1) - fabs(r - ds));
     return rew;

@@ -1024,16 +1024,22 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             int i1 = -1, i2 = -1;
             uint8_t f = 0;
             bool iso = true;
+            // (branch-free: every other drone slot is evaluated and the updates selected -- the lanes' j == i
+            // differ, so the branchy loop ran every body anyway)
             CH_UNROLL for (int j = 0; j < N; ++j) {
-                if (j >= n) break;
-                if (j == i) continue;
+                const bool v = j < n && j != i;
                 const R d = norm2(S.dx[b0 + j] - xi, S.dy[b0 + j] - yi);
-                if (d != d) f |= 8;
-                if (d < m1) { m2 = m1; m1 = d; } else if (d < m2) m2 = d;
-                if (d < R(kCollision)) f |= 2;
-                if (!(d > R(kMaxFormation))) iso = false;
-                if (i1 < 0 || d < b1) { i2 = i1; b2 = b1; i1 = j; b1 = d; }
-                else if (i2 < 0 || d < b2) { i2 = j; b2 = d; }
+                f |= (v && d != d) ? 8 : 0;
+                const bool lt1 = v && d < m1, lt2 = v && !(d < m1) && d < m2;
+                m2 = lt1 ? m1 : (lt2 ? d : m2);
+                m1 = lt1 ? d : m1;
+                f |= (v && d < R(kCollision)) ? 2 : 0;
+                iso = iso && !(v && !(d > R(kMaxFormation)));
+                const bool n1 = v && (i1 < 0 || d < b1), n2 = v && !n1 && (i2 < 0 || d < b2);
+                i2 = n1 ? i1 : (n2 ? j : i2);
+                b2 = n1 ? b1 : (n2 ? d : b2);
+                i1 = n1 ? j : i1;
+                b1 = n1 ? d : b1;
             }
             if (iso) f |= 4;
             if (fabs(pos[2] - R(kTargetAlt)) > R(kTargetAlt * 0.6)) f |= 1;
