@@ -726,7 +726,9 @@ __device__ __forceinline__ void flock_combine(const StepParams<R>& p, V2Smem<R>&
 
 // GT/NT/MT > 0 specialise the kernel for one geometry (envs per workgroup, drones, cattle): the LDS
 // carve and all index arithmetic then fold to immediates, which keeps the kernel within the SGPR file.
-template <class R, int MODE, int GT, int NT, int MT, bool PHYS = false, bool PW = false>
+// TOBS: the instantiation that writes terminal observations from their producers in the fast path (configs[3]'s
+// geometry, launched when the step asks for them); without it the same geometry takes the drained-copy path for them
+template <class R, int MODE, int GT, int NT, int MT, bool PHYS = false, bool PW = false, bool TOBS = false>
 __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
     extern __shared__ __align__(16) unsigned char smem[];
     constexpr bool marl = MODE == 1;
@@ -944,7 +946,11 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
     // drone wave; cattle state: the phase-0 lane; obs: the single late writer), with no drain or sync.
     // Only the 16-env x 4-drone geometry: at 2 drones x 8 cattle (C2/C3, 3 cow waves) the final pass after the
     // reset list costs more than the reset sync it saves (C2 16.2 -> 17.2 us, C3 17.1 -> 17.8 us).
-    const bool late = sep && GT == 16 && NT == 4, fast = late && !p.terminal_obs;
+    // tobs (fast): the terminal observation of a reset env is written by the same producers, into p.terminal_obs,
+    // each from the values it holds (drone rows: the drone wave; Euler angles, cattle entries, constant bytes: the cow
+    // waves), instead of a drained copy of the finished block behind two cow-wave syncs
+    const bool late = sep && GT == 16 && NT == 4, fast = late && (TOBS || !p.terminal_obs);
+    const bool tobs = TOBS && p.terminal_obs != nullptr;
     float* obs_wg = p.obs + (long long)e0 * RW;
     // final per-env scalars, held by the drone wave's env lanes until the write-back
     int f_n = 0, f_sc = 0, f_scA = 0, f_hp = 0, f_level = 0, f_tally = 0, f_spawn = 0, f_active = 0, f_episode = 0;
@@ -1017,6 +1023,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
         if (p.evald && live) CH_STS(&p.evald[di], eval_distance_step(ev_acc, ei[I_SC * G + dg] == 0, px0, py0, pos[0], pos[1]));
 
         // per-drone reward terms (CattleAviary.py:230-246, 572-679) and neighbour obs (BaseRLAviary.py:303-317)
+        int nb1 = -1, nb2 = -1;   // the two nearest drones (kept for a fast reset's terminal observation)
         if (live && task) {
             const int i = dk, b0 = dg * N;
             const R xi = pos[0], yi = pos[1];
@@ -1047,6 +1054,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             if constexpr (!SPLIT) spacing_terms(S, LT[ei[I_LEVEL * G + dg]], p.compat != 0, tid, m1, m2);
             // offsets from the f64 positions in f32 mode (S.dxd; the same array as S.dx in f64 mode)
             if (wobs) obs_nbr(obs_wg + dg * RW, S.dxd, S.dyd, b0, i, i1, i2);
+            nb1 = i1; nb2 = i2;
         }
         lds_signal(fl + F_T);
         if (tid == 0) TS(5, (long long)clock64());
@@ -1391,6 +1399,13 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             wave_sync();   // the reset flags and NUM_DRONES draws of the env lanes
             const bool rd = dlane && ei[I_RESET * G + dg];
             const int n_new = rd ? ei[I_NEWN * G + dg] : 0;
+            if (tobs && wobs && rd && live) {
+                // the terminal observation's own and neighbour entries, from this lane's end-of-episode state (its
+                // Euler angles, cattle entries and constant bytes come from the cow waves)
+                float* tb = p.terminal_obs + (long long)(e0 + dg) * RW;
+                obs_own_nrpy(tb, dk, pos[2], v, w);
+                if (task) obs_nbr(tb, S.dxd, S.dyd, dg * N, dk, nb1, nb2);
+            }
             double xd = 0, yd = 0, zd = 0;
             if (rd) {
                 reset_drone_xyz(dk, n_new, xd, yd, zd);
@@ -1745,15 +1760,20 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             if (b >= Gv * N) break;
             if (u < Gv * N) {
                 const int g = qdiv(u, N, rN), k = u - g * N;
-                if (k < ei[I_N * G + g] && !(fast && ei[I_RESET * G + g])) {
+                const bool rsf = fast && ei[I_RESET * G + g];   // (its cache and observation: the new episode's)
+                if (k < ei[I_N * G + g] && (!rsf || (tobs && wobs))) {
                     const int GN = G * N;
                     const R qq[4] = {S.dq[u], S.dq[GN + u], S.dq[2 * GN + u], S.dq[3 * GN + u]};
                     R r3[3];
                     quat_to_euler(qq, r3);
                     const long long dd = (long long)e0 * N + u;
+                    if (!rsf) {
 #pragma unroll
-                    for (int c = 0; c < 3; ++c) CH_STS(&p.rpy[c * DS + dd], r3[c]);
-                    if (wobs) obs_rpy(obs_wg + g * RW, k, r3);
+                        for (int c = 0; c < 3; ++c) CH_STS(&p.rpy[c * DS + dd], r3[c]);
+                        if (wobs) obs_rpy(obs_wg + g * RW, k, r3);
+                    } else {
+                        obs_rpy(p.terminal_obs + (long long)(e0 + g) * RW, k, r3);   // the terminal observation's
+                    }
                 }
             }
           }
@@ -1904,6 +1924,9 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                 const int n_old = ei[I_N * G + g];
                 const long long ci = (long long)e0 * M + u;
                 if (rs_) {
+                    if (tobs && wobs && j < m_obs)   // the terminal observation's entries, from this step's positions
+                        obs_cattle(p.terminal_obs + (long long)(e0 + g) * RW, S.dxd, S.dyd, g * N, j, n_old, cat_off,
+                                   S.cxd[u], S.cyd[u]);
                     // the new episode's spawn position (prefetched in LDS; in f32 mode re-read in f64 from the table)
                     const double x = MIX ? spawn_d(g, j, 0) : (double)S.spx[u], y = MIX ? spawn_d(g, j, 1) : (double)S.spy[u];
                     p.cattle[0 * CS + ci] = R(x); p.cattle[1 * CS + ci] = R(y);
@@ -1933,6 +1956,11 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
                 if (ei[I_FLOCK * G + g]) arrive_final(u);
             }
             if (!ew) euler_pass();
+            if (tobs && wobs)   // the terminal observations' constant bytes (no producer writes them)
+                for (int k = 0; k < nr; ++k) {
+                    const int g = ei[RS_LIST + k];
+                    obs_zero_env(p.terminal_obs + (long long)(e0 + g) * RW, ei[I_N * G + g], rows, cat_off, m_obs, ct, CW);
+                }
             TS_MAX(60);
         }
         if (nr && !fast) {   // uniform across the cow waves
@@ -2027,7 +2055,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
     }
 }
 
-template <class R, int MODE, int GT, int NT, int MT, bool PHYS = false, bool PW = false>
+template <class R, int MODE, int GT, int NT, int MT, bool PHYS = false, bool PW = false, bool TOBS = false>
 static hipError_t launch_v2_kernel(const StepParams<R>& p, int block, size_t lds, hipStream_t st, bool launch) {
     // opt-in to > 64 KiB of dynamic LDS, once per device (the attribute is per device context)
     static std::atomic<unsigned long long> attr_set{0};
@@ -2036,14 +2064,14 @@ static hipError_t launch_v2_kernel(const StepParams<R>& p, int block, size_t lds
     if (e != hipSuccess) return e;
     const unsigned long long bit = 1ull << (dev & 63);
     if (!(attr_set.load(std::memory_order_relaxed) & bit)) {
-        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_step2<R, MODE, GT, NT, MT, PHYS, PW>),
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_step2<R, MODE, GT, NT, MT, PHYS, PW, TOBS>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr_set.fetch_or(bit, std::memory_order_relaxed);
     }
     if (!launch) return hipSuccess;
     dim3 grid((p.E + p.G - 1) / p.G);
-    hipLaunchKernelGGL((k_step2<R, MODE, GT, NT, MT, PHYS, PW>), grid, dim3(block), lds, st, p);
+    hipLaunchKernelGGL((k_step2<R, MODE, GT, NT, MT, PHYS, PW, TOBS>), grid, dim3(block), lds, st, p);
     return hipGetLastError();
 }
 
@@ -2064,7 +2092,14 @@ hipError_t launch_step_v2(const StepParams<R>& p, int block, size_t lds, hipStre
     }
     if (p.mode == 1) return launch_v2_kernel<R, 1, 0, 0, 0>(p, block, lds, st, launch);
     if (G == 8 && N == 4 && M == 16) return launch_v2_kernel<R, 0, 8, 4, 16>(p, block, lds, st, launch);          // configs[3]
-    if (G == 16 && N == 4 && M == 16) return launch_v2_kernel<R, 0, 16, 4, 16>(p, block, lds, st, launch);         // configs[3], 512 threads
+    if (G == 16 && N == 4 && M == 16) {   // configs[3]: terminal observations from their producers (TOBS) when asked for
+        if (!launch) {   // (both instantiations' attribute opt-in at ch_create)
+            const hipError_t e = launch_v2_kernel<R, 0, 16, 4, 16, false, false, true>(p, block, lds, st, false);
+            if (e != hipSuccess) return e;
+        }
+        if (p.terminal_obs) return launch_v2_kernel<R, 0, 16, 4, 16, false, false, true>(p, block, lds, st, launch);
+        return launch_v2_kernel<R, 0, 16, 4, 16>(p, block, lds, st, launch);
+    }
     if (G == 16 && N == 2 && M == 8) return launch_v2_kernel<R, 0, 16, 2, 8>(p, block, lds, st, launch);          // configs[2]
     if (G == 4 && N == 2 && M == 8) return launch_v2_kernel<R, 0, 4, 2, 8>(p, block, lds, st, launch);            // configs[1]
     return launch_v2_kernel<R, 0, 0, 0, 0>(p, block, lds, st, launch);
