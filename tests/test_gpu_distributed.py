@@ -74,3 +74,38 @@ def test_sharded_hip_rollout_equals_single_process():
             assert np.array_equal(v, single_st[k][off:off + per], equal_nan=True), (r, k)
         assert np.allclose(sums, single_met, rtol=1e-12, atol=0)
     assert single_met[1] > 0, "the rollout should end episodes (auto-reset inside the sharded steps)"
+
+
+def _rccl_worker(port, out):
+    sys.path.insert(0, os.path.join(ROOT, "rl-cattle-herding_amd"))
+    os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    from cattleherd import distributed as D
+    # the call cattleherd.distributed.init makes for backend "nccl" (RCCL on ROCm), on a one-rank group
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    m = torch.arange(8, dtype=torch.float64, device="cuda")
+    dist.all_reduce(m)
+    t = torch.tensor([2.5], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.barrier()
+    out["sum"] = m.cpu().numpy()
+    out["max"] = float(t.item())
+    out["backend"] = dist.get_backend()
+    D.shutdown()
+
+
+def test_rccl_process_group_on_the_device():
+    """The multi-GPU collectives' transport: a process group on backend "nccl" (RCCL over xGMI on ROCm) initialised on
+    the device as cattleherd.distributed.init does it, an all-reduce (sum, max) of device tensors and a barrier.  One
+    rank: the box has one GPU and RCCL takes one rank per device; the 8-rank run is the driver's SCALE measurement."""
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    out = ctx.Manager().dict()
+    p = ctx.Process(target=_rccl_worker, args=(port, out))
+    p.start()
+    p.join(180)
+    assert p.exitcode == 0
+    assert np.array_equal(out["sum"], np.arange(8, dtype=np.float64)) and out["max"] == 2.5
+    assert out["backend"] == "nccl"
