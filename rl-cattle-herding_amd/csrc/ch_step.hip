@@ -156,7 +156,7 @@ struct V2Smem {
     const uint16_t* pl;                              // [P] unordered cow pairs, copied from p.pairs
     uint8_t *dflags, *herded, *md1, *md2;            // [G*N], [G*M], [G*N], [G*N]
     uint8_t* tdf;                                    // [G*M*N] shepherd term in range | predator in range << 1
-    uint8_t* hasnb;                                  // PW: [G*M] cow has a neighbour within sensing range
+    uint8_t* hasnb;                                  // (unused: has_sensing_neighbour)
     unsigned long long* nbm;                         // PW: [G*M] neighbours k whose pair is inside the bump support
     uint16_t* queue;                                 // PW: [W][P] pairs of the slot's env inside the bump support
 
@@ -353,6 +353,25 @@ template <class R> __device__ __forceinline__ bool in_sensing(R n2) {
     return s;
 }
 
+// Cow j of env g has another cow of its env within sensing range (flockUtils.py:237-258: the alpha sums run over the
+// neighbours inside r = 999 m; with none, its alpha term is 0).  One partner decides it almost always -- the next cow --
+// and only a cow out of that one's range scans the rest, with the pair's difference taken in the pair list's order
+// (the same n2 as the cheap pass).  Evaluated by the row instead of marked by the cheap pass: those byte stores (many
+// lanes of a pass chunk on the same cow) took ~40 % of the pass (tools/wg_trace.py, profiles/r04/zc).
+template <class R>
+__device__ __forceinline__ bool has_sensing_neighbour(const V2Smem<R>& S, int M, int g, int j) {
+    auto ins = [&](int k) {
+        const int lo = g * M + min(j, k), hi = g * M + max(j, k);
+        const R zx = S.cx[hi] - S.cx[lo], zy = S.cy[hi] - S.cy[lo];
+        return in_sensing(zx * zx + zy * zy);
+    };
+    bool has = M > 1 && ins(j + 1 < M ? j + 1 : 0);
+    if (!has)
+        for (int k = 0; k < M; ++k)
+            if (k != j && ins(k)) { has = true; break; }
+    return has;
+}
+
 template <class R>
 __device__ __forceinline__ void alpha_cheap(V2Smem<R>& S, int* fl, int M, int P, int nf, const int* flist, bool skip) {
     const float rP = 1.0f / (float)P;
@@ -370,7 +389,6 @@ __device__ __forceinline__ void alpha_cheap(V2Smem<R>& S, int* fl, int M, int P,
             const int bi = g * M + li, bj = g * M + hi;
             const R zx = S.cx[bj] - S.cx[bi], zy = S.cy[bj] - S.cy[bi];
             const R n2 = zx * zx + zy * zy;
-            if (in_sensing(n2)) { S.hasnb[bi] = 1; S.hasnb[bj] = 1; }
             cand = n2 <= R(kAlphaSupport2);
             if (cand) {
                 atomicOr(&S.nbm[bi], 1ull << hi);
@@ -470,7 +488,7 @@ __device__ __forceinline__ void alpha_row(V2Smem<R>& S, int M, int P, int u, int
             cxx += v[r] ? (fwd[r] ? t[r][2] : -t[r][2]) : R(0); cyy += v[r] ? (fwd[r] ? t[r][3] : -t[r][3]) : R(0);
         }
     }
-    if (S.hasnb[u]) { ux = C2A * gx + C2A * cxx; uy = C2A * gy + C2A * cyy; }
+    if (has_sensing_neighbour(S, M, g, j)) { ux = C2A * gx + C2A * cxx; uy = C2A * gy + C2A * cyy; }
     S.aux[u] = ux; S.auy[u] = uy;
 }
 
@@ -498,7 +516,6 @@ __device__ __forceinline__ void alpha_cheap_pw(V2Smem<R>& S, int M, int P, int g
             const int bi = g * M + li, bj = g * M + hi;
             const R zx = S.cx[bj] - S.cx[bi], zy = S.cy[bj] - S.cy[bi];
             const R n2 = zx * zx + zy * zy;
-            if (in_sensing(n2)) { S.hasnb[bi] = 1; S.hasnb[bj] = 1; }
             cand = n2 <= R(kAlphaSupport2);
             if (cand) {
                 atomicOr(&S.nbm[bi], 1ull << hi);
@@ -535,7 +552,6 @@ __device__ __forceinline__ void alpha_cheap_pw_b(V2Smem<R>& S, int M, int P, int
             const uint32_t pr = prw[c];
             const int li = pr & 0xff, hi = pr >> 8;
             const int bi = g * M + li, bj = g * M + hi;
-            if (in_sensing(n2[c])) { S.hasnb[bi] = 1; S.hasnb[bj] = 1; }
             cand = n2[c] <= R(kAlphaSupport2);
             if (cand) {
                 atomicOr(&S.nbm[bi], 1ull << hi);
@@ -596,7 +612,7 @@ __device__ __forceinline__ void alpha_row_pw(V2Smem<R>& S, int M, int P, int g, 
             cxx += v[r] ? (fwd[r] ? tcx : -tcx) : R(0); cyy += v[r] ? (fwd[r] ? tcy : -tcy) : R(0);
         }
     }
-    if (S.hasnb[u]) { ux = C2A * gx + C2A * cxx; uy = C2A * gy + C2A * cyy; }
+    if (has_sensing_neighbour(S, M, g, j)) { ux = C2A * gx + C2A * cxx; uy = C2A * gy + C2A * cyy; }
     S.aux[u] = ux; S.auy[u] = uy;
 }
 
@@ -870,7 +886,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             reinterpret_cast<uint32_t*>(S.LT)[k] = reinterpret_cast<const uint32_t*>(kLevels)[k];
         for (int k = ct; k < P; k += CW) const_cast<uint16_t*>(S.pl)[k] = p.pairs[k];
         for (int k = ct; k < G * M; k += CW) {
-            S.hasnb[k] = 0; S.nbm[k] = 0;
+            S.nbm[k] = 0;
             if (sep) S.cnt[k] = 0;
         }
 #ifndef CH_NO_STREAM_FULL
