@@ -54,6 +54,9 @@ def main():
             mr = np.max(d[bg] / r_[bg]) if bg.any() else 0.0
             print(f"   {name:7s} max abs {d.max():.3e}  max rel (|ref| > 1e-3) {mr:.3e}  "
                   f"q99.9 rel {np.quantile(d[bg] / r_[bg], 0.999) if bg.any() else 0.0:.3e}")
+        for rt, at in ((1e-4, 1e-6), (1e-4, 1e-7), (1e-4, 1e-8), (5e-5, 1e-8)):
+            okc = np.isclose(go[..., 7:10], ro[..., 7:10], rtol=rt, atol=at)
+            print(f"   angvel isclose(rtol {rt:g}, atol {at:g}) fails {int((~okc).sum())} of {okc.size}")
         relo = np.where(big, np.abs(go - ro) / np.maximum(np.abs(ro), 1e-30), 0)
         for idx in np.argsort(relo.ravel())[-5:][::-1]:
             e, r, c = np.unravel_index(idx, relo.shape)
