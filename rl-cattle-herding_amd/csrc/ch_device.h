@@ -141,9 +141,12 @@ template <class R> __device__ __forceinline__ void quat_to_euler(const R q[4], R
 
 // ---- DSLPIDControl.computeControl for a VEL target (DSLPIDControl.py:82-259,
 //      BaseRLAviary.py:185-222).  pid[9] = last_rpy[3], integral_pos_e[3], integral_rpy_e[3].
+// The torque mix and the motor speeds are f64 in either precision: the f32 mode's body rates come from the
+// small differences of four ~14 k rpm (the torques of the attitude loop, a few hundred pwm on ~40 k), which
+// f32 resolves to only ~1e-3 relative (tools/f32_emu.py); for R = double nothing changes.
 template <class R>
 __device__ __forceinline__ void pid_vel(const R pos[3], const R q[4], const R vel[3], const R Rm[9], const R rpy[3],
-                                        const float act[4], R dt, R pid[9], R rpm[4], double* dbg = nullptr) {
+                                        const float act[4], R dt, R pid[9], double rpm[4], double* dbg = nullptr) {
     // _preprocessAction VEL branch: the float32 action row keeps the unit vector in float32;
     // SPEED_LIMIT * abs(a[3]) is float32 under NumPy >= 2 (DESIGN.md "Numerics").
     const double speed_limit = 0.3 * kMaxSpeedKmh * (1000.0 / 3600.0);
@@ -193,7 +196,8 @@ __device__ __forceinline__ void pid_vel(const R pos[3], const R q[4], const R ve
     const R rot_e[3] = {E(2, 1), E(0, 2), E(1, 0)};
     const R P_TOR[3] = {R(70000.), R(70000.), R(60000.)}, I_TOR[3] = {R(.0), R(.0), R(500.)},
             D_TOR[3] = {R(20000.), R(20000.), R(12000.)};
-    R rates_e[3], tt[3];
+    R rates_e[3];
+    double tt[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         rates_e[i] = R(0.0) - divc(rpy[i] - pid[i], dt);
@@ -204,13 +208,14 @@ __device__ __forceinline__ void pid_vel(const R pos[3], const R q[4], const R ve
     pid[7] = clip(pid[7], R(-1.), R(1.));
 #pragma unroll
     for (int i = 0; i < 3; ++i)
-        tt[i] = clip(-P_TOR[i] * rot_e[i] + D_TOR[i] * rates_e[i] + I_TOR[i] * pid[6 + i], R(-3200), R(3200));
-    const R MIX[4][3] = {{R(-.5), R(-.5), R(-1)}, {R(-.5), R(.5), R(1)}, {R(.5), R(.5), R(-1)}, {R(.5), R(-.5), R(1)}};
+        tt[i] = clip(-double(P_TOR[i]) * double(rot_e[i]) + double(D_TOR[i]) * double(rates_e[i]) +
+                     double(I_TOR[i]) * double(pid[6 + i]), -3200.0, 3200.0);
+    const double MIX[4][3] = {{-.5, -.5, -1}, {-.5, .5, 1}, {.5, .5, -1}, {.5, -.5, 1}};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        R pwm = thrust + (MIX[k][0] * tt[0] + MIX[k][1] * tt[1] + MIX[k][2] * tt[2]);
-        pwm = clip(pwm, R(kMinPwm), R(kMaxPwm));
-        rpm[k] = R(kPwmScale) * pwm + R(kPwmConst);
+        double pwm = double(thrust) + (MIX[k][0] * tt[0] + MIX[k][1] * tt[1] + MIX[k][2] * tt[2]);
+        pwm = clip(pwm, kMinPwm, kMaxPwm);
+        rpm[k] = kPwmScale * pwm + kPwmConst;
     }
     if (dbg) {
         dbg[0] = tv[0]; dbg[1] = tv[1]; dbg[2] = tv[2];
@@ -234,42 +239,48 @@ template <class R> __device__ __forceinline__ void pos_add(R p[3], double* pacc,
     if (pacc) { pacc[i] = pacc[i] + (double)d; p[i] = R(pacc[i]); }
     else p[i] = p[i] + d;
 }
+// The prop torques (differences of four ~0.07 N forces), the world-frame angular acceleration and the
+// angular-velocity update are f64 in either precision (W = double; see pid_vel): f32 there left 1e-4 relative
+// errors on the body rates (tools/f32_emu.py: each of the three is needed; the damping and gyroscopic terms and
+// the body-frame division are not).  For R = double this is the same arithmetic.
 template <class R, class X = NoExtraForces>
-__device__ __forceinline__ void drone_substep(R p[3], R q[4], R v[3], R w[3], const R rpm[4], R dt, R damping,
+__device__ __forceinline__ void drone_substep(R p[3], R q[4], R v[3], R w[3], const double rpm[4], R dt, R damping,
                                               bool torque_world, bool gyro, const X& extra = X(),
                                               double* pacc = nullptr) {
+    using W = double;
     const R PX[4] = {R(0.028), R(-0.028), R(-0.028), R(0.028)}, PY[4] = {R(-0.028), R(-0.028), R(0.028), R(0.028)};
     R M[9];
     quat_to_mat(q, M);
     R F[3] = {0, 0, 0}, Tw[3] = {0, 0, 0}, tb[3];
-    R t0 = rpm[0] * rpm[0] * R(kKM), t1 = rpm[1] * rpm[1] * R(kKM), t2 = rpm[2] * rpm[2] * R(kKM),
-      t3 = rpm[3] * rpm[3] * R(kKM);
-    R tz = (-t0 + t1 - t2 + t3);
+    const W t0 = rpm[0] * rpm[0] * W(kKM), t1 = rpm[1] * rpm[1] * W(kKM), t2 = rpm[2] * rpm[2] * W(kKM),
+            t3 = rpm[3] * rpm[3] * W(kKM);
+    const W tz = (-t0 + t1 - t2 + t3);
     // PYB with the world-frame motor torque (the default): the prop wrench in closed form in the body
     // frame (the oracle's drone_substep, same operation order): torque (sum py f, -sum px f, 0) plus
     // R^T e_z tz; force R e_z sum f.  Other cases accumulate per-link world forces (variants add theirs).
     const bool body = std::is_same<X, NoExtraForces>::value && torque_world;
     if (body) {
-        R f[4];
+        W f[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) f[i] = rpm[i] * rpm[i] * R(kKF);
-        const R T = ((f[0] + f[1]) + f[2]) + f[3];
-        F[0] = M[2] * T; F[1] = M[5] * T; F[2] = M[8] * T;
-        tb[0] = R(0.028) * (((-f[0] - f[1]) + f[2]) + f[3]) + M[6] * tz;
-        tb[1] = R(0.028) * (((-f[0] + f[1]) + f[2]) - f[3]) + M[7] * tz;
-        tb[2] = M[8] * tz;
+        for (int i = 0; i < 4; ++i) f[i] = rpm[i] * rpm[i] * W(kKF);
+        const W T = ((f[0] + f[1]) + f[2]) + f[3];
+        F[0] = R(W(M[2]) * T); F[1] = R(W(M[5]) * T); F[2] = R(W(M[8]) * T);
+        tb[0] = R(W(0.028) * (((-f[0] - f[1]) + f[2]) + f[3]) + W(M[6]) * tz);
+        tb[1] = R(W(0.028) * (((-f[0] + f[1]) + f[2]) - f[3]) + W(M[7]) * tz);
+        tb[2] = R(W(M[8]) * tz);
     } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            R f = rpm[i] * rpm[i] * R(kKF);
+            R f = R(rpm[i] * rpm[i] * W(kKF));
             R fw[3] = {M[2] * f, M[5] * f, M[8] * f};
             R rw[3] = {M[0] * PX[i] + M[1] * PY[i], M[3] * PX[i] + M[4] * PY[i], M[6] * PX[i] + M[7] * PY[i]};
             R t[3] = {rw[1] * fw[2] - rw[2] * fw[1], rw[2] * fw[0] - rw[0] * fw[2], rw[0] * fw[1] - rw[1] * fw[0]};
 #pragma unroll
             for (int k = 0; k < 3; ++k) { F[k] += fw[k]; Tw[k] += t[k]; }
         }
-        if (torque_world) Tw[2] += tz;
-        else { Tw[0] += M[2] * tz; Tw[1] += M[5] * tz; Tw[2] += M[8] * tz; }
+        const R tzr = R(tz);
+        if (torque_world) Tw[2] += tzr;
+        else { Tw[0] += M[2] * tzr; Tw[1] += M[5] * tzr; Tw[2] += M[8] * tzr; }
         extra(M, F, Tw);
     }
     F[2] += R(-kMass * kG);
@@ -298,11 +309,12 @@ __device__ __forceinline__ void drone_substep(R p[3], R q[4], R v[3], R w[3], co
         for (int i = 0; i < 3; ++i) tb[i] -= g[i];
     }
     R ab[3] = {divc(tb[0], J[0]), divc(tb[1], J[1]), divc(tb[2], J[2])};
+    const W ab0 = W(ab[0]), ab1 = W(ab[1]), ab2 = W(ab[2]), dtw = W(dt);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-        R aw = M[i * 3 + 0] * ab[0] + M[i * 3 + 1] * ab[1] + M[i * 3 + 2] * ab[2];
+        const W aw = W(M[i * 3 + 0]) * ab0 + W(M[i * 3 + 1]) * ab1 + W(M[i * 3 + 2]) * ab2;
         v[i] = v[i] + divc(F[i], R(kMass)) * dt;
-        w[i] = w[i] + aw * dt;
+        w[i] = R(W(w[i]) + aw * dtw);
     }
 #pragma unroll
     for (int i = 0; i < 3; ++i) pos_add(p, pacc, i, v[i] * dt);
@@ -516,8 +528,10 @@ __device__ __forceinline__ void rk4_substep(R p[3], R q[4], R v[3], R w[3], R rr
 // is wave-uniform, so every lane of the branch joins each shuffle.
 template <class R>
 __device__ __forceinline__ void variant_substeps(const StepParams<R>& p, int base, int nsh, int n, R pos[3], R q[4],
-                                                 R v[3], R w[3], const R rpm[4], R lr[4], R rr[3],
+                                                 R v[3], R w[3], const double rpm_w[4], R lr[4], R rr[3],
                                                  double* pacc = nullptr) {
+    // the variants' terms in the state precision; the PYB wrench takes the f64 speeds (drone_substep)
+    const R rpm[4] = {R(rpm_w[0]), R(rpm_w[1]), R(rpm_w[2]), R(rpm_w[3])};
     const int ph = p.physics;
     const bool gnd = ph == CH_PHYS_PYB_GND || ph == CH_PHYS_PYB_GND_DRAG_DW;
     const bool drag = ph == CH_PHYS_PYB_DRAG || ph == CH_PHYS_PYB_GND_DRAG_DW;
@@ -541,7 +555,7 @@ __device__ __forceinline__ void variant_substeps(const StepParams<R>& p, int bas
                     }
                 }
             };
-            drone_substep(pos, q, v, w, rpm, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0, extra, pacc);
+            drone_substep(pos, q, v, w, rpm_w, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0, extra, pacc);
         }
 #pragma unroll
         for (int c = 0; c < 4; ++c) lr[c] = rpm[c];   // last_clipped_action (BaseAviary.py:450)

@@ -212,7 +212,7 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
             R Rm[9];
             quat_to_mat(q, Rm);
             quat_to_euler(q, rpy);
-            R rpm[4];
+            double rpm[4];
             if (!(p.phase_mask & 1)) {
                 pid_vel(pos, q, v, Rm, rpy, a, R(p.dt_ctrl), pid, rpm, p.debug ? p.debug + di * 16 : nullptr);
                 if constexpr (PHYS) {

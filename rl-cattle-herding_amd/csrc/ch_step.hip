@@ -744,8 +744,12 @@ __device__ __forceinline__ void flock_combine(const StepParams<R>& p, V2Smem<R>&
 // carve and all index arithmetic then fold to immediates, which keeps the kernel within the SGPR file.
 // TOBS: the instantiation that writes terminal observations from their producers in the fast path (configs[3]'s
 // geometry, launched when the step asks for them); without it the same geometry takes the drained-copy path for them
+// The f32 geometry-specialised kernels keep 4 waves per SIMD (<= 128 VGPRs): their f64 torque path (ch_device.h
+// drone_substep) would otherwise take them to 135 and 3 waves, one resident workgroup fewer per CU at large E.
 template <class R, int MODE, int GT, int NT, int MT, bool PHYS = false, bool PW = false, bool TOBS = false>
-__global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK) void k_step2(StepParams<R> p) {
+__global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK)
+__attribute__((amdgpu_waves_per_eu((sizeof(R) == 4 && GT > 0 && !PW && !PHYS) ? 4 : 1)))
+void k_step2(StepParams<R> p) {
     extern __shared__ __align__(16) unsigned char smem[];
     constexpr bool marl = MODE == 1;
     // f32 mode: positions, centroids and the approach delta in f64 (StepParams::pos64); PT = their type
@@ -998,7 +1002,7 @@ __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK
             if (rpy_valid) { rpy[0] = rpy_in[0]; rpy[1] = rpy_in[1]; rpy[2] = rpy_in[2]; }
             else quat_to_euler(q, rpy);
             if (!(p.phase_mask & 1)) {
-                R rpm[4];
+                double rpm[4];
                 pid_vel(pos, q, v, Rm, rpy, a, R(p.dt_ctrl), pid, rpm, p.debug ? p.debug + di * 16 : nullptr);
                 if constexpr (PHYS) {
                     variant_substeps(p, dg * N, N, n, pos, q, v, w, rpm, ph_lr, ph_rr, MIX ? pd : nullptr);

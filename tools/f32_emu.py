@@ -96,8 +96,11 @@ def pid(pos, q, vel, rpy, tv, pidst, dt_ctrl, pol):
 
 
 def substep(q, v, w, rpm, dt_, pol):
+    """pol keys: sub (state precision), wrench (prop forces / torques), wb, damp, gyro, ab, aw, wup (each piece of
+    the body-rate update; default = wrench)"""
     t = pol["sub"]
     tw = pol["wrench"]
+    P = lambda k: pol.get(k, tw)  # noqa: E731
     M = quat_to_mat(q, t)
     r = [tw(x) for x in rpm]
     Mw = [tw(x) for x in M]
@@ -113,23 +116,31 @@ def substep(q, v, w, rpm, dt_, pol):
     vv = [t(x) for x in v]
     sp = np.sqrt(vv[0] * vv[0] + vv[1] * vv[1] + vv[2] * vv[2])
     F = [F[i] - t(KMASS) * vv[i] * (k + k * sp) for i in range(3)]
-    ww = [tw(x) for x in w]
-    wb = [Mw[0 + i] * ww[0] + Mw[3 + i] * ww[1] + Mw[6 + i] * ww[2] for i in range(3)]
-    J = [tw(x) for x in KJ]
-    kw = tw(0.04)
-    sw = np.sqrt(wb[0] * wb[0] + wb[1] * wb[1] + wb[2] * wb[2])
-    tb = [tb[i] - J[i] * wb[i] * (kw + kw * sw) for i in range(3)]
-    Jw = [J[i] * wb[i] for i in range(3)]
-    g = [wb[1] * Jw[2] - wb[2] * Jw[1], wb[2] * Jw[0] - wb[0] * Jw[2], wb[0] * Jw[1] - wb[1] * Jw[0]]
-    tb = [tb[i] - g[i] for i in range(3)]
-    ab = [tb[i] / J[i] for i in range(3)]
-    dtw = tw(dt_)
+    a_ = P("wb")
+    wb = [a_(M[0 + i]) * a_(w[0]) + a_(M[3 + i]) * a_(w[1]) + a_(M[6 + i]) * a_(w[2]) for i in range(3)]
+    a_ = P("damp")
+    J = [a_(x) for x in KJ]
+    kw = a_(0.04)
+    wbd = [a_(x) for x in wb]
+    sw = np.sqrt(wbd[0] * wbd[0] + wbd[1] * wbd[1] + wbd[2] * wbd[2])
+    dmp = [J[i] * wbd[i] * (kw + kw * sw) for i in range(3)]
+    a_ = P("gyro")
+    J = [a_(x) for x in KJ]
+    wbg = [a_(x) for x in wb]
+    Jw = [J[i] * wbg[i] for i in range(3)]
+    g = [wbg[1] * Jw[2] - wbg[2] * Jw[1], wbg[2] * Jw[0] - wbg[0] * Jw[2], wbg[0] * Jw[1] - wbg[1] * Jw[0]]
+    a_ = P("ab")
+    tb = [a_(tb[i]) - a_(dmp[i]) for i in range(3)]
+    tb = [tb[i] - a_(g[i]) for i in range(3)]
+    ab = [tb[i] / a_(KJ[i]) for i in range(3)]
     dt = t(dt_)
     nv = [vv[i] + F[i] / t(KMASS) * dt for i in range(3)]
     nw = []
     for i in range(3):
-        aw = Mw[i * 3 + 0] * ab[0] + Mw[i * 3 + 1] * ab[1] + Mw[i * 3 + 2] * ab[2]
-        nw.append(pol["wstate"](tw(ww[i]) + aw * dtw))
+        a_ = P("aw")
+        aw = a_(M[i * 3 + 0]) * a_(ab[0]) + a_(M[i * 3 + 1]) * a_(ab[1]) + a_(M[i * 3 + 2]) * a_(ab[2])
+        a_ = P("wup")
+        nw.append(pol["wstate"](a_(w[i]) + a_(aw) * a_(dt_)))
     ws = [t(x) for x in nw]
     fang = np.sqrt(ws[0] * ws[0] + ws[1] * ws[1] + ws[2] * ws[2])
     s = np.sin(t(0.5) * fang * dt) / np.where(fang > 0, fang, t(1))
@@ -190,21 +201,20 @@ def main():
     ref = np.concatenate([np.asarray(env.get_state()["drone_angv"])[:n] for env in envs])
     f32, f64 = np.float32, np.float64
     base = dict(state=f32, pos=f32, euler=f32, att=f32, rate=f32, mix=f32, sub=f32, wrench=f32, wstate=f32)
+    mw = {**base, "mix": f64, "wrench": f64}
     pols = {
         "all f64": {k: f64 for k in base},
         "all f32 (shipped)": base,
         "f64 mix": {**base, "mix": f64},
-        "f64 rate+mix": {**base, "rate": f64, "mix": f64},
         "f64 wrench": {**base, "wrench": f64},
-        "f64 mix+wrench": {**base, "mix": f64, "wrench": f64},
-        "f64 mix+wrench, w carried f64": {**base, "mix": f64, "wrench": f64, "wcarry": f64},
-        "f64 att+mix+wrench, w carried f64": {**base, "att": f64, "mix": f64, "wrench": f64, "wcarry": f64},
-        "f64 rate+mix+wrench": {**base, "rate": f64, "mix": f64, "wrench": f64},
-        "f64 att+rate+mix+wrench": {**base, "att": f64, "rate": f64, "mix": f64, "wrench": f64},
-        "f64 euler+att+rate+mix+wrench": {**base, "euler": f64, "att": f64, "rate": f64, "mix": f64, "wrench": f64},
-        "f64 pos+euler+att+rate+mix+wrench": {**base, "pos": f64, "euler": f64, "att": f64, "rate": f64, "mix": f64,
-                                              "wrench": f64},
+        "f64 mix+wrench": mw,
+        "f64 mix + prop torque only": {**mw, "wb": f32, "damp": f32, "gyro": f32, "ab": f32, "aw": f32, "wup": f32},
     }
+    for piece in ("wb", "damp", "gyro", "ab", "aw", "wup"):
+        pols[f"f64 mix+wrench but {piece} f32"] = {**mw, piece: f32}
+    pols["f64 mix+wrench but wb, damp, gyro f32"] = {**mw, "wb": f32, "damp": f32, "gyro": f32}
+    pols["shipped: f64 mix, prop torque, aw, w update"] = {**mw, "wb": f32, "damp": f32, "gyro": f32, "ab": f32}
+    pols["f64 mix+wrench but wb, damp, gyro, aw f32"] = {**mw, "wb": f32, "damp": f32, "gyro": f32, "aw": f32}
     for name, pol in pols.items():
         got = run(states, acts, pol, n)
         g32 = got.astype(np.float32).astype(np.float64)
