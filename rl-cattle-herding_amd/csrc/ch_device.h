@@ -139,6 +139,23 @@ template <class R> __device__ __forceinline__ void quat_to_euler(const R q[4], R
     }
 }
 
+// one angle of quat_to_euler (c = 0 roll, 1 pitch, 2 yaw), the same operations: the step's Euler pass spreads the
+// three transcendentals of a drone over three lanes
+template <class R> __device__ __forceinline__ R quat_to_euler_c(const R q[4], int c) {
+    R x = q[0], y = q[1], z = q[2], w = q[3];
+    R sqx = x * x, sqy = y * y, sqz = z * z, squ = w * w;
+    R sarg = R(-2.0) * (x * z - w * y);
+    const bool lo = sarg <= R(-0.99999), hi = !lo && sarg >= R(0.99999);
+    if (c == 1) return lo ? R(-0.5 * kPi) : (hi ? R(0.5 * kPi) : m_asin(sarg));
+    R ya, xa;
+    if (lo) { ya = x; xa = -y; }
+    else if (hi) { ya = -x; xa = y; }
+    else if (c == 0) { ya = R(2) * (y * z + w * x); xa = squ - sqx - sqy + sqz; }
+    else { ya = R(2) * (x * y + w * z); xa = squ + sqx - sqy - sqz; }
+    const R r = m_atan2(ya, xa);
+    return (lo || hi) ? (c == 0 ? R(0) : R(2) * r) : r;
+}
+
 // ---- DSLPIDControl.computeControl for a VEL target (DSLPIDControl.py:82-259,
 //      BaseRLAviary.py:185-222).  pid[9] = last_rpy[3], integral_pos_e[3], integral_rpy_e[3].
 // The torque mix and the motor speeds are f64 in either precision: the f32 mode's body rates come from the

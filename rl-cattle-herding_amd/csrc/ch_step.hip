@@ -1775,24 +1775,24 @@ void k_step2(StepParams<R> p) {
         // getEulerFromQuaternion of the new attitudes (BaseAviary.py:704-766): the own row's roll, pitch, yaw and
         // the next step's PID input (the Euler cache); late: after the reset list, skipping fast-reset envs
         auto euler_pass = [&]() {
+          // one item per (angle, drone): 3 G N items, so three waves share a workgroup's transcendentals
           for (;;) {
-            const int b = grab(fl + C_EULER, 64, skip_post), u = b + lane;
-            if (b >= Gv * N) break;
-            if (u < Gv * N) {
+            const int b = grab(fl + C_EULER, 64, skip_post), t = b + lane;
+            if (b >= 3 * Gv * N) break;
+            if (t < 3 * Gv * N) {
+                const int c = t >= Gv * N ? (t >= 2 * Gv * N ? 2 : 1) : 0, u = t - c * Gv * N;
                 const int g = qdiv(u, N, rN), k = u - g * N;
                 const bool rsf = fast && ei[I_RESET * G + g];   // (its cache and observation: the new episode's)
                 if (k < ei[I_N * G + g] && (!rsf || (tobs && wobs))) {
                     const int GN = G * N;
                     const R qq[4] = {S.dq[u], S.dq[GN + u], S.dq[2 * GN + u], S.dq[3 * GN + u]};
-                    R r3[3];
-                    quat_to_euler(qq, r3);
+                    const R r = quat_to_euler_c(qq, c);
                     const long long dd = (long long)e0 * N + u;
                     if (!rsf) {
-#pragma unroll
-                        for (int c = 0; c < 3; ++c) CH_STS(&p.rpy[c * DS + dd], r3[c]);
-                        if (wobs) obs_rpy(obs_wg + g * RW, k, r3);
+                        CH_STS(&p.rpy[c * DS + dd], r);
+                        if (wobs) CH_ST(obs_wg + g * RW + k * 86 + 1 + c, (float)r);
                     } else {
-                        obs_rpy(p.terminal_obs + (long long)(e0 + g) * RW, k, r3);   // the terminal observation's
+                        CH_ST(p.terminal_obs + (long long)(e0 + g) * RW + k * 86 + 1 + c, (float)r);   // the terminal observation's
                     }
                 }
             }
