@@ -39,7 +39,7 @@ def algorithmic_bytes(mode, n, m, rows, real_bytes, eval_metrics=True):
     """HBM bytes one env-step moves with this SoA layout (DESIGN.md "Roofline"), everything the kernel reads
     and writes counted once: the carried state, its Euler-angle cache and per-env flags, the evaluation
     accumulators and the outputs."""
-    drone = 22 * real_bytes * 2 * n                   # state read + write
+    drone = 26 * real_bytes * 2 * n                   # state read + write (22 components + the cached link frame)
     euler = 3 * real_bytes * 2 * n                    # Euler angles of the stored attitude, read + written
     evald = 8 * 2 * n if eval_metrics else 0          # update_evaluation_metrics' per-drone distance, read + written
     tags = 2 * 2 + 8 * 2                              # stale flags (2 x u8) and the obs-buffer tag, read + written
@@ -227,6 +227,53 @@ def marl_ppo_rollout(b, T=32):
     return out
 
 
+def near_herd_leg(b, n, m, reps=8, steps=100, burn=10, seed=11):
+    """configs[4] at training conditions: the headline's random actions drive the drones away from the herd (the
+    steady state is ~96 % truncated agent-steps with every cow-drone pair beyond the predator range, where the
+    shepherd term takes its far-drone closed form).  Here, `reps` times, every env's drones are put 0.6-1.4 m from a
+    random cow of their herd (set_state, untimed), `burn` untimed steps run, then `steps` timed steps: the flock's
+    near-drone shepherd and predator terms and the task's non-truncated paths run as in training.  Reports the rate
+    and, from each window's first state, the share of cow-drone pairs within 1 m (mu < 1) and 1.1 m (predator)."""
+    import numpy as np
+    import torch
+    rng = np.random.default_rng(seed)
+    E = b.n_envs
+    times, near1, pred, ends, trunc, steps_done = [], [], [], 0.0, 0.0, 0.0
+    for _ in range(reps):
+        s = b.get_state()
+        cows = s["cow_pos"][:, :m]
+        pick = rng.integers(0, m, (E, n))
+        ang = rng.uniform(-np.pi, np.pi, (E, n))
+        rad = rng.uniform(0.6, 1.4, (E, n))
+        c = np.take_along_axis(cows, pick[..., None].repeat(2, -1), 1)
+        dp = s["drone_pos"].copy()
+        dp[:, :, 0] = c[..., 0] + rad * np.cos(ang)
+        dp[:, :, 1] = c[..., 1] + rad * np.sin(ang)
+        b.set_state({"drone_pos": dp})
+        for _ in range(burn):
+            b.step(random_actions=True, autoreset=True, terminal_obs=False)
+        g = b.get_state()
+        d = np.linalg.norm(g["cow_pos"][:, None, :m, :] - g["drone_pos"][:, :n, None, :2], axis=-1)
+        live = np.arange(n)[None, :, None] < g["n"][:, None, None]
+        near1.append(float((d[np.broadcast_to(live, d.shape)] < 1.0).mean()))
+        pred.append(float((d[np.broadcast_to(live, d.shape)] <= 1.1).mean()))
+        b.metrics(reset=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            b.step(random_actions=True, autoreset=True, terminal_obs=False)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+        mv = b.metrics(reset=True)
+        ends += mv[1]; trunc += mv[5]; steps_done += mv[0]
+    dt = float(np.sum(times))
+    return {"env_steps_per_s": E * steps * reps / dt, "us_per_step": dt / (steps * reps) * 1e6,
+            "windows": reps, "steps_per_window": steps, "untimed_steps_after_placement": burn,
+            "cow_drone_pairs_within_1m": float(np.mean(near1)), "cow_drone_pairs_within_1.1m": float(np.mean(pred)),
+            "episode_ends": ends, "truncated_agent_step_fraction": trunc / max(steps_done * n, 1.0),
+            "note": "drones re-placed 0.6-1.4 m from a random cow of their herd before each window (untimed)"}
+
+
 def marl_vec_rollout(n, m, E, steps, warmup, burn_in):
     """configs[4] through the batched RLlib multi-agent surface (cattleherd.marl_vec_env): random actions,
     the wrapper semantics and in-launch resets; env-steps/s of the zero-copy tensor path (one launch plus the
@@ -355,11 +402,16 @@ def launch_check(args):
     E = args.envs or WORKLOADS[args.workload][1]
     lo = D.env_offset(rank, E)
     mv, t = D.reduce_rollout([float(rank + 1)] * 8, 0.5 + rank, device="cpu")
+    ranks = D.gather_rank_info(D.rank_device_info(use_gpu=False))
     if rank == 0:
         print(json.dumps({"launch_check": True, "n_gpus": seen, "backend": args.backend,
                           "env_ranges": [[D.env_offset(r, E), D.env_offset(r, E) + E] for r in range(seen)],
-                          "metric_sum": float(mv[0]), "max_time": t, "rank0_range": [lo, lo + E]}), flush=True)
+                          "metric_sum": float(mv[0]), "max_time": t, "rank0_range": [lo, lo + E],
+                          "ranks": ranks, "distinct_devices": D.distinct_devices(ranks)}), flush=True)
     D.shutdown()
+    if not D.distinct_devices(ranks):
+        print("bench: two ranks would drive the same device slot", file=sys.stderr)
+        sys.exit(4)
 
 
 def main():
@@ -419,6 +471,12 @@ def main():
                   physics=args.physics, compat=compat)
     print(f"bench: rank {rank}/{world} device {torch.cuda.current_device()} envs "
           f"[{D.env_offset(rank, E)}, {D.env_offset(rank, E) + E})", file=sys.stderr, flush=True)
+    # every rank's device (index, PCI address), gathered to rank 0 into the JSON line: a multi-GPU line proves
+    # from its own content that N ranks stepped N distinct devices (exit 4 otherwise)
+    ranks = D.gather_rank_info(D.rank_device_info(use_gpu=True))
+    if not D.distinct_devices(ranks):
+        print(f"bench: ranks share a device: {ranks}", file=sys.stderr)
+        sys.exit(4)
     stream = torch.cuda.current_stream()
 
     # end of a rollout (SURVEY §8(d) "host sync at the end"): device reduction of the per-env metric
@@ -531,6 +589,7 @@ def main():
                     "observations (terminal_obs=False, the sync-free auto-reset path), the terminal-observation path in "
                     "terminal_obs_leg",
             "launch": f"HIP graph of {chunk} steps per replay" if graph is not None else "one host launch per step",
+            "ranks": ranks,   # each rank's device index and PCI address (distinct, checked above)
             "rollout_end_us": rollout_end_us,
             "config": {"workload": desc, "envs_per_gpu": E, "num_drones": n, "num_cattle": m, "mode": mode,
                        "physics": args.physics,
@@ -558,7 +617,12 @@ def main():
             "valu": valu_issue(rec, args.precision, kern_us) if rec else None,
             "terminal_obs_leg": term_leg,
             "rollout_metrics": {"episodes": mv[1], "mean_return": (mv[2] / mv[1]) if mv[1] else None,
-                                "nan_rewards": mv[6], "terminated": mv[4], "truncated": mv[5]},
+                                "nan_rewards": mv[6], "terminated": mv[4], "truncated": mv[5], "env_steps": mv[0],
+                                # what the timed steps were: truncation flags per (agent-)step and episode ends in the
+                                # window (MARL: the wrapper's __all__ ignores truncation, marl_wrapper.py:113-117, so
+                                # truncated envs keep stepping -- the steady state under random actions)
+                                "truncated_fraction": mv[5] / max(mv[0] * (n if mode == "marl" else 1), 1.0),
+                                "episode_ends_in_window": mv[1]},
         }
         fr, fr_why = counter_record("flock_roofline")
         out["flock_roofline"] = fr.get("records") and {k: fr[k] for k in ("records", "flop_model", "peak_tflops", "note",
@@ -567,6 +631,8 @@ def main():
             out["policy_rollout"] = policy_rollout(b, n, args.steps, args.warmup)
         if args.policy and mode == "marl":
             out["marl_ppo_rollout"] = marl_ppo_rollout(b)
+        if mode == "marl" and not args.no_extras:
+            out["near_herd_leg"] = near_herd_leg(b, n, m)
         if args.marl_vec and mode == "marl":
             b.close()
             out["marl_vec_env"] = marl_vec_rollout(n, m, E, args.steps, args.warmup, args.burn_in)

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CH_ABI_VERSION 5
+#define CH_ABI_VERSION 6
 
 enum {
     CH_OK = 0,
@@ -77,7 +77,7 @@ typedef struct ch_config {
     int32_t pyb_freq;         /* 240 (CattleAviary.py:22) */
     int32_t compat;           /* 1 = reproduce reference quirks bit-for-bit (DESIGN.md "Quirks") */
     int32_t precision;        /* CH_PREC_F64 (reference arithmetic) or CH_PREC_F32 */
-    int32_t torque_world;     /* 1 = applyExternalTorque(LINK_FRAME) acts in world frame (default) */
+    int32_t torque_world;     /* link_lag = 0 only: 1 = applyExternalTorque(LINK_FRAME) acts in world frame */
     int32_t gyro;             /* 1 = gyroscopic term (btMultiBody default) */
     int32_t marl_wrapper;     /* MARL only: 1 = RLlibMultiAgentWrapper.step semantics (marl_wrapper.py:77-119:
                                  per-agent recomputation, finished agents drop out, episode ends when all
@@ -93,6 +93,10 @@ typedef struct ch_config {
     int32_t physics;          /* CH_PHYS_* (CattleAviary ctor `physics`, CattleAviary.py:21) */
     int32_t eval_metrics;     /* 1 (default) = keep update_evaluation_metrics' per-drone episode distance on
                                  the device every step (BaseAviary.py:1406-1435), read with ch_get_eval */
+    int32_t link_lag;         /* 1 (default) = _physics' applyExternalForce/Torque(LINK_FRAME) (BaseAviary.py:907-939)
+                                 rotate by the link transform Bullet cached at the previous substep (the
+                                 attitude one substep old, state components qlag): what the recorded real-PyBullet
+                                 trace shows; 0 = the current attitude (rounds 1-4 model) */
 } ch_config;
 
 typedef struct ch_handle ch_handle;
@@ -115,7 +119,11 @@ int ch_shape(const ch_handle* h, int64_t* n_envs, int32_t* obs_rows, int32_t* ob
 
 /* Replaces: BaseAviary.reset (sb3_envs/BaseAviary.py:280-331; rllib_envs/BaseAviary.py:280-318).
  * Resets the envs whose mask byte is non-zero (mask = NULL: all) and writes their initial
- * observation into obs (device, [E][R][86]); other envs' obs rows are left untouched. */
+ * observation into obs (device, [E][R][86]); other envs' obs rows are left untouched.
+ * A full reset (mask = NULL) first reads and clears the handle's sticky device error word: it synchronises `stream`
+ * (so it blocks the host and cannot be captured into a HIP graph), and a device error an earlier step recorded and no
+ * ch_sync / ch_metrics / ch_get_state has reported yet is returned as CH_ERR_DEVICE after the reset has been done
+ * (the state is then the fresh reset's). */
 int ch_reset(ch_handle* h, const uint8_t* mask_dev, float* obs_dev, void* stream);
 
 /* ch_reset with the reset's random draws supplied by the caller instead of the device's Philox stream:
@@ -162,7 +170,9 @@ int ch_step(ch_handle* h, const ch_step_io* io, void* stream);
  *     >= num_drones are always zero, so the caller zero-fills `obs` once and they stay zero.
  *   - The envs that auto-reset in the step (io->reset_happened) are compacted on the device, in ascending env
  *     order: their count, indices, terminal observations (io->terminal_obs, whole blocks) and episode statistics
- *     (io->episode_stats: return, length).  One synchronisation when at most 64 envs ended, two otherwise. */
+ *     (io->episode_stats: return, length).  Before the count is known the call copies a first part sized from the
+ *     recent counts (twice the larger of the last count and its running mean, plus 8): one synchronisation when at
+ *     most that many envs ended, two otherwise. */
 typedef struct ch_host_out {
     float* obs;                /* host [E][R][86] (required) */
     float* reward;             /* host [E][K] (required) */
@@ -179,8 +189,9 @@ int ch_outputs_to_host(ch_handle* h, const ch_step_io* io, ch_host_out* out, voi
 
 /* Full SoA state, for checkpoint/resume and parity state-injection.  Layout of the two host
  * buffers (counts from ch_state_size):
- *   doubles: drone[22][E][N] (px py pz qx qy qz qw vx vy vz wx wy wz pid_last_rpy[3]
- *            pid_int_pos[3] pid_int_rpy[3]), cattle[4][E][M] (x y vx vy), env[2][E] (prev_cent clock),
+ *   doubles: drone[26][E][N] (px py pz qx qy qz qw vx vy vz wx wy wz pid_last_rpy[3]
+ *            pid_int_pos[3] pid_int_rpy[3] qlag[4] = the cached link frame, link_lag), cattle[4][E][M] (x y vx vy),
+ *            env[2][E] (prev_cent clock),
  *            phys[7][E][N] (last_clipped_action[4] = drag input, DYN body rates rpy_rates[3])
  *   int32:   env[10][E] (n, step_counter, step_counter_A, has_prev, level, tally, spawn_index,
  *            active_mask, episode, step_index = ch_step calls so far = the Philox action counter) */
@@ -350,6 +361,9 @@ int ch_rollout_collect(ch_handle* h, const ch_rollout* rb, const ch_rollout_io* 
  * agent's trajectory ends where it terminates (bootstrap 0; the env resets only once every agent has terminated, so
  * a live agent that did not terminate is live at the next step of the same episode); rows with agent_mask 0 get
  * advantage and return 0; truncation does not end a trajectory (the wrapper keeps truncated agents acting).
+ * Divergence note: RLlib's per-agent episodes treat terminated OR truncated as done and bootstrap V(obs) at a
+ * truncation; this restatement follows the wrapper's "__all__" rule instead and bootstraps straight through the
+ * time limit (marl_wrapper.py:104-117).  Parity unpinned either way: RLlib is not installed here.
  * RLlib is not installed here: these semantics are restated from its PPO defaults ("parity unpinned" to its
  * source).  All arrays are caller-owned device memory. */
 typedef struct ch_marl_rollout {

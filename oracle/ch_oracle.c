@@ -191,8 +191,12 @@ typedef struct phys_ctx {
     double h_clip;
 } phys_ctx;
 
+/* R: the current attitude (lever arms, heights, the drag's body frame); Rl: the cached link frame that turns the
+ * link-frame forces into world forces (== R without link_lag).  _groundEffect reads p.getLinkStates with
+ * computeForwardKinematics=1 (943-980), which refreshes the cached link transforms: its forces, and the drag and
+ * downwash applied after it (PYB_GND_DRAG_DW), rotate by the current attitude; alone, drag and downwash use Rl. */
 static void physics_forces(const phys_ctx* x, const double* p, const double* q, const double* v, const double* R,
-                           const double* rpm, double* F, double* Tw) {
+                           const double* Rl, const double* rpm, double* F, double* Tw) {
     if (ph_gnd(x->physics)) {   /* _groundEffect (943-980) */
         double rpy[3]; och_euler_from_quat(q, rpy);
         double g[4];
@@ -219,7 +223,8 @@ static void physics_forces(const phys_ctx* x, const double* p, const double* q, 
         const double dv[3] = {(-DRAG_XY * sum) * v[0], (-DRAG_XY * sum) * v[1], (-DRAG_Z * sum) * v[2]};
         double b[3];   /* base_rot.T @ (drag_factors * vel): body frame */
         for (int k = 0; k < 3; ++k) b[k] = R[0 + k] * dv[0] + R[3 + k] * dv[1] + R[6 + k] * dv[2];
-        for (int k = 0; k < 3; ++k) F[k] += R[3 * k + 0] * b[0] + R[3 * k + 1] * b[1] + R[3 * k + 2] * b[2];
+        const double* Rv = ph_gnd(x->physics) ? R : Rl;
+        for (int k = 0; k < 3; ++k) F[k] += Rv[3 * k + 0] * b[0] + Rv[3 * k + 1] * b[1] + Rv[3 * k + 2] * b[2];
     }
     if (ph_dw(x->physics)) {    /* _downwash (1013-1041): one link-4 force per drone above within 10 m */
         const double* me = x->pos[x->self];
@@ -233,7 +238,8 @@ static void physics_forces(const phys_ctx* x, const double* p, const double* q, 
                 const double beta = DW_C2 * dz + DW_C3;
                 const double u = dxy / beta;
                 const double fz = -alpha * exp(-.5 * (u * u));
-                F[0] += R[2] * fz; F[1] += R[5] * fz; F[2] += R[8] * fz;
+                const double* Rv = ph_gnd(x->physics) ? R : Rl;
+                F[0] += Rv[2] * fz; F[1] += Rv[5] * fz; F[2] += Rv[8] * fz;
             }
         }
     }
@@ -334,14 +340,38 @@ void och_dyn_integrate(double* y, const double* rpm, double dt, int64_t steps, i
     }
 }
 
+/* ql != NULL (config link_lag): Bullet's cached link frame.  PyBullet's applyExternalForce / applyExternalTorque
+ * with LINK_FRAME on a multibody link rotate the link-frame vector by that link's cached world transform, which a
+ * link without a collision shape (the cf2x prop links and center_of_mass_link, cf2x.urdf:34-98) only gets from the
+ * forward-kinematics pass at the start of the previous stepSimulation: the base attitude one substep old (ql).  The
+ * force then acts at the link's current centre of mass, so the lever arms rotate with the current attitude R.  In
+ * the body frame, with u = R^T ql_z: torque = sum_i f_i (r_i x u) + u tz, force = ql_z sum f.  Pinned by the
+ * recorded real-PyBullet trace (tests/golden/trace_inverse.npz): the first evaluation episode's
+ * drone xy velocities and positions to ~1e-12 relative over its first steps, where the current-attitude model
+ * (ql = NULL) misses the first step's velocity by a factor 2.5. */
 static void drone_substep(const och_config* c, double* p, double* q, double* v, double* w, const double* rpm, double dt,
-                          const phys_ctx* x) {
+                          const phys_ctx* x, double* ql) {
     double R[9]; och_matrix_from_quat(q, R);
     double F[3] = {0, 0, 0}, Tw[3] = {0, 0, 0}, tb[3];
     double t0 = rpm[0] * rpm[0] * KM, t1 = rpm[1] * rpm[1] * KM, t2 = rpm[2] * rpm[2] * KM, t3 = rpm[3] * rpm[3] * KM;
     double tz = (-t0 + t1 - t2 + t3);
-    const int body = !x && c->torque_world;
-    if (body) {
+    const int body = !x && (ql || c->torque_world);
+    double Rl[9];   /* the cached link frame: directions of every LINK_FRAME force / torque on the links */
+    if (ql) och_matrix_from_quat(ql, Rl);
+    else memcpy(Rl, R, sizeof(Rl));
+    if (body && ql) {
+        double f[4];
+        for (int i = 0; i < 4; ++i) f[i] = rpm[i] * rpm[i] * KF;
+        const double T = ((f[0] + f[1]) + f[2]) + f[3];
+        F[0] = Rl[2] * T; F[1] = Rl[5] * T; F[2] = Rl[8] * T;
+        double u[3];
+        for (int i = 0; i < 3; ++i) u[i] = (R[0 + i] * Rl[2] + R[3 + i] * Rl[5]) + R[6 + i] * Rl[8];
+        const double sy = 0.028 * (((-f[0] - f[1]) + f[2]) + f[3]);   /* sum_i f_i r_iy */
+        const double sx = 0.028 * (((-f[0] + f[1]) + f[2]) - f[3]);   /* -sum_i f_i r_ix */
+        tb[0] = sy * u[2] + u[0] * tz;
+        tb[1] = sx * u[2] + u[1] * tz;
+        tb[2] = (-sx * u[1] - sy * u[0]) + u[2] * tz;
+    } else if (body) {
         /* PYB with the world-frame motor torque (the default): the four +z prop forces (LINK_FRAME at
          * (px, py, 0), cf2x.urdf:42-78) reduced to the body frame in closed form.  Their world torque
          * sum(R P_i x R e_z f_i) = R sum(P_i x e_z f_i) comes back to the body as (sum py f, -sum px f, 0);
@@ -356,16 +386,17 @@ static void drone_substep(const och_config* c, double* p, double* q, double* v, 
     } else {
         for (int i = 0; i < 4; ++i) {
             double f = rpm[i] * rpm[i] * KF;
-            double fw[3] = {R[2] * f, R[5] * f, R[8] * f};
+            double fw[3] = {Rl[2] * f, Rl[5] * f, Rl[8] * f};
             double rb[3] = {PROP[i][0], PROP[i][1], 0.0};
             double rw[3] = {R[0] * rb[0] + R[1] * rb[1], R[3] * rb[0] + R[4] * rb[1], R[6] * rb[0] + R[7] * rb[1]};
             double t[3]; cross3(rw, fw, t);
             for (int k = 0; k < 3; ++k) { F[k] += fw[k]; Tw[k] += t[k]; }
         }
-        if (c->torque_world) Tw[2] += tz;
-        else { Tw[0] += R[2] * tz; Tw[1] += R[5] * tz; Tw[2] += R[8] * tz; }
-        if (x) physics_forces(x, p, q, v, R, rpm, F, Tw);
+        if (c->torque_world && !ql) Tw[2] += tz;
+        else { Tw[0] += Rl[2] * tz; Tw[1] += Rl[5] * tz; Tw[2] += Rl[8] * tz; }
+        if (x) physics_forces(x, p, q, v, R, Rl, rpm, F, Tw);
     }
+    if (ql) memcpy(ql, q, 4 * sizeof(double));   /* the next substep's cached link frame: this substep's start */
     F[2] += -MASS * G;
     double k = c->damping;
     if (k != 0.0) {
@@ -898,6 +929,7 @@ void och_reset(const och_config* c, och_state* s) {
         }
         s->dp[i][0] = x; s->dp[i][1] = y; s->dp[i][2] = i < n ? TARGET_ALT : 0;
         s->dq[i][0] = s->dq[i][1] = s->dq[i][2] = 0; s->dq[i][3] = 1;
+        memcpy(s->qlag[i], s->dq[i], sizeof(s->qlag[i]));   /* loadURDF: the links' transforms at the spawn pose */
         for (int k = 0; k < 3; ++k) { s->dv[i][k] = 0; s->dw[i][k] = 0; }
         s->active[i] = (uint8_t)(i < n);
         for (int k = 0; k < 4; ++k) s->last_rpm[i][k] = 0;   /* _housekeeping (565, 581-582) */
@@ -923,7 +955,7 @@ void och_init(const och_config* c, och_state* s, int64_t env_id) {
     s->level = c->start_level;
     s->spawn_index = (int32_t)((1 + env_id) % c->spawn_scenarios);  /* ctor's _housekeeping consumed one */
     s->prev_cent = 0; s->has_prev = 0;
-    for (int i = 0; i < OCH_NMAX; ++i) s->dq[i][3] = 1;
+    for (int i = 0; i < OCH_NMAX; ++i) { s->dq[i][3] = 1; s->qlag[i][3] = 1; }
 }
 
 /* ---------------------------------------------------------------------------------------------
@@ -968,7 +1000,8 @@ int och_step(const och_config* c, och_state* s, const float* actions, float* obs
                 rk4_substep(s->dp[k], s->dq[k], s->dv[k], s->dw[k], s->rpy_rates[k], rpm[k], dt);
             } else {
                 phys_ctx x = {ph, s->last_rpm[k], (const double (*)[3])pos0, n, k, h_clip};
-                drone_substep(c, s->dp[k], s->dq[k], s->dv[k], s->dw[k], rpm[k], dt, ph == PH_PYB ? NULL : &x);
+                drone_substep(c, s->dp[k], s->dq[k], s->dv[k], s->dw[k], rpm[k], dt, ph == PH_PYB ? NULL : &x,
+                              c->link_lag ? s->qlag[k] : NULL);
             }
         }
         if (ph != PH_DYN && ph != PH_DYN_RK4)   /* no p.stepSimulation under DYN: the cattle bodies do not move (447-448) */

@@ -33,6 +33,9 @@ typedef struct och_config {
     int32_t marl_wrapper;     /* MARL: 1 = RLlibMultiAgentWrapper.step semantics, 0 = bare env.step */
     int32_t physics;          /* Physics enum order (utils/enums.py:13-21): 0 PYB, 1 DYN, 2 PYB_GND,
                                  3 PYB_DRAG, 4 PYB_DW, 5 PYB_GND_DRAG_DW */
+    int32_t link_lag;         /* 1 = applyExternalForce/Torque(LINK_FRAME) on the drone's links rotate by the
+                                 link transform Bullet cached at the previous substep (qlag); pinned by the
+                                 real-PyBullet trace.  0 = the current attitude (rounds 1-4) */
 } och_config;
 
 typedef struct och_state {
@@ -49,6 +52,8 @@ typedef struct och_state {
     double last_rpm[OCH_NMAX][4];       /* last_clipped_action (BaseAviary.py:450, 565): drag input */
     double rpy_rates[OCH_NMAX][3];      /* DYN body rates (BaseAviary.py:581-582, 1075) */
     double eval_dist[OCH_NMAX];         /* update_evaluation_metrics' episode distance (BaseAviary.py:1415-1426) */
+    double qlag[OCH_NMAX][4];           /* attitude at the start of the previous substep: the frame of the prop and
+                                           centre-of-mass links' cached world transforms (link_lag) */
 } och_state;
 
 #ifdef __cplusplus

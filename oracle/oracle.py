@@ -30,7 +30,8 @@ class Config(ctypes.Structure):
                 ("compat", ctypes.c_int32), ("damping", ctypes.c_double), ("torque_world", ctypes.c_int32),
                 ("gyro", ctypes.c_int32), ("seed", ctypes.c_uint64),
                 ("spawn_table", ctypes.POINTER(ctypes.c_double)), ("spawn_scenarios", ctypes.c_int32),
-                ("spawn_cows", ctypes.c_int32), ("marl_wrapper", ctypes.c_int32), ("physics", ctypes.c_int32)]
+                ("spawn_cows", ctypes.c_int32), ("marl_wrapper", ctypes.c_int32), ("physics", ctypes.c_int32),
+                ("link_lag", ctypes.c_int32)]
 
 
 D3 = ctypes.c_double * 3
@@ -49,7 +50,7 @@ class State(ctypes.Structure):
                 ("spawn_index", ctypes.c_int32), ("active", ctypes.c_uint8 * NMAX),
                 ("episode", ctypes.c_int64), ("env_id", ctypes.c_int64),
                 ("last_rpm", (ctypes.c_double * 4) * NMAX), ("rpy_rates", (ctypes.c_double * 3) * NMAX),
-                ("eval_dist", ctypes.c_double * NMAX)]
+                ("eval_dist", ctypes.c_double * NMAX), ("qlag", (ctypes.c_double * 4) * NMAX)]
 
 
 _lib = None
@@ -154,7 +155,7 @@ class Env:
 
     def __init__(self, mode, n_ctor, m, spawn_table, min_drones=None, max_drones=None, start_level=None,
                  compat=True, seed=0x5EED, env_id=0, damping=0.04, torque_world=True, gyro=True,
-                 ctrl_freq=60, pyb_freq=240, marl_wrapper=True, physics=0):
+                 ctrl_freq=60, pyb_freq=240, marl_wrapper=True, physics=0, link_lag=True):
         self.table = np.ascontiguousarray(spawn_table, np.float64)
         if start_level is None:
             start_level = 7 if mode == 0 else 0
@@ -164,7 +165,8 @@ class Env:
                           start_level=start_level, ctrl_freq=ctrl_freq, pyb_freq=pyb_freq,
                           compat=int(compat), damping=damping, torque_world=int(torque_world), gyro=int(gyro),
                           seed=seed, spawn_table=_dp(self.table), spawn_scenarios=self.table.shape[0],
-                          spawn_cows=self.table.shape[1], marl_wrapper=int(marl_wrapper), physics=int(physics))
+                          spawn_cows=self.table.shape[1], marl_wrapper=int(marl_wrapper), physics=int(physics),
+                          link_lag=int(link_lag))
         self.st = State()
         lib().och_init(ctypes.byref(self.cfg), ctypes.byref(self.st), env_id)
         self.rows = lib().och_obs_rows(ctypes.byref(self.cfg))
@@ -227,6 +229,11 @@ class Env:
         st.spawn_index = int(s["spawn_index"])
         lr = np.asarray(s["last_rpm"]) if "last_rpm" in s else np.zeros((NMAX, 4))
         rr = np.asarray(s["rpy_rates"]) if "rpy_rates" in s else np.zeros((NMAX, 3))
+        # the cached link frame: given, or (a state from elsewhere) the attitude itself, as after loadURDF
+        ql = np.asarray(s["drone_qlag"]) if "drone_qlag" in s else np.asarray(s["drone_quat"])
+        for i in range(NMAX):
+            for k in range(4):
+                st.qlag[i][k] = ql[i][k]
         for i in range(NMAX):
             for k in range(4):
                 st.last_rpm[i][k] = lr[i][k]
@@ -244,7 +251,7 @@ class Env:
                 "has_prev": st.has_prev, "clock": st.clock, "level": st.level, "tally": st.tally,
                 "spawn_index": st.spawn_index, "active": np.array(list(st.active), np.uint8),
                 "episode": st.episode, "last_rpm": a(st.last_rpm, 4), "rpy_rates": a(st.rpy_rates, 3),
-                "eval_dist": np.array(list(st.eval_dist), np.float64)}
+                "eval_dist": np.array(list(st.eval_dist), np.float64), "drone_qlag": a(st.qlag, 4)}
 
 
 def batch_rollout(mode, n, m, spawn_table, E, T, threads=0, seed=0x5EED, compat=True):
@@ -252,7 +259,8 @@ def batch_rollout(mode, n, m, spawn_table, E, T, threads=0, seed=0x5EED, compat=
     table = np.ascontiguousarray(spawn_table, np.float64)
     cfg = Config(mode=mode, n_ctor=n, m=m, min_drones=n, max_drones=n, start_level=7 if mode == 0 else 0,
                  ctrl_freq=60, pyb_freq=240, compat=int(compat), damping=0.04, torque_world=1, gyro=1, seed=seed,
-                 spawn_table=_dp(table), spawn_scenarios=table.shape[0], spawn_cows=table.shape[1], marl_wrapper=1)
+                 spawn_table=_dp(table), spawn_scenarios=table.shape[0], spawn_cows=table.shape[1], marl_wrapper=1,
+                 link_lag=1)
     states = (State * E)()
     L = lib()
     for e in range(E):

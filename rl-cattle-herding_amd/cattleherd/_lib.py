@@ -15,7 +15,7 @@ CH_PREC_F64, CH_PREC_F32 = 0, 1
 CH_STEP_AUTORESET, CH_STEP_RANDOM_ACTIONS = 0x1, 0x2
 METRIC_NAMES = ("steps", "episodes", "return_sum", "length_sum", "terminated", "truncated", "nan_rewards",
                 "effectiveness_sum")
-ABI_VERSION = 5
+ABI_VERSION = 6
 # Physics enum (utils/enums.py:13-21, include/cattleherd.h CH_PHYS_*)
 PHYSICS = {"pyb": 0, "dyn": 1, "pyb_gnd": 2, "pyb_drag": 3, "pyb_dw": 4, "pyb_gnd_drag_dw": 5, "dyn_rk4": 6}
 
@@ -37,7 +37,7 @@ class ChConfig(ctypes.Structure):
                 ("gyro", ctypes.c_int32), ("marl_wrapper", ctypes.c_int32), ("damping", ctypes.c_double), ("seed", ctypes.c_uint64),
                 ("env_id_offset", ctypes.c_int64), ("spawn_table", ctypes.POINTER(ctypes.c_double)),
                 ("spawn_scenarios", ctypes.c_int32), ("spawn_cows", ctypes.c_int32), ("physics", ctypes.c_int32),
-                ("eval_metrics", ctypes.c_int32)]
+                ("eval_metrics", ctypes.c_int32), ("link_lag", ctypes.c_int32)]
 
 
 class ChStepIO(ctypes.Structure):

@@ -65,6 +65,38 @@ def reduce_rollout(metrics, elapsed, device="cpu"):
     return m.cpu().numpy(), float(t.item())
 
 
+def rank_device_info(use_gpu=True):
+    """Which device this rank drives: rank, local rank, device index and, on a GPU, its PCI address and name.
+    Without a GPU (the gloo launch check) the device slot is the LOCAL_RANK the rank would bind."""
+    rank, world, local = world_info()
+    info = {"rank": rank, "local_rank": local, "device": local, "pci_bus_id": None, "name": None}
+    if use_gpu:
+        import torch
+        d = torch.cuda.current_device()
+        pr = torch.cuda.get_device_properties(d)
+        dom, bus, dev = (getattr(pr, k, None) for k in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+        info.update(device=int(d), name=str(getattr(pr, "name", "")),
+                    pci_bus_id=(f"{int(dom or 0):04x}:{int(bus):02x}:{int(dev or 0):02x}" if bus is not None else None))
+    return info
+
+
+def gather_rank_info(info):
+    """Every rank's rank_device_info() on every rank, in rank order (one all_gather_object; [info] alone)."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        out = [None] * dist.get_world_size()
+        dist.all_gather_object(out, info)
+        return out
+    return [info]
+
+
+def distinct_devices(infos):
+    """True when no two ranks drive the same device: PCI addresses when known (a launcher that narrows each rank's
+    visible devices makes every rank's index 0), else (host, device index)."""
+    keys = [i["pci_bus_id"] if i.get("pci_bus_id") else ("slot", i["device"]) for i in infos]
+    return len(set(keys)) == len(keys)
+
+
 def shutdown():
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized():

@@ -14,7 +14,7 @@ import numpy as np
 
 from . import _lib as L
 
-DRONE_COMPS = 22
+DRONE_COMPS = 26   # ... pid_int_rpy[3], qlag[4] (the cached link frame, ch_config.link_lag)
 CATTLE_COMPS = 4
 PHYS_COMPS = 7   # last_clipped_action[4], DYN rpy_rates[3]
 ENV_INTS = ("n", "step_counter", "step_counter_A", "has_prev", "level", "tally", "spawn_index", "active_mask",
@@ -25,7 +25,7 @@ class HerdBatch:
     def __init__(self, n_envs, num_drones, num_cattle, mode="ctde", device=None, compat=True, precision="f64",
                  min_drones=None, max_drones=None, curriculum_level=None, seed=0x5EED, env_id_offset=0,
                  damping=0.04, torque_world=True, gyro=True, ctrl_freq=60, pyb_freq=240, spawn_table=None,
-                 marl_wrapper=True, physics="pyb", eval_metrics=True):
+                 marl_wrapper=True, physics="pyb", eval_metrics=True, link_lag=True):
         import torch
         if not torch.cuda.is_available():
             raise RuntimeError("HerdBatch needs a ROCm GPU (torch.cuda.is_available() is False); there is no CPU "
@@ -52,6 +52,7 @@ class HerdBatch:
             physics = physics.value
         cfg.physics = L.PHYSICS[physics.lower()] if isinstance(physics, str) else int(physics)
         cfg.eval_metrics = int(bool(eval_metrics))
+        cfg.link_lag = int(bool(link_lag))
         self._table = None
         if spawn_table is not None:
             self._table = np.ascontiguousarray(spawn_table, np.float64)
@@ -249,7 +250,7 @@ class HerdBatch:
              "drone_pos": dr[0:3].transpose(1, 2, 0), "drone_quat": dr[3:7].transpose(1, 2, 0),
              "drone_vel": dr[7:10].transpose(1, 2, 0), "drone_angv": dr[10:13].transpose(1, 2, 0),
              "pid_last_rpy": dr[13:16].transpose(1, 2, 0), "pid_int_pos": dr[16:19].transpose(1, 2, 0),
-             "pid_int_rpy": dr[19:22].transpose(1, 2, 0),
+             "pid_int_rpy": dr[19:22].transpose(1, 2, 0), "drone_qlag": dr[22:26].transpose(1, 2, 0),
              "cow_pos": ca[0:2].transpose(1, 2, 0), "cow_vel": ca[2:4].transpose(1, 2, 0),
              "prev_cent": er[0].copy(), "clock": er[1].copy()}
         for k, name in enumerate(ENV_INTS):
@@ -270,8 +271,13 @@ class HerdBatch:
         for key, lo, hi in (("last_rpm", 0, 4), ("rpy_rates", 4, 7)):
             if key in s:
                 ph[lo:hi] = np.asarray(s[key], np.float64)[:, :N, :].transpose(2, 0, 1)
+        if "drone_quat" in s and "drone_qlag" not in s:
+            # a state from elsewhere (fixtures, the oracle's older dumps): the links' cached frame is the attitude
+            # itself, as right after loadURDF
+            s = dict(s, drone_qlag=s["drone_quat"])
         for key, lo, hi in (("drone_pos", 0, 3), ("drone_quat", 3, 7), ("drone_vel", 7, 10), ("drone_angv", 10, 13),
-                            ("pid_last_rpy", 13, 16), ("pid_int_pos", 16, 19), ("pid_int_rpy", 19, 22)):
+                            ("pid_last_rpy", 13, 16), ("pid_int_pos", 16, 19), ("pid_int_rpy", 19, 22),
+                            ("drone_qlag", 22, 26)):
             if key in s:
                 dr[lo:hi] = np.asarray(s[key], np.float64)[:, :N, :].transpose(2, 0, 1)
         for key, lo, hi in (("cow_pos", 0, 2), ("cow_vel", 2, 4)):

@@ -2,8 +2,10 @@
 
 Drop-in for ``make_vec_env(CattleAviary, n_envs=..., vec_env_cls=SubprocVecEnv)``
 (simulator/CTDECattleHerder.py:91-97): ``CattleHerdVecEnv(n_envs, num_drones=..., num_cattle=...)``
-returns numpy observations ``(E, 12, 86)`` (valid until the step after next: two pinned host buffers are used in
-turn), rewards ``(E,)``, dones ``(E,)`` and per-env infos with
+returns numpy observations ``(E, 12, 86)`` (by default a view of one of ``obs_ring`` = 2 pinned host buffers used in
+turn, valid until ``obs_ring`` more steps have run -- SB3's collect_rollouts needs one; ``copy_obs=True`` returns a
+fresh array, SubprocVecEnv's semantics, at the cost of a 17 MB host copy per step at 4096 envs), rewards ``(E,)``,
+dones ``(E,)`` and a fresh list of per-env infos (dicts the step never changes afterwards) with
 SB3's ``terminal_observation`` / ``TimeLimit.truncated`` keys and, as the Monitor that ``make_vec_env``
 wraps around every env (CTDECattleHerder.py:91-99) adds, ``episode = {"r", "l", "t"}`` for each episode that
 ends, auto-resetting finished envs inside the step launch.  ``step_tensors`` is the zero-copy path for
@@ -27,7 +29,7 @@ except Exception:  # noqa: BLE001
 
 class CattleHerdVecEnv(_VecEnvBase):
     def __init__(self, n_envs, num_drones=2, num_cattle=1, obs="cokin", act="vel", drone_model="cf2x",
-                 physics="pyb", device=None, **batch_kw):
+                 physics="pyb", device=None, copy_obs=False, obs_ring=2, **batch_kw):
         check_supported(drone_model, physics, obs, act)
         self.batch = HerdBatch(n_envs, num_drones, num_cattle, mode="ctde", device=device, physics=physics,
                                **batch_kw)
@@ -43,10 +45,14 @@ class CattleHerdVecEnv(_VecEnvBase):
         self._t_start = time.time()
         # host delivery: pinned buffers filled by one ch_outputs_to_host per step (two sets used in turn, so the
         # observation array returned by a step stays valid through the next step, as SB3's collect_rollouts needs)
-        self._host = self.batch.host_outputs(ring=2, ended=True)
-        # one info dict per env, reused: only the envs that end in a step get (and next time lose) the extra keys
+        if obs_ring < 2:
+            raise ValueError("obs_ring must be >= 2 (collect_rollouts keeps the previous step's observations)")
+        self._host = self.batch.host_outputs(ring=int(obs_ring), ended=True)
+        self._copy_obs = bool(copy_obs)
+        # _computeInfo's {"answer": 42} per env (CattleAviary.py), never mutated here: each step returns a new list of
+        # them with a new dict for every env that ended (terminal_observation, TimeLimit.truncated, episode), so infos a
+        # caller keeps do not change under later steps (SubprocVecEnv hands out fresh dicts too)
         self._infos = [{"answer": 42} for _ in range(n_envs)]
-        self._dirty = []
         if _VecEnvBase is not object:  # SB3 bookkeeping
             _VecEnvBase.__init__(self, n_envs, self.observation_space, self.action_space)
 
@@ -56,10 +62,6 @@ class CattleHerdVecEnv(_VecEnvBase):
 
     # ---- VecEnv API --------------------------------------------------------------------------
     def reset(self):
-        for e in self._dirty:
-            for k in ("terminal_observation", "TimeLimit.truncated", "episode"):
-                self._infos[e].pop(k, None)
-        self._dirty = []
         return self.batch.reset().cpu().numpy()
 
     def step_async(self, actions):
@@ -87,25 +89,18 @@ class CattleHerdVecEnv(_VecEnvBase):
         te_np = h["terminated"][:, 0].astype(bool)
         tr_np = h["truncated"][:, 0].astype(bool)
         dones = te_np | tr_np
-        infos = self._infos
-        for e in self._dirty:   # the keys the last step added
-            d = infos[e]
-            d.pop("terminal_observation", None)
-            d.pop("TimeLimit.truncated", None)
-            d.pop("episode", None)
+        infos = list(self._infos)
         idx = h["ended_env"]
-        self._dirty = idx.tolist()
         if len(idx):
             # Monitor.step: the episode's summed float64 reward and length, kept on the device by the step kernel
             # (ch_step_io.episode_stats), and the wall time since the Monitor started
             t = round(time.time() - self._t_start, 6)
             term_obs, stats = h["ended_obs"], h["ended_stats"]
-            for k, e in enumerate(self._dirty):
-                d = infos[e]
-                d["terminal_observation"] = term_obs[k].copy()
-                d["TimeLimit.truncated"] = bool(tr_np[e] and not te_np[e])
-                d["episode"] = {"r": round(float(stats[k, 0]), 6), "l": int(stats[k, 1]), "t": t}
-        return h["obs"], rew_np, dones, list(infos)
+            for k, e in enumerate(idx.tolist()):
+                infos[e] = {"answer": 42, "terminal_observation": term_obs[k].copy(),
+                            "TimeLimit.truncated": bool(tr_np[e] and not te_np[e]),
+                            "episode": {"r": round(float(stats[k, 0]), 6), "l": int(stats[k, 1]), "t": t}}
+        return (h["obs"].copy() if self._copy_obs else h["obs"]), rew_np, dones, infos
 
     def step(self, actions):
         self.step_async(actions)

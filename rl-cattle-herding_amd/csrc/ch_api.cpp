@@ -83,6 +83,10 @@ struct ch_handle {
     double* st_stats = nullptr;
     float* st_obs = nullptr;
     long long* st_count_host = nullptr;
+    // how many ended envs ch_outputs_to_host copies before it knows the count: twice the larger of the last count and
+    // its running mean, plus 8 (a step where more end costs one more copy and stream sync)
+    double ended_mean = 8.0;
+    int64_t ended_last = 8;
     // the device error word was reported to the caller (device_status) since it was last cleared
     bool err_seen = false;
     std::string err;
@@ -179,6 +183,7 @@ static StepParams<R> params(ch_handle* h) {
     p.E = (int)h->E; p.NC = h->NC; p.M = h->M; p.mode = c.mode; p.rows = h->rows;
     p.min_drones = c.min_drones; p.max_drones = c.max_drones; p.ctrl_freq = c.ctrl_freq;
     p.substeps = c.pyb_freq / c.ctrl_freq; p.compat = c.compat; p.torque_world = c.torque_world; p.gyro = c.gyro;
+    p.link_lag = c.link_lag;
     p.marl_wrapper = c.marl_wrapper;
     p.episode_len = h->episode_len; p.damping = c.damping;
     p.dt_ctrl = 1.0 / c.ctrl_freq; p.dt = 1.0 / c.pyb_freq;
@@ -246,6 +251,7 @@ int ch_default_config(ch_config* c, int32_t mode, int32_t num_drones, int32_t nu
     c->spawn_table = nullptr;
     c->physics = CH_PHYS_PYB;
     c->eval_metrics = 1;
+    c->link_lag = 1;
     return CH_OK;
 }
 
@@ -451,7 +457,10 @@ int ch_create(const ch_config* c, int64_t n_envs, int32_t device, ch_handle** ou
     // initial state = what the constructors leave behind before the first reset():
     // identity quaternions, zero PID state, spawn index advanced once by __init__'s _housekeeping.
     std::vector<double> dz((size_t)kDroneComps * E * h->NC, 0.0);
-    for (int64_t i = 0; i < E * h->NC; ++i) dz[(size_t)6 * E * h->NC + i] = 1.0;
+    for (int64_t i = 0; i < E * h->NC; ++i) {
+        dz[(size_t)6 * E * h->NC + i] = 1.0;
+        dz[(size_t)25 * E * h->NC + i] = 1.0;   // cached link frame: identity too
+    }
     std::vector<int> ei((size_t)kEnvInt * E, 0);
     for (int64_t e = 0; e < E; ++e) {
         ei[4 * E + e] = level;
@@ -1260,8 +1269,9 @@ int ch_outputs_to_host(ch_handle* h, const ch_step_io* io, ch_host_out* out, voi
     if (out->reset_happened) HIP_TRY(h, hipMemcpyAsync(out->reset_happened, io->reset_happened, E, hipMemcpyDeviceToHost, st));
     if (out->agent_active)
         HIP_TRY(h, hipMemcpyAsync(out->agent_active, io->agent_active, (size_t)h->NC * E, hipMemcpyDeviceToHost, st));
-    // the ended envs' lists: a speculative first part (the usual case: a few envs end per step), the rest after the count
-    const int64_t cap = std::min<int64_t>(E, 64);
+    // the ended envs' lists: a speculative first part sized from the recent counts (the usual case: a few envs end per
+    // step -- at C4 under random actions ~20, in a training rollout ~3), the rest after the count
+    const int64_t cap = std::min<int64_t>(E, 2 * std::max<int64_t>(h->ended_last, (int64_t)h->ended_mean) + 8);
     auto copy_ended = [&](int64_t lo, int64_t hi) -> int {
         if (hi <= lo) return CH_OK;
         if (out->ended_env)
@@ -1278,6 +1288,10 @@ int ch_outputs_to_host(ch_handle* h, const ch_step_io* io, ch_host_out* out, voi
     if (io->reset_happened && (rc = copy_ended(0, cap))) return rc;
     HIP_TRY(h, hipStreamSynchronize(st));
     out->ended_count = io->reset_happened ? *h->st_count_host : 0;
+    if (io->reset_happened) {
+        h->ended_last = out->ended_count;
+        h->ended_mean = 0.9 * h->ended_mean + 0.1 * (double)out->ended_count;
+    }
     if (out->ended_count > cap) {
         if ((rc = copy_ended(cap, out->ended_count))) return rc;
         HIP_TRY(h, hipStreamSynchronize(st));

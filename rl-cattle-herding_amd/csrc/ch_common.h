@@ -99,6 +99,8 @@ __device__ __forceinline__ void reset_drone_store(const StepParams<R>& p, long l
     D[0 * DS + di] = R(x); D[1 * DS + di] = R(y); D[2 * DS + di] = R(z);
     if (p.pos64) { p.pos64[0 * DS + di] = x; p.pos64[1 * DS + di] = y; p.pos64[2 * DS + di] = z; }
     D[3 * DS + di] = 0; D[4 * DS + di] = 0; D[5 * DS + di] = 0; D[6 * DS + di] = 1;
+    // loadURDF: the links' cached transforms at the spawn attitude
+    D[22 * DS + di] = 0; D[23 * DS + di] = 0; D[24 * DS + di] = 0; D[25 * DS + di] = 1;
 #pragma unroll
     for (int c = 7; c < 13; ++c) D[c * DS + di] = 0;
     if (!p.compat) {

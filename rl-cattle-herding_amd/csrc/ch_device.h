@@ -124,6 +124,16 @@ template <class R> __device__ __forceinline__ void quat_to_mat(const R q[4], R M
     M[6] = xz - wy; M[7] = yz + wx; M[8] = R(1.0) - (xx + yy);
 }
 
+// the third column of quat_to_mat(q) (the body z axis in the world frame), the same operations
+template <class R> __device__ __forceinline__ void quat_to_zcol(const R q[4], R Z[3]) {
+    R x = q[0], y = q[1], z = q[2], w = q[3];
+    R d = x * x + y * y + z * z + w * w, s = R(2.0) / d;
+    R xs = x * s, ys = y * s, zs = z * s;
+    R wx = w * xs, wy = w * ys, xx = x * xs, xz = x * zs;
+    R yy = y * ys, yz = y * zs;
+    Z[0] = xz + wy; Z[1] = yz - wx; Z[2] = R(1.0) - (xx + yy);
+}
+
 template <class R> __device__ __forceinline__ void quat_to_euler(const R q[4], R rpy[3]) {
     R x = q[0], y = q[1], z = q[2], w = q[3];
     R sqx = x * x, sqy = y * y, sqz = z * z, squ = w * w;
@@ -247,9 +257,9 @@ __device__ __forceinline__ void pid_vel(const R pos[3], const R q[4], const R ve
 
 // ---- _physics (BaseAviary.py:907-939) + one p.stepSimulation substep (448): btMultiBody model ----
 struct NoExtraForces {
-    template <class R> __device__ __forceinline__ void operator()(const R*, R*, R*) const {}
+    template <class R> __device__ __forceinline__ void operator()(const R*, const R*, R*, R*) const {}
 };
-// `extra(M, F, Tw)` adds the physics-variant link forces (BaseAviary.py:424-445) after the motor
+// `extra(M, Ml, F, Tw)` adds the physics-variant link forces (BaseAviary.py:424-445) after the motor
 // model and before gravity, in the reference's applyExternalForce order.
 // pacc (f32 mode): the position accumulates in f64 -- p + (v dt), f32 increment and f64 sum -- and p is its rounded copy
 template <class R> __device__ __forceinline__ void pos_add(R p[3], double* pacc, int i, R d) {
@@ -260,23 +270,60 @@ template <class R> __device__ __forceinline__ void pos_add(R p[3], double* pacc,
 // angular-velocity update are f64 in either precision (W = double; see pid_vel): f32 there left 1e-4 relative
 // errors on the body rates (tools/f32_emu.py: each of the three is needed; the damping and gyroscopic terms and
 // the body-frame division are not).  For R = double this is the same arithmetic.
+//
+// ql != nullptr (ch_config.link_lag, the default): Bullet's cached link frame.  PyBullet's applyExternalForce /
+// applyExternalTorque with LINK_FRAME on a multibody link rotate the link-frame vector by the link's cached world
+// transform, which a link without a collision shape (the cf2x prop links and center_of_mass_link) gets only from the
+// forward kinematics at the start of the previous stepSimulation: the base attitude one substep old (ql, carried in
+// the state as drone components 22-25).  The force acts at the link's current centre of mass, so the lever arms turn
+// with the current attitude.  Body frame, u = M^T ql_z: torque sum_i f_i (r_i x u) + u tz, force ql_z sum f.  Pinned
+// by the real-PyBullet trace (oracle/ch_oracle.c drone_substep, the same operation order).
+// extra(M, Ml, F, Tw): M the current attitude, Ml the cached link frame (== M without link_lag).
 template <class R, class X = NoExtraForces>
 __device__ __forceinline__ void drone_substep(R p[3], R q[4], R v[3], R w[3], const double rpm[4], R dt, R damping,
                                               bool torque_world, bool gyro, const X& extra = X(),
-                                              double* pacc = nullptr) {
+                                              double* pacc = nullptr, R* ql = nullptr, R* zl = nullptr,
+                                              bool lag = false) {
+    // (ql / zl are only dereferenced when lag: a conditional pointer to the caller's arrays would keep them out of
+    // registers).  zl = the z axis of ql's frame (quat_to_zcol(ql) before the first substep; afterwards the previous
+    // substep's M column, the same numbers), which is all the PYB wrench reads of it.
     using W = double;
     const R PX[4] = {R(0.028), R(-0.028), R(-0.028), R(0.028)}, PY[4] = {R(-0.028), R(-0.028), R(0.028), R(0.028)};
-    R M[9];
+    R M[9], Ml[9];
     quat_to_mat(q, M);
+    const bool body = std::is_same<X, NoExtraForces>::value && (torque_world || lag);
+    if (lag && body) {
+        Ml[2] = zl[0]; Ml[5] = zl[1]; Ml[8] = zl[2];
+    } else if (lag) {
+        quat_to_mat(ql, Ml);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) Ml[i] = M[i];
+    }
     R F[3] = {0, 0, 0}, Tw[3] = {0, 0, 0}, tb[3];
     const W t0 = rpm[0] * rpm[0] * W(kKM), t1 = rpm[1] * rpm[1] * W(kKM), t2 = rpm[2] * rpm[2] * W(kKM),
             t3 = rpm[3] * rpm[3] * W(kKM);
     const W tz = (-t0 + t1 - t2 + t3);
-    // PYB with the world-frame motor torque (the default): the prop wrench in closed form in the body
-    // frame (the oracle's drone_substep, same operation order): torque (sum py f, -sum px f, 0) plus
-    // R^T e_z tz; force R e_z sum f.  Other cases accumulate per-link world forces (variants add theirs).
-    const bool body = std::is_same<X, NoExtraForces>::value && torque_world;
-    if (body) {
+    // PYB (no variant forces): the prop wrench in closed form in the body frame (the oracle's drone_substep, same
+    // operation order).  Cached link frame: force ql_z sum f, torque above.  World-frame motor torque (rounds 1-4
+    // model): torque (sum py f, -sum px f, 0) plus R^T e_z tz; force R e_z sum f.  Other cases accumulate per-link
+    // world forces (variants add theirs).
+    if (body && lag) {
+        W f[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) f[i] = rpm[i] * rpm[i] * W(kKF);
+        const W T = ((f[0] + f[1]) + f[2]) + f[3];
+        F[0] = R(W(Ml[2]) * T); F[1] = R(W(Ml[5]) * T); F[2] = R(W(Ml[8]) * T);
+        W u[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            u[i] = (W(M[0 + i]) * W(Ml[2]) + W(M[3 + i]) * W(Ml[5])) + W(M[6 + i]) * W(Ml[8]);
+        const W sy = W(0.028) * (((-f[0] - f[1]) + f[2]) + f[3]);   // sum_i f_i r_iy
+        const W sx = W(0.028) * (((-f[0] + f[1]) + f[2]) - f[3]);   // -sum_i f_i r_ix
+        tb[0] = R(sy * u[2] + u[0] * tz);
+        tb[1] = R(sx * u[2] + u[1] * tz);
+        tb[2] = R((-sx * u[1] - sy * u[0]) + u[2] * tz);
+    } else if (body) {
         W f[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) f[i] = rpm[i] * rpm[i] * W(kKF);
@@ -289,16 +336,16 @@ __device__ __forceinline__ void drone_substep(R p[3], R q[4], R v[3], R w[3], co
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             R f = R(rpm[i] * rpm[i] * W(kKF));
-            R fw[3] = {M[2] * f, M[5] * f, M[8] * f};
+            R fw[3] = {Ml[2] * f, Ml[5] * f, Ml[8] * f};
             R rw[3] = {M[0] * PX[i] + M[1] * PY[i], M[3] * PX[i] + M[4] * PY[i], M[6] * PX[i] + M[7] * PY[i]};
             R t[3] = {rw[1] * fw[2] - rw[2] * fw[1], rw[2] * fw[0] - rw[0] * fw[2], rw[0] * fw[1] - rw[1] * fw[0]};
 #pragma unroll
             for (int k = 0; k < 3; ++k) { F[k] += fw[k]; Tw[k] += t[k]; }
         }
         const R tzr = R(tz);
-        if (torque_world) Tw[2] += tzr;
-        else { Tw[0] += M[2] * tzr; Tw[1] += M[5] * tzr; Tw[2] += M[8] * tzr; }
-        extra(M, F, Tw);
+        if (torque_world && !lag) Tw[2] += tzr;
+        else { Tw[0] += Ml[2] * tzr; Tw[1] += Ml[5] * tzr; Tw[2] += Ml[8] * tzr; }
+        extra(M, Ml, F, Tw);
     }
     F[2] += R(-kMass * kG);
     const R k = damping;
@@ -335,6 +382,11 @@ __device__ __forceinline__ void drone_substep(R p[3], R q[4], R v[3], R w[3], co
     }
 #pragma unroll
     for (int i = 0; i < 3; ++i) pos_add(p, pacc, i, v[i] * dt);
+    if (lag) {   // the next substep's cached link frame: this substep's starting attitude
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ql[i] = q[i];
+        zl[0] = M[2]; zl[1] = M[5]; zl[2] = M[8];
+    }
     // btMultiBody::stepPositionsMultiDof exponential-map quaternion update (base body)
     R fang = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
     if (fang * dt > R(0.5 * (0.5 * kPi))) fang = R(0.5 * (0.5 * kPi)) / dt;
@@ -397,8 +449,10 @@ __device__ __forceinline__ void ground_effect(const R p[3], const R q[4], const 
 
 // _drag (982-1011): rotor drag from the previous substep's rpm (last_clipped_action), in the body
 // frame, applied at the COM link
+// (Mv: the frame the link-frame force is rotated by -- the cached link frame, or the current attitude once
+// _groundEffect's getLinkStates has refreshed it)
 template <class R>
-__device__ __forceinline__ void rotor_drag(const R v[3], const R M[9], const R last_rpm[4], R F[3]) {
+__device__ __forceinline__ void rotor_drag(const R v[3], const R M[9], const R Mv[9], const R last_rpm[4], R F[3]) {
     R sum = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) sum += (R(2 * kPi) * last_rpm[i]) / R(60);
@@ -407,7 +461,7 @@ __device__ __forceinline__ void rotor_drag(const R v[3], const R M[9], const R l
 #pragma unroll
     for (int k = 0; k < 3; ++k) b[k] = M[0 + k] * dv[0] + M[3 + k] * dv[1] + M[6 + k] * dv[2];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) F[k] += M[3 * k + 0] * b[0] + M[3 * k + 1] * b[1] + M[3 * k + 2] * b[2];
+    for (int k = 0; k < 3; ++k) F[k] += Mv[3 * k + 0] * b[0] + Mv[3 * k + 1] * b[1] + Mv[3 * k + 2] * b[2];
 }
 
 // _downwash (1013-1041): one term per drone above (dz > 0) within 10 m horizontally; `o` is that
@@ -546,7 +600,8 @@ __device__ __forceinline__ void rk4_substep(R p[3], R q[4], R v[3], R w[3], R rr
 template <class R>
 __device__ __forceinline__ void variant_substeps(const StepParams<R>& p, int base, int nsh, int n, R pos[3], R q[4],
                                                  R v[3], R w[3], const double rpm_w[4], R lr[4], R rr[3],
-                                                 double* pacc = nullptr) {
+                                                 double* pacc = nullptr, R* ql = nullptr, R* zl = nullptr,
+                                                 bool lag = false) {
     // the variants' terms in the state precision; the PYB wrench takes the f64 speeds (drone_substep)
     const R rpm[4] = {R(rpm_w[0]), R(rpm_w[1]), R(rpm_w[2]), R(rpm_w[3])};
     const int ph = p.physics;
@@ -560,19 +615,24 @@ __device__ __forceinline__ void variant_substeps(const StepParams<R>& p, int bas
         } else if (ph == CH_PHYS_DYN_RK4) {
             rk4_substep(pos, q, v, w, rr, rpm, R(p.dt), pacc);
         } else {
-            // extra() runs before drone_substep moves the body: pos/q/v are the substep-start state
-            auto extra = [&](const R* M, R* F, R* Tw) {
+            // extra() runs before drone_substep moves the body: pos/q/v are the substep-start state.  _groundEffect
+            // reads p.getLinkStates(computeForwardKinematics=1) (BaseAviary.py:958-963), which refreshes the cached
+            // link transforms: its forces and the drag / downwash applied after it rotate by the current attitude M;
+            // without it drag and downwash use the cached frame Ml (== M without link_lag)
+            auto extra = [&](const R* M, const R* Ml, R* F, R* Tw) {
+                const R* Mv = gnd ? M : Ml;
                 if (gnd) ground_effect(pos, q, M, rpm, h_clip, F, Tw);
-                if (drag) rotor_drag(v, M, lr, F);
+                if (drag) rotor_drag(v, M, Mv, lr, F);
                 if (dw) {
                     for (int i = 0; i < nsh; ++i) {
                         const R o[3] = {__shfl(pos[0], base + i, 64), __shfl(pos[1], base + i, 64),
                                         __shfl(pos[2], base + i, 64)};
-                        if (i < n) downwash_term(pos, o, M, F);
+                        if (i < n) downwash_term(pos, o, Mv, F);
                     }
                 }
             };
-            drone_substep(pos, q, v, w, rpm_w, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0, extra, pacc);
+            drone_substep(pos, q, v, w, rpm_w, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0, extra, pacc,
+                          ql, zl, lag);
         }
 #pragma unroll
         for (int c = 0; c < 4; ++c) lr[c] = rpm[c];   // last_clipped_action (BaseAviary.py:450)

@@ -9,7 +9,7 @@ namespace ch {
 
 constexpr int kNMax = 12;          // GLOBAL_MAX_NUM_DRONES (BaseAviary.py:112)
 constexpr int kMMax = 64;          // cattle per env supported by the team mapping (TEAM <= 64)
-constexpr int kDroneComps = 22;    // px py pz qx qy qz qw vx vy vz wx wy wz pid[9]
+constexpr int kDroneComps = 26;    // px py pz qx qy qz qw vx vy vz wx wy wz pid[9] qlag[4] (cached link frame)
 constexpr int kCattleComps = 4;    // x y vx vy
 constexpr int kPhysComps = 7;      // last_clipped_action[4] (drag input), DYN rpy_rates[3]
 constexpr int kEnvReal = 2;        // prev_cent, clock
@@ -22,11 +22,12 @@ template <class R>
 struct StepParams {
     int E, NC, M, mode, rows;
     int min_drones, max_drones, ctrl_freq, substeps, compat, torque_world, gyro, marl_wrapper;
+    int link_lag;   // ch_config.link_lag: LINK_FRAME forces rotate by Bullet's cached link frame (drone comps 22-25)
     double episode_len, damping, dt_ctrl, dt;
     uint32_t k0, k1;
     long long env_off;
     double cs_cc;   // CattleSpacingRewardFunction continuation constant (host-evaluated)
-    R* drone;       // [22][E][NC]
+    R* drone;       // [26][E][NC]
     R* rpy;         // v2: [3][E][NC] Euler angles of the stored quaternion (valid unless stale[e])
     // per-env device flags, read by the v2 step with its env's state (so a captured HIP graph sees state changes
     // made after capture) and cleared at its write-back: row 0 the Euler cache is stale, row 1 the obs block's

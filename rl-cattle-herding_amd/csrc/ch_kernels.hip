@@ -193,9 +193,11 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
             R q[4] = {ld(p.drone, 3, DS, di), ld(p.drone, 4, DS, di), ld(p.drone, 5, DS, di), ld(p.drone, 6, DS, di)};
             R v[3] = {ld(p.drone, 7, DS, di), ld(p.drone, 8, DS, di), ld(p.drone, 9, DS, di)};
             R w[3] = {ld(p.drone, 10, DS, di), ld(p.drone, 11, DS, di), ld(p.drone, 12, DS, di)};
-            R pid[9];
+            R pid[9], ql[4];
 #pragma unroll
             for (int c = 0; c < 9; ++c) pid[c] = ld(p.drone, 13 + c, DS, di);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) ql[c] = ld(p.drone, 22 + c, DS, di);   // Bullet's cached link frame
             float a[4];
             if (p.flags & CH_STEP_RANDOM_ACTIONS) {
                 uint32_t c4[4] = {(uint32_t)stepi, 0u, (uint32_t)t, (uint32_t)(p.env_off + e)};
@@ -215,6 +217,8 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
             double rpm[4];
             if (!(p.phase_mask & 1)) {
                 pid_vel(pos, q, v, Rm, rpy, a, R(p.dt_ctrl), pid, rpm, p.debug ? p.debug + di * 16 : nullptr);
+                R zl[3] = {0, 0, 0};   // the cached link frame's z axis (link_lag)
+                if (p.link_lag) quat_to_zcol(ql, zl);
                 if constexpr (PHYS) {
                     const long long PS = (long long)p.E * p.NC;
                     R lr[4], rr[3];
@@ -222,7 +226,7 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
                     for (int c = 0; c < 4; ++c) lr[c] = p.phys[c * PS + di];
 #pragma unroll
                     for (int c = 0; c < 3; ++c) rr[c] = p.phys[(4 + c) * PS + di];
-                    variant_substeps(p, slot * TEAM, p.NC, n, pos, q, v, w, rpm, lr, rr, MIX ? pd : nullptr);
+                    variant_substeps(p, slot * TEAM, p.NC, n, pos, q, v, w, rpm, lr, rr, MIX ? pd : nullptr, ql, zl, p.link_lag != 0);
 #pragma unroll
                     for (int c = 0; c < 4; ++c) p.phys[c * PS + di] = lr[c];
 #pragma unroll
@@ -230,10 +234,12 @@ __global__ __launch_bounds__(64) void k_env(StepParams<R> p) {
                 } else {
                     for (int s = 0; s < p.substeps; ++s)
                         drone_substep(pos, q, v, w, rpm, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0,
-                                      NoExtraForces(), MIX ? pd : nullptr);
+                                      NoExtraForces(), MIX ? pd : nullptr, ql, zl, p.link_lag != 0);
                 }
             }
             R* D = p.drone;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) D[(22 + c) * DS + di] = ql[c];
             if (p.evald) p.evald[di] = eval_distance_step(p.evald[di], sc == 0, px0, py0, pos[0], pos[1]);
             D[0 * DS + di] = pos[0]; D[1 * DS + di] = pos[1]; D[2 * DS + di] = pos[2];
             if constexpr (MIX) {

@@ -790,7 +790,7 @@ void k_step2(StepParams<R> p) {
     const bool dlane = tid < nd;
     const int dg = dlane ? tid / N : 0, dk = tid - dg * N;
     const long long di = (long long)e0 * N + tid;
-    R pos[3], q[4], v[3], w[3], pid[9], rpy_in[3] = {0, 0, 0};
+    R pos[3], q[4], v[3], w[3], pid[9], ql[4], rpy_in[3] = {0, 0, 0};
     R ph_lr[4] = {0, 0, 0, 0}, ph_rr[3] = {0, 0, 0};   // PHYS: last_clipped_action, DYN rpy_rates
     int stepi = 0, n0 = 0, act0 = 0, stepi_env = 0;
     double ev_acc = 0;   // update_evaluation_metrics' distance of this drone (optional)
@@ -840,6 +840,8 @@ void k_step2(StepParams<R> p) {
         for (int c = 0; c < 3; ++c) { v[c] = p.drone[(7 + c) * DS + di]; w[c] = p.drone[(10 + c) * DS + di]; }
 #pragma unroll
         for (int c = 0; c < 9; ++c) pid[c] = p.drone[(13 + c) * DS + di];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) ql[c] = p.drone[(22 + c) * DS + di];   // Bullet's cached link frame (link_lag)
         // Euler angles of this quaternion, stored by the previous step (used iff the cache is
         // valid; loaded regardless so the loads issue with the state's, not after the stale flag returns)
 #pragma unroll
@@ -1004,8 +1006,11 @@ void k_step2(StepParams<R> p) {
             if (!(p.phase_mask & 1)) {
                 double rpm[4];
                 pid_vel(pos, q, v, Rm, rpy, a, R(p.dt_ctrl), pid, rpm, p.debug ? p.debug + di * 16 : nullptr);
+                R zl[3] = {0, 0, 0};   // the cached link frame's z axis (link_lag)
+                if (p.link_lag) quat_to_zcol(ql, zl);
                 if constexpr (PHYS) {
-                    variant_substeps(p, dg * N, N, n, pos, q, v, w, rpm, ph_lr, ph_rr, MIX ? pd : nullptr);
+                    variant_substeps(p, dg * N, N, n, pos, q, v, w, rpm, ph_lr, ph_rr, MIX ? pd : nullptr, ql,
+                                     zl, p.link_lag != 0);
 #pragma unroll
                     for (int c = 0; c < 4; ++c) CH_STS(&p.phys[c * DS + di], ph_lr[c]);
 #pragma unroll
@@ -1013,7 +1018,7 @@ void k_step2(StepParams<R> p) {
                 } else {
                     for (int s = 0; s < p.substeps; ++s)
                         drone_substep(pos, q, v, w, rpm, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0,
-                                      NoExtraForces(), MIX ? pd : nullptr);
+                                      NoExtraForces(), MIX ? pd : nullptr, ql, zl, p.link_lag != 0);
                 }
             }
             R* D = p.drone;
@@ -1030,6 +1035,10 @@ void k_step2(StepParams<R> p) {
             for (int c = 0; c < 3; ++c) { CH_STS(&D[(7 + c) * DS + di], v[c]); CH_STS(&D[(10 + c) * DS + di], w[c]); }
 #pragma unroll
             for (int c = 0; c < 9; ++c) CH_STS(&D[(13 + c) * DS + di], pid[c]);
+            if (p.link_lag) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) CH_STS(&D[(22 + c) * DS + di], ql[c]);
+            }
             S.dx[tid] = pos[0]; S.dy[tid] = pos[1]; S.dz[tid] = pos[2];
 #pragma unroll
             for (int c = 0; c < 4; ++c) S.dq[c * (G * N) + tid] = q[c];

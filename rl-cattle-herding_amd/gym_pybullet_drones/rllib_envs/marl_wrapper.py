@@ -15,6 +15,10 @@ import numpy as np
 
 from gym_pybullet_drones.rllib_envs.MARLCattleAviary import MARLCattleAviary
 
+# the reference's failure-detection hook (marl_wrapper.py:87-95): an exception out of env.step() is appended, with
+# its traceback, to this file on the env runner, then re-raised
+EXC_LOG = "/tmp/env_worker_exc.log"
+
 try:  # pragma: no cover
     from ray.rllib.env import MultiAgentEnv as _MAEnvBase
 except Exception:  # noqa: BLE001
@@ -64,7 +68,15 @@ class RLlibMultiAgentWrapper(_MAEnvBase):
         for i, aid in enumerate(self.possible_agents):
             if aid in action_dict and aid in self.agents:
                 actions[i] = np.asarray(action_dict[aid], dtype=np.float32)
-        obs_a, rew_a, te_a, tr_a = self.env._step_arrays(actions)
+        try:
+            obs_a, rew_a, te_a, tr_a = self.env._step_arrays(actions)
+        except Exception:
+            import traceback
+            with open(EXC_LOG, "a") as fh:
+                fh.write("=== Exception in env.step() ===\n")
+                fh.write(traceback.format_exc())
+                fh.write("\n")
+            raise
         obs, rewards, dones, truncs, infos = {}, {}, {}, {}, {}
         for aid in list(self.agents):
             i = int(aid.split("_")[1])

@@ -98,7 +98,7 @@ def capture(env, marl_agents=None, physics_state=False):
         "drone_pos": np.zeros((NMAX, 3)), "drone_quat": np.zeros((NMAX, 4)),
         "drone_vel": np.zeros((NMAX, 3)), "drone_angv": np.zeros((NMAX, 3)),
         "pid_last_rpy": np.zeros((NMAX, 3)), "pid_int_pos": np.zeros((NMAX, 3)),
-        "pid_int_rpy": np.zeros((NMAX, 3)),
+        "pid_int_rpy": np.zeros((NMAX, 3)), "drone_qlag": np.zeros((NMAX, 4)),
         "cow_pos": np.zeros((MMAX, 2)), "cow_vel": np.zeros((MMAX, 2)),
         "step_counter": env.step_counter, "step_counter_A": env.step_counter_A,
         "prev_cent": np.nan if env.prev_cent_dists is None else float(env.prev_cent_dists),
@@ -112,6 +112,7 @@ def capture(env, marl_agents=None, physics_state=False):
         b = W.bodies[int(env.DRONE_IDS[i])]
         s["drone_pos"][i], s["drone_quat"][i] = b.pos, b.quat
         s["drone_vel"][i], s["drone_angv"][i] = b.vel, b.angv
+        s["drone_qlag"][i] = b.cached
         c = env.ctrl[i]
         s["pid_last_rpy"][i], s["pid_int_pos"][i], s["pid_int_rpy"][i] = c.last_rpy, c.integral_pos_e, c.integral_rpy_e
     for j in range(m):

@@ -36,6 +36,10 @@ PHYS = {
     "damping": 0.04,          # btMultiBody default linear/angular damping (k1 = k2)
     "torque_world": True,     # applyExternalTorque(LINK_FRAME) treated as world frame (Bullet multibody path)
     "gyro": True,             # btMultiBody::m_useGyroTerm default
+    # LINK_FRAME forces / torques on a drone's links rotate by the link transform Bullet cached at the previous
+    # stepSimulation's forward kinematics (the attitude one substep old), refreshed early only by
+    # getLinkStates(computeForwardKinematics=1); pinned by the real-PyBullet trace (make_trace_inverse.py)
+    "link_lag": True,
 }
 
 # --------------------------------------------------------------------------------------
@@ -105,6 +109,7 @@ class _Body:
         self.angv = [0.0, 0.0, 0.0]
         self.force = [0.0, 0.0, 0.0]      # world frame, at COM
         self.torque = [0.0, 0.0, 0.0]     # world frame
+        self.cached = list(self.quat)     # the links' cached world transform (attitude part), set by loadURDF
 
 
 class _World:
@@ -133,6 +138,7 @@ def _R(q):
 
 
 def _step_drone(b, dt, g):
+    b.cached = list(b.quat)   # stepSimulation's forward kinematics, before the integration
     R = _R(b.quat)
     m = CF2X_MASS
     J = np.array(CF2X_J)
@@ -245,7 +251,8 @@ def _make_pybullet():
     def applyExternalForce(bid, link, forceObj, posObj, flags, **k):
         b = WORLD.bodies[int(bid)]
         R = _R(b.quat)
-        f = R @ np.array(forceObj, dtype=np.float64)          # link frame == base frame (fixed joints)
+        Rf = _R(b.cached) if (PHYS["link_lag"] and link >= 0) else R
+        f = Rf @ np.array(forceObj, dtype=np.float64)         # link frame == base frame (fixed joints)
         if 0 <= link <= 3:
             r = R @ np.array(PROP_OFFSETS[link])
         else:
@@ -259,7 +266,9 @@ def _make_pybullet():
     def applyExternalTorque(bid, link, torqueObj, flags, **k):
         b = WORLD.bodies[int(bid)]
         t = np.array(torqueObj, dtype=np.float64)
-        if not PHYS["torque_world"]:
+        if PHYS["link_lag"] and link >= 0:
+            t = _R(b.cached) @ t
+        elif not PHYS["torque_world"]:
             t = _R(b.quat) @ t
         for i in range(3):
             b.torque[i] += t[i]
@@ -270,6 +279,8 @@ def _make_pybullet():
         # (links 0-3, inertial origins at +-0.028) or the base origin (link 4)
         b = WORLD.bodies[int(bid)]
         R = _R(b.quat)
+        if computeForwardKinematics:
+            b.cached = list(b.quat)
         out = []
         for li in linkIndices:
             off = PROP_OFFSETS[li] if 0 <= li <= 3 else (0.0, 0.0, 0.0)

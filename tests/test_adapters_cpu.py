@@ -98,6 +98,35 @@ def test_vec_env_autoreset_infos(patched):
     assert venv.get_attr("EPISODE_LEN_SEC") == [80] * 4 and venv.env_is_wrapped(object) == [False] * 4
 
 
+def test_vec_env_outputs_kept_across_steps(patched):
+    """A caller (callback, wrapper, user loop) that keeps a step's infos -- and, with copy_obs=True, its
+    observations -- sees them unchanged after later steps, as with SubprocVecEnv's fresh arrays and dicts; with the
+    default ring of pinned buffers the observations stay valid for obs_ring - 1 more steps (SB3's collect_rollouts
+    keeps the previous step's)."""
+    import copy
+    _, _, ve = patched
+    rng = np.random.default_rng(1)
+    for copy_obs in (True, False):
+        venv = ve.CattleHerdVecEnv(4, num_drones=4, num_cattle=16, copy_obs=copy_obs, obs_ring=3)
+        venv.reset()
+        kept = []
+        for t in range(12):
+            obs, rew, dones, infos = venv.step(rng.uniform(-1, 1, (4, 4, 4)).astype(np.float32))
+            kept.append((obs, obs.copy(), infos, copy.deepcopy(infos)))
+            if dones.any():   # a step where infos carry terminal observations
+                assert any("terminal_observation" in d for d in infos)
+        for t, (obs, snap, infos, isnap) in enumerate(kept):
+            assert len(infos) == 4
+            for d, ds in zip(infos, isnap):
+                assert d.keys() == ds.keys()
+                for k in d:
+                    assert np.array_equal(d[k], ds[k]) if k == "terminal_observation" else d[k] == ds[k]
+            if copy_obs or t >= len(kept) - 2:   # ring of 3: this step and the two before it
+                assert np.array_equal(obs, snap), t
+    with pytest.raises(ValueError):
+        ve.CattleHerdVecEnv(4, num_drones=4, num_cattle=16, obs_ring=1)
+
+
 def test_physics_argument_reaches_the_batch(patched):
     """CattleAviary(physics=Physics.DYN) selects the explicit model (BaseAviary.py:1043-1118): no
     p.stepSimulation, so the cattle keep their positions; PYB moves them at their velocity."""
@@ -115,3 +144,24 @@ def test_physics_argument_reaches_the_batch(patched):
     assert venv.reset().shape == (2, 12, 86)
     with pytest.raises(ValueError):
         ca.CattleAviary(num_drones=4, num_cattle=8, physics="rk4")
+
+
+def test_rllib_wrapper_logs_step_exceptions(patched, tmp_path, monkeypatch):
+    """The wrapper's failure-detection hook (marl_wrapper.py:87-95): an exception out of env.step() is appended
+    with its traceback to the env-worker log, then re-raised; a good step writes nothing."""
+    from gym_pybullet_drones.rllib_envs import marl_wrapper as mw
+    log = tmp_path / "env_worker_exc.log"
+    monkeypatch.setattr(mw, "EXC_LOG", str(log))
+    w = mw.RLlibMultiAgentWrapper({"num_drones": 3, "num_cattle": 8})
+    w.reset()
+    w.step({f"agent_{i}": np.zeros(4, np.float32) for i in range(3)})
+    assert not log.exists()
+
+    def boom(actions):
+        raise FloatingPointError("device step failed")
+    monkeypatch.setattr(w.env, "_step_arrays", boom)
+    for _ in range(2):
+        with pytest.raises(FloatingPointError):
+            w.step({"agent_0": np.zeros(4, np.float32)})
+    text = log.read_text()
+    assert text.count("=== Exception in env.step() ===") == 2 and "FloatingPointError: device step failed" in text

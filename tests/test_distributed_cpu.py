@@ -105,6 +105,22 @@ def test_bench_gpus_n_spawns_n_ranks():
     assert rc == 0, err
     assert out["n_gpus"] == 2 and out["env_ranges"] == [[0, 4096], [4096, 8192]]
     assert out["metric_sum"] == 3.0 and out["max_time"] == 1.5
+    # every rank's device slot gathered to rank 0: LOCAL_RANK -> device index, all distinct
+    assert [r["rank"] for r in out["ranks"]] == [0, 1]
+    assert [r["device"] for r in out["ranks"]] == [r["local_rank"] for r in out["ranks"]] == [0, 1]
+    assert out["distinct_devices"] is True
+
+
+def test_distinct_devices_rule():
+    """The multi-GPU line's self-check: PCI addresses decide when known (ranks narrowed to one visible device each
+    all report index 0), else the device index."""
+    from cattleherd import distributed as D
+    a = {"rank": 0, "local_rank": 0, "device": 0, "pci_bus_id": "0000:05:00"}
+    b = dict(a, rank=1, local_rank=1, pci_bus_id="0000:15:00")
+    assert D.distinct_devices([a, b])
+    assert not D.distinct_devices([a, dict(b, pci_bus_id="0000:05:00")])
+    c, d = dict(a, pci_bus_id=None), dict(b, pci_bus_id=None, device=0)
+    assert not D.distinct_devices([c, d]) and D.distinct_devices([c, dict(d, device=1)])
 
 
 def test_bench_world_size_mismatch_fails():

@@ -1,8 +1,11 @@
 """The f32 mode's precision policy, checked on the host (tools/f32_emu.py): the drone path evaluated with numpy
-float32 / float64 per piece from oracle states reproduces the oracle bit for bit in all-f64, misses 1e-4 relative
-on the body rates in all-f32 (the pre-round-4 kernel: 2.5e-4 measured on the GPU, profiles/r04/zj/f32_probe_before.log),
-and holds it with the pieces ch_device.h carries in f64 since round 4 (8.0e-5 measured on the GPU,
-profiles/r04/zk/f32_probe3.log; the GPU test is test_gpu_parity.py::test_f32_throughput_mode_error_budget)."""
+float32 / float64 per piece from oracle states reproduces the oracle bit for bit in all-f64 and misses in all-f32.
+With the rounds 1-4 rigid body the kernel's pieces in f64 (torque mix, motor speeds, prop wrench, angular update)
+held the body rates to 1e-4 relative (8.0e-5 measured on the GPU, profiles/r04/zk/f32_probe3.log).  Bullet's cached
+link frame (link_lag, the trace-pinned default since round 5) couples the yaw rate to the roll / pitch torques through
+the one-substep-old thrust axis, and every f32 piece of the PID feeds that coupling: the same policy holds the body
+rates to 3e-4 (yaw; roll and pitch stay inside 1e-4) -- DESIGN.md §3.  The GPU test is
+test_gpu_parity.py::test_f32_throughput_mode_error_budget."""
 import os
 import sys
 
@@ -15,5 +18,6 @@ def test_f32_policy_body_rates_within_1e4_relative():
     d = f32_emu.draw(E=96)
     pols = f32_emu.policies()
     assert f32_emu.errors(pols["all f64"], d) == (0.0, 0.0)
-    assert f32_emu.errors(pols["all f32 (before round 4)"], d)[1] > 1e-4
-    assert f32_emu.errors(pols["kernel (round 4)"], d)[1] < 1e-4
+    e32 = f32_emu.errors(pols["all f32 (before round 4)"], d)[1]
+    ek = f32_emu.errors(pols["kernel (round 4)"], d)[1]
+    assert e32 > 2.5e-4 and ek < 3e-4 and ek < 0.75 * e32, (e32, ek)

@@ -59,7 +59,8 @@ def test_rollout_fixture_parity(fname):
     resets = set(d["reset_at"].tolist())
     idx = [t for t in range(T - 1) if t not in resets]
     nxt = stack([states[t + 1] for t in idx])
-    for k in ("drone_pos", "drone_quat", "drone_vel", "drone_angv", "pid_int_rpy", "pid_int_pos", "pid_last_rpy"):
+    for k in ("drone_pos", "drone_quat", "drone_vel", "drone_angv", "pid_int_rpy", "pid_int_pos", "pid_last_rpy",
+              "drone_qlag"):
         assert close(g[k][idx, :n], nxt[k][:, :n], 1e-9, 1e-12)[0], k
     if physics:
         assert close(g["last_rpm"][idx, :n], nxt["last_rpm"][:, :n], 1e-9, 1e-9)[0]
@@ -114,7 +115,8 @@ def test_step_vs_oracle(mode, n, m, level, compat):
     assert np.array_equal(tr.cpu().numpy(), np.stack([r[3] for r in ref]).reshape(E, K))
     g = b.get_state()
     want = stack([env.get_state() for env in envs])
-    for k in ("drone_pos", "drone_quat", "drone_vel", "drone_angv", "pid_int_rpy", "pid_int_pos", "pid_last_rpy"):
+    for k in ("drone_pos", "drone_quat", "drone_vel", "drone_angv", "pid_int_rpy", "pid_int_pos", "pid_last_rpy",
+              "drone_qlag"):
         assert close(g[k][:, :n], want[k][:, :n], 1e-9, 1e-12)[0], k
     assert close(g["cow_pos"], want["cow_pos"][:, :m], 1e-12, 1e-13)[0]
     assert close(g["cow_vel"], want["cow_vel"][:, :m], 1e-12, 1e-14)[0]
@@ -158,7 +160,7 @@ def test_physics_variant_step_vs_oracle(physics, mode, n, m):
     g = b.get_state()
     want = stack([env.get_state() for env in envs])
     for k in ("drone_pos", "drone_quat", "drone_vel", "drone_angv", "pid_int_rpy", "pid_int_pos", "pid_last_rpy",
-              "rpy_rates"):
+              "rpy_rates", "drone_qlag"):
         assert close(g[k][:, :n], want[k][:, :n], 1e-9, 1e-12)[0], k
     assert close(g["last_rpm"][:, :n], want["last_rpm"][:, :n], 1e-12, 1e-9)[0]
     assert close(g["cow_pos"], want["cow_pos"][:, :m], 1e-12, 1e-13)[0]
@@ -172,10 +174,10 @@ def _oracle_view(g, e, nmax):
     for k, v in g.items():
         x = np.asarray(v[e])
         if k in ("drone_pos", "drone_quat", "drone_vel", "drone_angv", "pid_last_rpy", "pid_int_pos", "pid_int_rpy",
-                 "last_rpm", "rpy_rates", "active"):
+                 "last_rpm", "rpy_rates", "active", "drone_qlag"):
             pad = np.zeros((nmax,) + x.shape[1:], x.dtype)
             pad[:x.shape[0]] = x
-            if k == "drone_quat":
+            if k in ("drone_quat", "drone_qlag"):
                 pad[x.shape[0]:, 3] = 1
             x = pad
         out[k] = x
@@ -203,6 +205,16 @@ def test_random_rollout_with_autoreset_vs_oracle(physics, mode, n, m):
     envs = [O.Env(mode, n, m, table, env_id=e, physics=ph) for e in range(E)]
     o0 = np.stack([env.reset() for env in envs])
     assert close(b.obs.cpu().numpy(), o0, 1e-6, 1e-7)[0]
+    if mode == 1:
+        # a MARL episode ends only when every agent has terminated (marl_wrapper.py:113-117): half the envs start with
+        # their drones 0.8 m apart and the level-0 spacing clock just short of its 10 s hold (curriculum_learning.py:13-34)
+        # so that auto-resets happen inside the rollout whatever the physics does with random actions
+        s = b.get_state()
+        ev = np.arange(E) % 2 == 0
+        s["drone_pos"][ev, :, 0] = 0.8 * np.arange(n)[None, :]
+        s["drone_pos"][ev, :, 1] = 0.0
+        s["clock"][ev] = 10.0 - 3.0 / 60
+        b.set_state({"drone_pos": s["drone_pos"], "clock": s["clock"]})
     R, K = b.obs_rows, b.reward_cols
     resets = 0
     for t in range(T):
@@ -234,7 +246,7 @@ def test_random_rollout_with_autoreset_vs_oracle(physics, mode, n, m):
     assert np.array_equal(st["episode"], want["episode"])
     assert np.array_equal(st["spawn_index"], want["spawn_index"])
     # last_clipped_action / rpy_rates are carried only under the variants that read them (PYB: unused)
-    for k in ("drone_pos", "drone_quat", "drone_vel") + (("last_rpm", "rpy_rates") if ph else ()):
+    for k in ("drone_pos", "drone_quat", "drone_vel", "drone_qlag") + (("last_rpm", "rpy_rates") if ph else ()):
         assert close(st[k][:, :n], want[k][:, :n], 1e-9, 1e-9)[0], k
     assert close(st["cow_pos"], want["cow_pos"][:, :m], 1e-12, 1e-13)[0]
     # update_evaluation_metrics' per-drone distance, accumulated on the device every step (BaseAviary.py:1415-1426)
@@ -272,7 +284,7 @@ def test_f32_throughput_mode_error_budget():
     One step from diverse oracle states (tests/diag/f32_probe.py over 256 states, profiles/r03/f32_probe.log):
     rewards within 1e-4 relative (measured max abs 1.5e-7, median relative 9e-8) with a 1e-6 floor for rewards
     near zero; observations within 1e-4 relative with a 1e-6 floor, and the body rates (columns 7-9) within
-    1e-4 relative down to 1e-8: the attitude loop's torque mix, the motor speeds, the body torque and the
+    1e-4 relative down to 1e-8 (the yaw rate, column 9, 3e-4 under the cached link frame): the attitude loop's torque mix, the motor speeds, the body torque and the
     angular-velocity update run in f64 (ch_device.h pid_vel / drone_substep; in f32 they left 2.5e-4 relative
     on rates of ~3e-3 rad/s, tools/f32_emu.py); terminated / truncated flags identical; the state round trip
     keeps the f64 positions."""
@@ -294,11 +306,17 @@ def test_f32_throughput_mode_error_budget():
     torch.cuda.synchronize()
     ref = [env.step(acts[e], autoreset=False) for e, env in enumerate(envs)]
     ro = np.stack([r[0] for r in ref])
-    # every column within 1e-4 relative with a 1e-6 floor
-    ok, worst = close(obs.cpu().numpy(), ro, 1e-4, 1e-6)
+    # every column but the yaw rate within 1e-4 relative with a 1e-6 floor
+    o = obs.cpu().numpy()
+    cols = [c for c in range(86) if c != 9]
+    ok, worst = close(o[..., cols], ro[..., cols], 1e-4, 1e-6)
     assert ok, worst
-    # the body rates (torque mix and angular-velocity update carried in f64) within 1e-4 relative down to 1e-8
-    ok, worst = close(obs.cpu().numpy()[..., 7:10], ro[..., 7:10], 1e-4, 1e-8)
+    # roll / pitch rates (torque mix and angular-velocity update carried in f64) within 1e-4 relative down to 1e-8;
+    # the yaw rate within 3e-4: Bullet's cached link frame (link_lag) couples it to the roll / pitch torques, and every
+    # f32 piece of the PID feeds that coupling (tools/f32_emu.py, tests/test_f32_emulation.py)
+    ok, worst = close(o[..., 7:9], ro[..., 7:9], 1e-4, 1e-8)
+    assert ok, worst
+    ok, worst = close(o[..., 9], ro[..., 9], 3e-4, 1e-8)
     assert ok, worst
     rr = np.array([r[1][0] for r in ref])
     assert close(rew.cpu().numpy()[:, 0], rr, 1e-4, 1e-6)[0], np.max(np.abs(rew.cpu().numpy()[:, 0] - rr))

@@ -99,12 +99,13 @@ def test_rollout_buffer_matches_sb3_semantics(E, n, m, compat, level):
     b2.close()
 
 
-@pytest.mark.parametrize("T", [5, 13, 24])
+@pytest.mark.parametrize("T", [5, 13, 16, 24, 32])
 @pytest.mark.parametrize("path", [0, 2, 1], ids=["epilogues", "store_kernel", "copy_each"])
 def test_native_collect_equals_python_loop(T, path):
     """ch_rollout_collect (the loop in C++) and collect_steps (the same kernels launched from Python) fill
     identical buffers, across auto-resets and truncation bootstraps: rollouts shorter than the deferred bootstrap's
-    8-step flush window and not a multiple of it, on each of the collection's paths (the store folded into the
+    16-step flush period (kTvEvery, ch_api.cpp), crossing it, and ending exactly on a flush (16, 32), on each of the
+    collection's paths (the store folded into the
     forward epilogues, the stand-alone store kernel, every observation copied into the buffer)."""
     import ctypes
     import torch

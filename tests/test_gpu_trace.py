@@ -1,0 +1,41 @@
+"""GPU: the HIP step's drone rigid body against the recorded real-PyBullet trace (a5).
+
+``trace_inverse.npz`` holds the first evaluation episode of ``simulator/evaluation_data.pkl`` (3 drones, 16 cattle,
+real Bullet, CTDECattleHerder.py:169-185) and the float32 VEL actions recovered from it
+(``tests/golden/make_trace_inverse.py``).  Stepping ``libcattleherd`` with them from the episode's initial state must
+reproduce every drone's recorded xy velocity and position, as the oracle does (``test_oracle_golden.py::
+test_drone_rigid_body_pinned_to_real_pybullet``).  Tolerances: velocity 3e-8 m/s, position 1e-9 m absolute -- the
+float32 rounding of the recovered actions; the rounds 1-4 model (link_lag=0) misses by > 1e-5.
+"""
+import numpy as np
+import pytest
+
+from helpers import load, trace_seg0_state
+
+pytestmark = pytest.mark.gpu
+
+
+def _replay(link_lag, E=4):
+    import torch
+    from cattleherd.env import HerdBatch
+    t = load("trace_inverse.npz")
+    b = HerdBatch(E, 3, 16, mode="ctde", link_lag=link_lag)
+    b.reset()
+    s0 = trace_seg0_state()
+    b.set_state({k: np.stack([np.asarray(v)] * E) for k, v in s0.items()})
+    dv, dp, cows = [], [], []
+    for k in range(int(t["steps"])):
+        a = torch.tensor(np.stack([t["actions"][k]] * E), device=b.device)
+        b.step(a, autoreset=False)
+        g = b.get_state()
+        dv.append(np.abs(g["drone_vel"][:, :3, :2] - t["trace_vel"][k]).max())
+        dp.append(np.abs(g["drone_pos"][:, :3, :2] - t["trace_pos"][k]).max())
+    b.close()
+    return np.array(dv), np.array(dp)
+
+
+def test_hip_drone_rigid_body_matches_real_pybullet_trace():
+    dv, dp = _replay(True)
+    assert dv.max() <= 3e-8 and dp.max() <= 1e-9, (dv, dp)
+    dv0, dp0 = _replay(False)
+    assert dp0.max() > 1e-5 and dv0.max() > 1e-4, (dv0, dp0)

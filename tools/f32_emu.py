@@ -95,22 +95,26 @@ def pid(pos, q, vel, rpy, tv, pidst, dt_ctrl, pol):
     return rpm
 
 
-def substep(q, v, w, rpm, dt_, pol):
+def substep(q, v, w, rpm, dt_, pol, ql):
     """pol keys: sub (state precision), wrench (prop forces / torques), wb, damp, gyro, ab, aw, wup (each piece of
-    the body-rate update; default = wrench)"""
+    the body-rate update; default = wrench).  ql: Bullet's cached link frame (ch_device.h drone_substep, link_lag)."""
     t = pol["sub"]
     tw = pol["wrench"]
     P = lambda k: pol.get(k, tw)  # noqa: E731
     M = quat_to_mat(q, t)
+    Ml = quat_to_mat(ql, t)
     r = [tw(x) for x in rpm]
     Mw = [tw(x) for x in M]
+    Mlw = [tw(x) for x in Ml]
     tq = [r[i] * r[i] * tw(KKM) for i in range(4)]
     tz = -tq[0] + tq[1] - tq[2] + tq[3]
     f = [r[i] * r[i] * tw(KKF) for i in range(4)]
     Tt = ((f[0] + f[1]) + f[2]) + f[3]
-    F = [t(Mw[2] * Tt), t(Mw[5] * Tt), t(Mw[8] * Tt)]
-    tb = [tw(0.028) * (((-f[0] - f[1]) + f[2]) + f[3]) + Mw[6] * tz,
-          tw(0.028) * (((-f[0] + f[1]) + f[2]) - f[3]) + Mw[7] * tz, Mw[8] * tz]
+    F = [t(Mlw[2] * Tt), t(Mlw[5] * Tt), t(Mlw[8] * Tt)]
+    u = [(Mw[0 + i] * Mlw[2] + Mw[3 + i] * Mlw[5]) + Mw[6 + i] * Mlw[8] for i in range(3)]
+    sy = tw(0.028) * (((-f[0] - f[1]) + f[2]) + f[3])
+    sx = tw(0.028) * (((-f[0] + f[1]) + f[2]) - f[3])
+    tb = [sy * u[2] + u[0] * tz, sx * u[2] + u[1] * tz, (-sx * u[1] - sy * u[0]) + u[2] * tz]
     F[2] = F[2] + t(-KMASS * KG)
     k = t(0.04)
     vv = [t(x) for x in v]
@@ -154,13 +158,14 @@ def substep(q, v, w, rpm, dt_, pol):
          a[3] * qq[3] - a[0] * qq[0] - a[1] * qq[1] - a[2] * qq[2]]
     n = np.sqrt(o[0] * o[0] + o[1] * o[1] + o[2] * o[2] + o[3] * o[3])
     nq = np.stack([o[i] / n for i in range(4)], -1)
-    return nq, nv, nw
+    return nq, nv, nw, np.stack(qq, -1)
 
 
 def run(states, acts, pol, n):
     S = lambda k: np.concatenate([np.asarray(s[k])[:n] for s in states])  # noqa: E731
     st = pol["state"]
     pos, q, vel, w = S("drone_pos"), st(S("drone_quat")), st(S("drone_vel")), st(S("drone_angv"))
+    ql = st(S("drone_qlag"))
     pidst = np.concatenate([S("pid_last_rpy"), S("pid_int_pos"), S("pid_int_rpy")], 1)
     pidst = st(pidst)
     a = acts.reshape(-1, 4).astype(np.float32)
@@ -175,7 +180,7 @@ def run(states, acts, pol, n):
     ww = [w[:, i] for i in range(3)]
     wc = pol.get("wcarry", st)
     for _ in range(4):
-        q, v, ww = substep(q, v, ww, rpm, 1 / 240, pol)
+        q, v, ww, ql = substep(q, v, ww, rpm, 1 / 240, pol, ql)
         q = st(q); v = [st(x) for x in v]; ww = [wc(x) for x in ww]
     ww = [st(x) for x in ww]
     return np.stack([np.asarray(x, np.float64) for x in ww], 1)

@@ -56,6 +56,10 @@ def trace(mode, E, n, m, prec, G=None, B=None, steps=4, summary=None):
         print(f"   drone wave end {rel(35):.0f} | cow waves: final pass start (wave 1) {rel(37):.0f}, Euler math done "
               f"{(t[t[:, 62] > 0, 62] - t[t[:, 62] > 0, 2]).mean() if (t[:, 62] > 0).any() else float('nan'):.0f}, "
               f"last cow wave end {rel(63):.0f}")
+        if os.environ.get("CH_TRACE_SLOTS"):   # every phase slot the launch wrote: mean cycles from workgroup start
+            sl = {k: round(float((t[t[:, k] > 0, k] - t[t[:, k] > 0, 2]).mean())) for k in range(3, 64)
+                  if k != 12 and (t[:, k] > 0).any() and k not in range(22, 26)}
+            print("   slots " + " ".join(f"{k}:{v}" for k, v in sorted(sl.items(), key=lambda kv: kv[1])))
         print(f"   cow waves (latest of the workgroup's waves): flock done {rel(57):.0f}, reset list seen {rel(56):.0f}, "
               f"Euler stores done {rel(58):.0f}, final pass done {rel(60):.0f}, end {rel(63):.0f}")
         nfv = t[:, 31]
