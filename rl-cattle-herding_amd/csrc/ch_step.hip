@@ -78,6 +78,22 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
 }
+// Quad broadcast: lane K of every group of four lanes, to all four (DPP quad_perm: a VALU move, no LDS traffic).
+// Called convergently by the whole wave.  With four drones per env the drones of an env are one quad of the drone wave.
+template <int K> __device__ __forceinline__ int qb(int x) {
+    return __builtin_amdgcn_update_dpp(0, x, K | (K << 2) | (K << 4) | (K << 6), 0xf, 0xf, false);
+}
+template <int K> __device__ __forceinline__ float qb(float x) { return __builtin_bit_cast(float, qb<K>(__builtin_bit_cast(int, x))); }
+template <int K> __device__ __forceinline__ double qb(double x) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, x);
+    const int lo = qb<K>((int)(unsigned)u), hi = qb<K>((int)(unsigned)(u >> 32));
+    return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+// the four drones' values of this lane's env, in drone order
+template <class T> __device__ __forceinline__ void qall(T x, T out[4]) {
+    out[0] = qb<0>(x); out[1] = qb<1>(x); out[2] = qb<2>(x); out[3] = qb<3>(x);
+}
+
 // called convergently by a whole wave: its LDS writes are published, then the counter is bumped once
 __device__ __forceinline__ void lds_signal(int* f) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -313,12 +329,18 @@ __device__ __forceinline__ int nearest_two(const R* dx, const R* dy, int b0, int
 // spacing reward terms of drone slot u from its two nearest-neighbour distances (CattleAviary.py:230-246,
 // 572-679): simple and complex spacing of both, and the drone's spacing reward
 template <class R>
-__device__ __forceinline__ void spacing_terms(V2Smem<R>& S, const Level& Lv, bool compat, int u, R m1, R m2) {
-    const R sa = simple_spacing(m1, Lv), sb = simple_spacing(m2, Lv);
-    const R ca = complex_spacing(m1, Lv), cb = complex_spacing(m2, Lv);
-    R ps = 0;   // per-drone spacing reward (CattleAviary.py:238-246)
+__device__ __forceinline__ void spacing_terms_r(const Level& Lv, bool compat, R m1, R m2, R& sa, R& sb, R& ca, R& cb,
+                                                R& ps) {
+    sa = simple_spacing(m1, Lv); sb = simple_spacing(m2, Lv);
+    ca = complex_spacing(m1, Lv); cb = complex_spacing(m2, Lv);
+    ps = 0;   // per-drone spacing reward (CattleAviary.py:238-246)
     if (compat || m1 < R(INFINITY)) ps += (ca + sa) / R(2.0);
     if (compat || m2 < R(INFINITY)) ps += (cb + sb) / R(2.0);
+}
+template <class R>
+__device__ __forceinline__ void spacing_terms(V2Smem<R>& S, const Level& Lv, bool compat, int u, R m1, R m2) {
+    R sa, sb, ca, cb, ps;
+    spacing_terms_r(Lv, compat, m1, m2, sa, sb, ca, cb, ps);
     S.sa[u] = sa; S.sb[u] = sb; S.ca[u] = ca; S.cb[u] = cb; S.psp[u] = ps;
 }
 
@@ -764,6 +786,16 @@ void k_step2(StepParams<R> p) {
 #else
     constexpr bool SPLIT = false;
 #endif
+    // QUAD (the CTDE 16-env x 4-drone geometry): the per-env bookkeeping -- centroids, _computeTerminated /
+    // _computeTruncated, the reset decision, the reward's per-drone sums, metrics and the env write-back -- runs on the
+    // drone wave's quads (env g = lanes 4g..4g+3, the env's drones) with the per-drone terms in registers and
+    // gathered by DPP quad broadcasts in drone order, instead of on 16 env lanes reading them back from LDS.
+    // CH_NO_QUAD for the env-lane form.
+#ifdef CH_NO_QUAD
+    constexpr bool QUAD = false;
+#else
+    constexpr bool QUAD = !marl && GT == 16 && NT == 4 && !SPLIT;
+#endif
     const int G = GT ? GT : p.G, N = NT ? NT : p.NC, M = MT ? MT : p.M, P = MT ? MT * (MT - 1) / 2 : p.P;
     const int rows = marl ? N : 12;
     const V2Layout L(G, N, M, P, MODE, (int)sizeof(R), PW ? (int)(blockDim.x >> 6) - 1 : 0, !PW && p.sep);
@@ -1053,6 +1085,9 @@ void k_step2(StepParams<R> p) {
 
         // per-drone reward terms (CattleAviary.py:230-246, 572-679) and neighbour obs (BaseRLAviary.py:303-317)
         int nb1 = -1, nb2 = -1;   // the two nearest drones (kept for a fast reset's terminal observation)
+        // QUAD: this drone's terms in registers (nearest distances, flags, spacing terms; the cattle term after H)
+        R q_pa = 0, q_pb = 0, q_sa = 0, q_sb = 0, q_ca = 0, q_cb = 0, q_ps = 0, q_sc = 0;
+        int q_df = 0;
         if (live && task) {
             const int i = dk, b0 = dg * N;
             const R xi = pos[0], yi = pos[1];
@@ -1079,8 +1114,13 @@ void k_step2(StepParams<R> p) {
             }
             if (iso) f |= 4;
             if (fabs(pos[2] - R(kTargetAlt)) > R(kTargetAlt * 0.6)) f |= 1;
-            S.pa[tid] = m1; S.pb[tid] = m2; S.dflags[tid] = f;
-            if constexpr (!SPLIT) spacing_terms(S, LT[ei[I_LEVEL * G + dg]], p.compat != 0, tid, m1, m2);
+            if constexpr (QUAD) {
+                q_pa = m1; q_pb = m2; q_df = f;
+                spacing_terms_r(LT[ei[I_LEVEL * G + dg]], p.compat != 0, m1, m2, q_sa, q_sb, q_ca, q_cb, q_ps);
+            } else {
+                S.pa[tid] = m1; S.pb[tid] = m2; S.dflags[tid] = f;
+                if constexpr (!SPLIT) spacing_terms(S, LT[ei[I_LEVEL * G + dg]], p.compat != 0, tid, m1, m2);
+            }
             // offsets from the f64 positions in f32 mode (S.dxd; the same array as S.dx in f64 mode)
             if (wobs) obs_nbr(obs_wg + dg * RW, S.dxd, S.dyd, b0, i, i1, i2);
             nb1 = i1; nb2 = i2;
@@ -1099,12 +1139,14 @@ void k_step2(StepParams<R> p) {
         // 30.5k cycles but the drone wave's end moved from 37.0k to 38.4k (the cow waves' final pass now competes
         // with its reward), 197.4 vs 196.8 M env-steps/s.
 #ifdef CH_EARLY_RESET
-        constexpr bool EARLY = !marl && !SPLIT;
+        constexpr bool EARLY = !marl && !SPLIT && !QUAD;
 #else
         constexpr bool EARLY = false;
 #endif
-        const int g = tid;
-        const bool envl = g < Gv;
+        // the env this lane keeps the books of: lane g (env lanes), or the lane's quad (QUAD; lane k = 0 stores)
+        const int g = QUAD ? dg : tid;
+        const bool envl = QUAD ? dlane : g < Gv;
+        const bool envw = envl && (!QUAD || dk == 0);
         bool h_done = !EARLY;
         if constexpr (EARLY) {
             const int lv0 = envl ? ei[I_LEVEL * G + g] : 0;
@@ -1113,7 +1155,8 @@ void k_step2(StepParams<R> p) {
         if (h_done) lds_wait(fl + F_H, Gv * M + force, p.err);   // every cow item
         if (tid == 0) TS(6, (long long)clock64());
         if (live && task && !SPLIT && h_done) {
-            S.scat[tid] = cattle_term(S, tid, M, R(p.cs_cc));
+            if constexpr (QUAD) q_sc = cattle_term(S, tid, M, R(p.cs_cc));
+            else S.scat[tid] = cattle_term(S, tid, M, R(p.cs_cc));
             if constexpr (marl) {
                 // MARLCattleAviary._computeReward's per-agent part at the step's starting level
                 // (MARLCattleAviary.py:110-178), on every drone lane at once: the prefix
@@ -1170,6 +1213,19 @@ void k_step2(StepParams<R> p) {
         PT cent = 0;   // HerdCentroid/DroneCentroid distance (f64 also in f32 mode; R(cent) where the f32 math reads it)
         R eff = 0, ms = R(INFINITY), scx = 0, scy = 0;
         const PT max_step_p = PT(0.3 * kMaxSpeedKmh * (1000.0 / 3600.0)) / PT(p.ctrl_freq);
+        // QUAD: the env's four drones' positions and terms on every lane of its quad (convergent DPP moves)
+        constexpr int NQ = QUAD ? 4 : 1;
+        PT qx[NQ], qy[NQ];
+        R qpa[NQ], qpb[NQ], qsa[NQ], qsb[NQ], qca[NQ], qcb[NQ], qps[NQ], qsc[NQ];
+        int qdf[NQ];
+        if constexpr (QUAD) {
+            PT x0 = 0, y0 = 0;
+            if (live) {
+                if constexpr (MIX) { x0 = pd[0]; y0 = pd[1]; } else { x0 = PT(pos[0]); y0 = PT(pos[1]); }
+            }
+            qall(x0, qx); qall(y0, qy); qall(q_pa, qpa); qall(q_pb, qpb); qall(q_df, qdf);
+            qall(q_sa, qsa); qall(q_sb, qsb); qall(q_ca, qca); qall(q_cb, qcb); qall(q_ps, qps); qall(q_sc, qsc);
+        }
         if (envl && task) {
             const int n = f_n;
             PT sdx = 0, sdy = 0;
@@ -1179,7 +1235,7 @@ void k_step2(StepParams<R> p) {
             // that starts at +0 unchanged (x + +0 = x unless x = -0, and such a sum is never -0)
             CH_UNROLL for (int i = 0; i < N; ++i) {
                 const bool li = i < n;
-                const PT xi = S.dxd[b0 + i], yi = S.dyd[b0 + i];
+                const PT xi = QUAD ? qx[i % NQ] : S.dxd[b0 + i], yi = QUAD ? qy[i % NQ] : S.dyd[b0 + i];
                 sdx += li ? xi : PT(0); sdy += li ? yi : PT(0);
             }
             sdx = divc(sdx, PT(n)); sdy = divc(sdy, PT(n));
@@ -1190,8 +1246,8 @@ void k_step2(StepParams<R> p) {
             uint8_t any = 0;
             CH_UNROLL for (int i = 0; i < N; ++i) {
                 const bool li = i < n;
-                const R pa = S.pa[b0 + i];
-                const uint8_t df = li ? S.dflags[b0 + i] : 0;
+                const R pa = QUAD ? qpa[i % NQ] : S.pa[b0 + i];
+                const uint8_t df = li ? (QUAD ? (uint8_t)qdf[i % NQ] : S.dflags[b0 + i]) : 0;
                 if (li && pa < ms) ms = pa;
                 anynan |= (df & 8) != 0;
                 any |= df;
@@ -1409,14 +1465,14 @@ void k_step2(StepParams<R> p) {
         }
         // publish the reset list: the cow waves rebuild those envs while this wave finishes the reward.
         // This wave's drone-state stores are complete first (the cow waves overwrite reset drones).
-        if (envl) ei[I_RESET * G + g] = rs;
+        if (envw) ei[I_RESET * G + g] = rs;
         // the next episode's NUM_DRONES draw (BaseAviary.py:307), once: reset_scalars takes it from here.  (Drawn on
         // every env lane ahead of the cow items' hand-off instead, measured: no gain, profiles/r03/n/ab_draw.log.)
         int n_next = 0;
         if (envl && rs) n_next = p.reset_n ? p.reset_n[e] : reset_draw_n(p, f_episode, p.env_off + e);
-        if (envl && rs) ei[I_NEWN * G + g] = n_next;
-        const unsigned long long rbal = __ballot(rs != 0);
-        if (rs) ei[RS_LIST + __popcll(rbal & ((1ull << g) - 1ull))] = g;
+        if (envw && rs) ei[I_NEWN * G + g] = n_next;
+        const unsigned long long rbal = __ballot(envw && rs != 0);
+        if (envw && rs) ei[RS_LIST + __popcll(rbal & ((1ull << tid) - 1ull))] = g;   // (writers in env order)
         if (tid == 0) ei[NR_AT] = __popcll(rbal);
         if (tid == 0) TS(27, (long long)clock64());
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -1485,11 +1541,14 @@ void k_step2(StepParams<R> p) {
                 R psp_i[NT ? NT : 12], scat_i[NT ? NT : 12];
                 CH_UNROLL for (int i = 0; i < N; ++i) {
                     const bool li = i < n;
-                    const R pa = S.pa[b0 + i], pb = S.pb[b0 + i];
+                    const int iq = i % NQ;
+                    const R pa = QUAD ? qpa[iq] : S.pa[b0 + i], pb = QUAD ? qpb[iq] : S.pb[b0 + i];
                     const bool ua = li && (p.compat || pa < R(INFINITY)), ub = li && (p.compat || pb < R(INFINITY));
-                    sp_complex += ua ? S.ca[b0 + i] : R(0); sp_simple += ua ? S.sa[b0 + i] : R(0);
-                    sp_complex += ub ? S.cb[b0 + i] : R(0); sp_simple += ub ? S.sb[b0 + i] : R(0);
-                    psp_i[i] = S.psp[b0 + i]; scat_i[i] = S.scat[b0 + i];
+                    sp_complex += ua ? (QUAD ? qca[iq] : S.ca[b0 + i]) : R(0);
+                    sp_simple += ua ? (QUAD ? qsa[iq] : S.sa[b0 + i]) : R(0);
+                    sp_complex += ub ? (QUAD ? qcb[iq] : S.cb[b0 + i]) : R(0);
+                    sp_simple += ub ? (QUAD ? qsb[iq] : S.sb[b0 + i]) : R(0);
+                    psp_i[i] = QUAD ? qps[iq] : S.psp[b0 + i]; scat_i[i] = QUAD ? qsc[iq] : S.scat[b0 + i];
                 }
                 const R n2 = R(n * 2.0), nn = R(n);
                 sp_complex = divc(sp_complex, n2); sp_simple = divc(sp_simple, n2);
@@ -1505,8 +1564,10 @@ void k_step2(StepParams<R> p) {
                 R tot = 0;
                 CH_UNROLL for (int i = 0; i < N; ++i) tot += i < n ? rg + R(0.5) * ((psp_i[i] - msp) + (scat_i[i] - mcat)) : R(0);
                 R rew = divc(tot, nn);
-                CH_ST(&p.reward[e], (float)rew);
-                p.term[e] = te2; p.trunc[e] = tr;
+                if (envw) {
+                    CH_ST(&p.reward[e], (float)rew);
+                    p.term[e] = te2; p.trunc[e] = tr;
+                }
                 ret = (double)rew;
                 n_term = te2; n_trunc = tr; n_nan = rew != rew;
             }
@@ -1526,7 +1587,7 @@ void k_step2(StepParams<R> p) {
             o[kMetricCurLen] += 1;
             if (done) {
                 // SB3 Monitor's episode record (its reward sum and length) for the env that ends here
-                if (p.episode_stats) {
+                if (p.episode_stats && envw) {
                     CH_ST(&p.episode_stats[2 * (long long)e], o[kMetricCurReturn]);
                     CH_ST(&p.episode_stats[2 * (long long)e + 1], o[kMetricCurLen]);
                 }
@@ -1537,24 +1598,25 @@ void k_step2(StepParams<R> p) {
                 o[kMetricCurLen] = 0;
             }
 #pragma unroll
-            for (int r = 0; r < kMetricRows; ++r) CH_STS(&p.metrics[r * E + e], o[r]);
+            for (int r = 0; r < kMetricRows; ++r)
+                if (envw) CH_STS(&p.metrics[r * E + e], o[r]);
             if (g == 0) TS(28, (long long)clock64());
-            if (p.reset_happened) p.reset_happened[e] = rs;
+            if (p.reset_happened && envw) p.reset_happened[e] = rs;
             // SB3 auto-reset: the new episode's scalars (the cow waves rebuild its bodies and observation)
             if (rs) reset_scalars(p, e, f_n, f_sc, f_scA, f_spawn, f_episode, f_active, f_hp, f_prev, f_clock, n_next);
-            if (p.agent_active)
+            if (p.agent_active && envw)
                 for (int i = 0; i < N; ++i) p.agent_active[(long long)e * N + i] = (f_active >> i) & 1;
-        } else if (envl && p.reset_happened) {
+        } else if (envw && p.reset_happened) {
             p.reset_happened[e] = 0;
         }
         if (tid == 0) TS(7, (long long)clock64());
         // ---- env scalars back to HBM from the env lanes' registers (nothing after this step reads them)
-        if (tid < Gv) {
-            const int e = e0 + tid;
+        if (QUAD ? envw : tid < Gv) {
+            const int e = e0 + (QUAD ? dg : tid);
             CH_STS(&p.envi[0 * E + e], f_n); CH_STS(&p.envi[1 * E + e], f_sc); CH_STS(&p.envi[2 * E + e], f_scA);
             CH_STS(&p.envi[3 * E + e], f_hp); CH_STS(&p.envi[4 * E + e], f_level); CH_STS(&p.envi[5 * E + e], f_tally);
             CH_STS(&p.envi[6 * E + e], f_spawn); CH_STS(&p.envi[7 * E + e], f_active); CH_STS(&p.envi[8 * E + e], f_episode);
-            CH_STS(&p.envi[9 * E + e], stepi_env + 1);   // ch_step calls on this env
+            CH_STS(&p.envi[9 * E + e], (QUAD ? stepi : stepi_env) + 1);   // ch_step calls on this env
             CH_STS(&p.envr[0 * E + e], R(f_prev)); CH_STS(&p.envr[1 * E + e], f_clock);
             if constexpr (MIX) CH_STS(&p.prev64[e], f_prev);
             // this step wrote the env's Euler cache and, unless obs were masked off, its whole obs block
