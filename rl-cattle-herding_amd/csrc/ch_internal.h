@@ -114,8 +114,7 @@ struct V2Layout {
     size_t slot;   // W > 0: reals per wave slot
     size_t off[NOFF + 1];
     static __host__ __device__ size_t al(size_t x) { return (x + 15) & ~size_t(15); }
-    __host__ __device__ __attribute__((always_inline)) V2Layout(int G_, int N_, int M_, int P_, int mode, int rb, int W_ = 0,
-                                                              bool sep_ = false)
+    __host__ __device__ V2Layout(int G_, int N_, int M_, int P_, int mode, int rb, int W_ = 0, bool sep_ = false)
         : G(G_), N(N_), M(M_), P(P_), W(W_), sep(W_ == 0 && sep_) {
         rows = mode == CH_MODE_CTDE ? 12 : N;
         slot = 3 * (size_t)P > 6 * (size_t)M * N ? 3 * (size_t)P : 6 * (size_t)M * N;

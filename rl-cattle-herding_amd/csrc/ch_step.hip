@@ -638,102 +638,6 @@ __device__ __forceinline__ void alpha_row_pw(V2Smem<R>& S, int M, int P, int g, 
     S.aux[u] = ux; S.auy[u] = uy;
 }
 
-// ---- PW2: two flocking envs per cow-wave pass (compile-time herd of M <= 32 cows) -----------------------------------
-// Lane h * 32 + j holds cow j of the pass's env h.  The candidate test of the cheap pass (|z|^2 <= 1.44 (1 + 1e-9),
-// z = q_hi - q_lo as the pair list orders it) runs per cow over every other cow of its env -- no LDS atomics, both
-// halves of the wave busy -- and gives the cow's whole neighbour mask.  The pairs (j, k > j) are queued in (j, k)
-// order at base_j (an exclusive scan of the upper-mask counts), the full evaluation writes the pair's table entry at
-// its queue position, and the rows (both envs at once) find the entry of neighbour k at base_j + rank of k in j's
-// upper mask (k > j) or base_k + rank of j in k's (k < j; read from k's packed mask word).  Two envs share the wave's
-// table slot (3 P reals) when their queues fit together, else the second waits for the first's rows.  The set of
-// pairs, each pair's terms and each row's neighbour order are those of the single-env path: bit-identical outputs.
-__device__ __forceinline__ unsigned long long pw2_word(unsigned mask, int base) {
-    return (unsigned long long)mask | ((unsigned long long)(unsigned)base << 32);
-}
-template <class R, int M>
-__device__ __forceinline__ unsigned alpha_mask_pw2(const V2Smem<R>& S, int g, int j) {
-    const R xj = S.cx[g * M + j], yj = S.cy[g * M + j];
-    unsigned mask = 0;
-#pragma unroll
-    for (int k = 0; k < M; ++k) {
-        const R xk = S.cx[g * M + k], yk = S.cy[g * M + k];
-        const bool up = k > j;
-        const R zx = up ? xk - xj : xj - xk, zy = up ? yk - yj : yj - yk;
-        mask |= (k != j && zx * zx + zy * zy <= R(kAlphaSupport2)) ? (1u << k) : 0u;
-    }
-    return mask;
-}
-__device__ __forceinline__ unsigned upper_bits(unsigned mask, int j) { return j >= 31 ? 0u : mask & ~((2u << j) - 1u); }
-// inclusive scan of x over the 32 lanes of each half wave
-__device__ __forceinline__ int scan32(int x) {
-#pragma unroll
-    for (int d = 1; d < 32; d <<= 1) {
-        const int y = __shfl_up(x, d, 32);
-        x += ((threadIdx.x & 31) >= d) ? y : 0;
-    }
-    return x;
-}
-// the alpha row of cow j of env g (neighbour mask `mask`, queue base `base`) from the wave's queue-indexed table
-template <class R, int M>
-__device__ __forceinline__ void alpha_row_pw2(V2Smem<R>& S, int P, int g, int j, unsigned mask, int base, const R* tb) {
-    const R C2A = R(2 * 1.7320508075688772);
-    const int u = g * M + j;
-    const unsigned upj = upper_bits(mask, j);
-    R gx = 0, gy = 0, cxx = 0, cyy = 0, ux = 0, uy = 0;
-    const R pjx = S.cvx[u], pjy = S.cvy[u];
-    // four neighbours per round, branch-free as in alpha_row_pw (an empty slot reads entry 0 / cow j, adds +0)
-    for (unsigned m = mask; m;) {
-        R t[4][5];
-        bool v[4], fwd[4];
-        int k4[4];
-        unsigned long long wk[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            v[r] = m != 0;
-            k4[r] = v[r] ? __ffs(m) - 1 : j;
-            m &= m - 1;
-            fwd[r] = j < k4[r];
-            wk[r] = (v[r] && !fwd[r]) ? S.nbm[g * M + k4[r]] : 0ull;
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int k = k4[r];
-            int q = 0;
-            if (v[r]) {
-                if (fwd[r]) q = base + __popc(upj & ((1u << k) - 1u));
-                else q = (int)(wk[r] >> 32) + __popc(upper_bits((unsigned)wk[r], k) & ((1u << j) - 1u));
-            }
-            t[r][0] = tb[q]; t[r][1] = tb[P + q]; t[r][2] = tb[2 * P + q];
-            t[r][3] = S.cvx[g * M + k]; t[r][4] = S.cvy[g * M + k];
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const R b = t[r][2], pkx = t[r][3], pky = t[r][4];
-            const R dvx = fwd[r] ? pkx - pjx : pjx - pkx, dvy = fwd[r] ? pky - pjy : pjy - pky;
-            const R tcx = b * dvx, tcy = b * dvy;
-            gx += v[r] ? (fwd[r] ? t[r][0] : -t[r][0]) : R(0); gy += v[r] ? (fwd[r] ? t[r][1] : -t[r][1]) : R(0);
-            cxx += v[r] ? (fwd[r] ? tcx : -tcx) : R(0); cyy += v[r] ? (fwd[r] ? tcy : -tcy) : R(0);
-        }
-    }
-    if (has_sensing_neighbour(S, M, g, j)) { ux = C2A * gx + C2A * cxx; uy = C2A * gy + C2A * cyy; }
-    S.aux[u] = ux; S.auy[u] = uy;
-}
-// the full evaluation of queue entries [q0, q0 + 64): entry = j | k << 6 | h << 12 (pair (j, k > j) of env gs[h])
-template <class R, int M>
-__device__ __forceinline__ void alpha_full_pw2(V2Smem<R>& S, int P, int gA, int gB, int q0, int qn, R* tb,
-                                               const uint16_t* qu) {
-    const R ra = sigma_norm_n(R(1.2)), da = ra;
-    const int q = q0 + (threadIdx.x & 63);
-    if (q >= qn) return;
-    const int e = qu[q], j = e & 63, k = (e >> 6) & 63, g = (e >> 12) ? gB : gA;
-    const int bi = g * M + j, bj = g * M + k;
-    const R zx = S.cx[bj] - S.cx[bi], zy = S.cy[bj] - S.cy[bi];
-    const R nrm = sqrt(zx * zx + zy * zy);
-    R gx = 0, gy = 0, cx = 0, cy = 0;
-    const R b = pair_terms_n(nrm, zx, zy, R(0), R(0), R(0), R(0), ra, da, gx, gy, cx, cy);
-    tb[q] = gx; tb[P + q] = gy; tb[2 * P + q] = b;
-}
-
 // the shepherd term of a drone closer than 1 m (mu < 1: the projected agent q_ik lies between cow and drone),
 // the general pair_terms evaluation.  Rare, so it is kept out of line: inlined at each of the unrolled drone
 // slots of shepherd_sum it would add ~1.2k instructions to the kernel's instruction-cache footprint.
@@ -1802,78 +1706,7 @@ void k_step2(StepParams<R> p) {
                 store_final(u);
             }
         };
-        // PW2 (compile-time herd of <= 32 cows; CH_NO_PW2 for the one-env-per-pass path): the pass's state -- envs gA
-        // and gB (-1: none), whether they share the table (both) or gB waits for gA's rows (phase 1 then 2) -- is
-        // wave-uniform; each lane keeps its cow's mask and queue base in registers
-#ifdef CH_NO_PW2
-        constexpr bool PW2 = false;
-#else
-        constexpr bool PW2 = PW && MT > 0 && MT <= 32;
-#endif
-        constexpr int MP = PW2 ? MT : 32;
-        int gA = -1, gB = -1, ph2 = 0, qnA2 = 0;
-        bool both2 = false;
-        unsigned msk2 = 0;
-        int base2 = 0;
-        const int h2 = (tid & 63) >> 5, j2 = tid & 31;
-        auto pw2_queue = [&](int h, int off) __attribute__((always_inline)) {   // lanes of half h: queue their upper pairs at off + base, pack the mask
-            if (h2 != h || j2 >= MP) return;
-            const int g = h ? gB : gA;
-            unsigned up = upper_bits(msk2, j2);
-            int qpos = off + base2;
-            S.nbm[g * MP + j2] = pw2_word(msk2, qpos);
-            for (; up; up &= up - 1) qu[qpos++] = (uint16_t)(j2 | ((__ffs(up) - 1) << 6) | (h << 12));
-        };
-        auto alpha_step2 = [&]() __attribute__((always_inline)) -> bool {
-            if (f_cur < 0) {
-                f_cur = grab(fl + C_PAIRS, 2, skip_now);
-                if (f_cur >= nf) return false;
-                CHUNK_T0;
-                gA = flist[f_cur];
-                gB = f_cur + 1 < nf ? flist[f_cur + 1] : -1;
-                const int gl = h2 ? gB : gA;
-                const bool vl = j2 < MP && gl >= 0;
-                msk2 = vl ? alpha_mask_pw2<R, MP>(S, gl, j2) : 0u;
-                const int cnt = vl ? __popc(upper_bits(msk2, j2)) : 0;
-                const int incl = scan32(cnt);
-                base2 = incl - cnt;
-                qnA2 = __builtin_amdgcn_readlane(incl, 31);
-                const int qnB = gB >= 0 ? __builtin_amdgcn_readlane(incl, 63) : 0;
-                both2 = gB >= 0 && qnA2 + qnB <= P;
-                pw2_queue(0, 0);
-                if (both2) pw2_queue(1, qnA2);
-                qn = both2 ? qnA2 + qnB : qnA2;
-                qd = 0; ph2 = 1;
-                wave_sync();   // the queue and the packed mask words
-                CHUNK_T1(0);
-                return true;
-            }
-            CHUNK_T0;
-            if (qd < qn) {
-                alpha_full_pw2<R, MP>(S, P, gA, gB, qd, qn, tb, qu);
-                qd += 64;
-            }
-            if (qd >= qn) {
-                wave_sync();   // every table entry of the pass
-                const bool rows = j2 < MP && (ph2 == 1 ? (h2 == 0 || both2) : h2 == 1);
-                if (rows) alpha_row_pw2<R, MP>(S, P, h2 ? gB : gA, j2, msk2, base2, tb);
-                wave_sync();   // the slot is free again
-                if (ph2 == 1 && gB >= 0 && !both2) {   // gB's queue now, in the freed slot
-                    pw2_queue(1, 0);
-                    qn = __builtin_amdgcn_readlane(base2 + (int)__popc(upper_bits(msk2, j2)), 63);
-                    qd = 0; ph2 = 2;
-                    wave_sync();
-                } else {
-                    f_cur = -1;
-                }
-            }
-            CHUNK_T1(0);
-            return true;
-        };
-        auto alpha_step = [&]() __attribute__((always_inline)) -> bool {
-          if constexpr (PW2) {
-            return alpha_step2();
-          } else {
+        auto alpha_step = [&]() -> bool {
             if (f_cur < 0) {
                 f_cur = grab(fl + C_PAIRS, 1, skip_now);
                 ch = 0; qn = 0; qd = 0;
@@ -1902,7 +1735,6 @@ void k_step2(StepParams<R> p) {
             }
             CHUNK_T1(0);
             return true;
-          }
         };
         if constexpr (PW) {
             tb = S.tgx + (size_t)(tid / 64 - 1) * L.slot;
@@ -2013,7 +1845,7 @@ void k_step2(StepParams<R> p) {
         }
         // getEulerFromQuaternion of the new attitudes (BaseAviary.py:704-766): the own row's roll, pitch, yaw and
         // the next step's PID input (the Euler cache); late: after the reset list, skipping fast-reset envs
-        auto euler_pass = [&]() __attribute__((always_inline)) {
+        auto euler_pass = [&]() {
           // one item per (angle, drone): 3 G N items, so three waves share a workgroup's transcendentals
           for (;;) {
             const int b = grab(fl + C_EULER, 64, skip_post), t = b + lane;
