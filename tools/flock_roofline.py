@@ -52,11 +52,12 @@ def work(s, n_cfg):
     flop = (f * (P * FLOP["cheap_pair"] + inr * FLOP["alpha_pair"] + M * nd * FLOP["cow_drone_pair"] +
                  M * FLOP["cow"])).sum()
     byts = (f * (24 * M + 8 * nd)).sum()
-    return {"flocking_envs": int(flock.sum()), "alpha_pairs": int((f * inr).sum()), "pairs_per_flocking_env":
+    return {"flocking_envs": int(flock.sum()), "alpha_pairs": int((f * inr).sum()),
+            "cow_drone_pairs": int((f * M * nd).sum()), "cheap_pairs": int(f.sum() * P), "pairs_per_flocking_env":
             float(inr[flock].mean()) if flock.any() else 0.0, "flop": float(flop), "bytes": float(byts)}
 
 
-def measure(mode, E, n, m, launches, warm):
+def measure(mode, E, n, m, launches, warm, reps=5):
     import torch
     from cattleherd import _lib
     from cattleherd.env import HerdBatch
@@ -67,21 +68,23 @@ def measure(mode, E, n, m, launches, warm):
     torch.cuda.synchronize()
     s0 = b.get_state()
     L = _lib.lib()
-    res = {}
-    for mask in (0, 13, 15):
-        # back-to-back launches from the same state, one event pair around them
-        b.set_state(s0)
-        L.ch__set_phase_mask(b.handle, ctypes.c_int32(mask))
-        b.step(random_actions=True, autoreset=True, terminal_obs=False)   # (rewrites the obs blocks in full)
-        b.set_state(s0)
-        s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        torch.cuda.synchronize()
-        s_ev.record()
-        for _ in range(launches):
-            b.step(random_actions=True, autoreset=True, terminal_obs=False)
-        e_ev.record()
-        torch.cuda.synchronize()
-        res[mask] = s_ev.elapsed_time(e_ev) * 1000.0 / launches
+    res = {0: [], 13: [], 15: []}
+    # masks interleaved over `reps` rounds, each round back-to-back launches from the same state under one event
+    # pair; the median per mask (one slow round -- a clock ramp, a neighbour's job -- does not move the difference)
+    for _ in range(reps):
+        for mask in (0, 13, 15):
+            b.set_state(s0)
+            L.ch__set_phase_mask(b.handle, ctypes.c_int32(mask))
+            b.step(random_actions=True, autoreset=True, terminal_obs=False)   # (rewrites the obs blocks in full)
+            b.set_state(s0)
+            s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            s_ev.record()
+            for _ in range(launches):
+                b.step(random_actions=True, autoreset=True, terminal_obs=False)
+            e_ev.record()
+            torch.cuda.synchronize()
+            res[mask].append(s_ev.elapsed_time(e_ev) * 1000.0 / launches)
     # the work of the same launches, counted from the state each one starts from (the sequence is deterministic:
     # Philox draws keyed by the env state)
     b.set_state(s0)
@@ -93,7 +96,8 @@ def measure(mode, E, n, m, launches, warm):
         b.step(random_actions=True, autoreset=True, terminal_obs=False)
     L.ch__set_phase_mask(b.handle, ctypes.c_int32(0))
     b.close()
-    res = {k: (v, None) for k, v in res.items()}
+    spread = {k: [float(min(v)), float(max(v))] for k, v in res.items()}
+    res = {k: (float(np.median(v)), None) for k, v in res.items()}
     flock_us = res[13][0] - res[15][0]
     flop = float(np.mean([w["flop"] for w in ws]))
     byts = float(np.mean([w["bytes"] for w in ws]))
@@ -101,7 +105,11 @@ def measure(mode, E, n, m, launches, warm):
     gbs = byts / (flock_us * 1e-6) / 1e9
     return {"mode": mode, "envs": E, "drones": n, "cattle": m, "launches": launches,
             "full_step_us": res[0][0], "flock_only_us": res[13][0], "skeleton_us": res[15][0], "flock_phase_us": flock_us,
+            "min_max_us": {"full": spread[0], "flock_only": spread[13], "skeleton": spread[15]}, "reps": reps,
             "flocking_envs_per_launch": float(np.mean([w["flocking_envs"] for w in ws])),
+            "alpha_pairs_per_launch": float(np.mean([w["alpha_pairs"] for w in ws])),
+            "cow_drone_pairs_per_launch": float(np.mean([w["cow_drone_pairs"] for w in ws])),
+            "cheap_pairs_per_launch": float(np.mean([w["cheap_pairs"] for w in ws])),
             "alpha_pairs_per_flocking_env": float(np.mean([w["pairs_per_flocking_env"] for w in ws])),
             "useful_flop_per_launch": flop, "achieved_tflops": tflops, "frac_of_fp64_peak": tflops / PEAK_TFLOPS,
             "flock_bytes_per_launch": byts, "achieved_gbs": gbs, "frac_of_hbm": gbs / HBM_GBS,
@@ -125,7 +133,8 @@ def main():
         recs.append(r)
     out = {"code_object": code_object_hash(), "records": recs, "flop_model": FLOP, "peak_tflops": PEAK_TFLOPS,
            "note": "flock phase = launch time under phase mask 13 (flock only) minus mask 15 (skeleton), per launch, "
-                   "from one burnt-in state; useful FLOP counted on the host from the state each launch starts from "
+                   "from one burnt-in state, median of `reps` interleaved rounds (flock_only_us is the masked launch "
+                   "itself, an upper bound on the phase); useful FLOP counted on the host from the state each launch starts from "
                    "(tools/flock_roofline.py docstring); peak = fp64 vector FMA rate; ridge 9.8 FLOP/B; the flock carries "
                    "~16.5 FLOP/B, so 40 % of HBM would need ~2/3 of the fp64 FMA peak in useful FLOP"}
     os.makedirs(a.out, exist_ok=True)
