@@ -153,6 +153,9 @@ def policy_rollout(b, n, steps, warmup):
     # the packed actor-critic reads the observation once, but each workgroup still streams both heads' weights
     # for its 16 rows, which is what the forward waits on: measured slower, reported beside it
     out["ppo_rollout_fused_nets"] = ppo_rollout(b, d, fused=True)
+    # the actor forward in the step kernel's workgroups (k_step2_actor, ch_rollout_collect path bit 2), the critic
+    # alone after it
+    out["ppo_rollout_fused_step"] = ppo_rollout(b, d, fused_step=True)
     return out
 
 
@@ -168,7 +171,7 @@ def burn_in(b, steps=PPO_BURN_IN):
         b.step(None, random_actions=True, autoreset=True, terminal_obs=False)
 
 
-def ppo_rollout(b, d, T=32, fused=False):
+def ppo_rollout(b, d, T=32, fused=False, fused_step=False):
     """SB3 collect_rollouts on the device (cattleherd.rollout): per step the actor and critic forwards (fused=True:
     one launch of the two heads packed as one net, DevicePolicy.sb3_actor_critic, bit-identical to the separate
     nets), Gaussian sample / log-prob / buffer store (with the previous step's reward bootstrap), env step with
@@ -183,16 +186,26 @@ def ppo_rollout(b, d, T=32, fused=False):
     nets = (DevicePolicy.sb3_actor_critic(sd), None) if fused else (actor, critic)
     log_std = torch.full((actor.dims[-1],), -1.0, device=b.device)   # log_std_init (CTDECattleHerder.py:122)
     rb = DeviceRolloutBuffer(b, T, act_dim=actor.dims[-1])
+    import ctypes
+    from cattleherd import _lib
+    L = _lib.lib()
+    L.ch__rollout_fused_steps.restype = ctypes.c_int64
+    L.ch__set_rollout_path(b.handle, ctypes.c_int32(4 if fused_step else 8))
     burn_in(b)
     rb.collect(*nets, log_std, seed=1)
     torch.cuda.synchronize()
+    f0 = L.ch__rollout_fused_steps(b.handle)
     t0 = time.perf_counter()
     rb.collect(*nets, log_std, seed=2)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    nf = L.ch__rollout_fused_steps(b.handle) - f0
+    L.ch__set_rollout_path(b.handle, ctypes.c_int32(0))
     out = {"env_steps_per_s": b.n_envs * T / dt, "ms_per_step": dt / T * 1000.0, "n_steps": T,
            "burn_in": PPO_BURN_IN,
-           "policy": "actor + critic fused (one forward per step)" if fused else "actor and critic separately",
+           "policy": ("actor + critic fused (one forward per step)" if fused else "actor and critic separately") +
+                     (", actor forward in the step kernel (k_step2_actor)" if fused_step else ""),
+           "fused_steps": int(nf),
            "buffer_GB": sum(t.numel() * 4 for t in (rb.obs, rb.actions)) / 1e9}
     del rb
     return out

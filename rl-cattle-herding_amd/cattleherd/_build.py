@@ -12,7 +12,7 @@ CSRC = os.path.join(ROOT, "csrc")
 BUILD = os.path.join(ROOT, "build")
 LIB = os.path.join(PKG, "libcattleherd.so")
 SOURCES = ["ch_kernels.hip", "ch_step.hip", "ch_policy.hip", "ch_aux.hip", "ch_api.cpp"]
-HEADERS = ["ch_device.h", "ch_internal.h", "ch_common.h", "ch_spawn_table.inc"]
+HEADERS = ["ch_device.h", "ch_internal.h", "ch_common.h", "ch_spawn_table.inc", "ch_mlp2_dev.h", "ch_rollout_dev.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("CH_OFFLOAD_ARCH", "gfx950")
 # fp-contract off: the fp64 path keeps the reference's rounding (no fused multiply-adds), so it

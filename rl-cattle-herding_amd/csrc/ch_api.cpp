@@ -74,8 +74,10 @@ struct ch_handle {
     float* tv_val = nullptr;
     size_t tv_obs_n = 0, tv_val_n = 0;
     // ch_rollout_collect's path (diagnostics / tests, ch__set_rollout_path): bit 0 copy every step's observation into
-    // the buffer instead of stepping into its slots, bit 1 the stand-alone store kernel instead of the forward epilogues
+    // the buffer instead of stepping into its slots, bit 1 the stand-alone store kernel instead of the forward epilogues,
+    // bit 2 the actor forward fused into the step kernel (k_step2_actor, where the geometry takes it), bit 3 never fused
     int rollout_path = 0;
+    long long fused_steps = 0;   // fused steps launched by ch_rollout_collect (ch__rollout_fused_steps)
     // ch_outputs_to_host's device staging of the envs that auto-reset (allocated on first use): count, indices,
     // episode statistics, terminal observation blocks; and the pinned host copy of the count
     long long* st_count = nullptr;
@@ -338,7 +340,8 @@ int ch_create(const ch_config* c, int64_t n_envs, int32_t device, ch_handle** ou
     {   // ch_rollout_collect's path: the environment's choice, ch__set_rollout_path overrides it per handle
         const char* v = getenv("CH_ROLLOUT_COPY");
         const char* k = getenv("CH_ROLLOUT_STORE_KERNEL");
-        h->rollout_path = ((v && v[0] == '1') ? 1 : 0) | ((k && k[0] == '1') ? 2 : 0);
+        const char* f = getenv("CH_FUSED_ACTOR");
+        h->rollout_path = ((v && v[0] == '1') ? 1 : 0) | ((k && k[0] == '1') ? 2 : 0) | ((f && f[0] == '1') ? 4 : 0);
     }
 
     auto cleanup = [&](int code) { free_all(h); std::string m = h->err; delete h; g_create_err = m; return code; };
@@ -587,6 +590,28 @@ int ch_reset_with(ch_handle* h, const uint8_t* mask_dev, const int32_t* num_dron
     return mask_dev ? CH_OK : clear_error_word(h, st, "ch_reset_with");   // as ch_reset
 }
 
+extern "C++" template <class P>
+static void fill_step(const ch_handle* h, const ch_step_io* io, P& p) {
+    p.actions = io->actions; p.actions_out = io->actions_out; p.obs = io->obs; p.reward = io->reward;
+    p.term = io->terminated; p.trunc = io->truncated; p.terminal_obs = io->terminal_obs;
+    p.agent_active = io->agent_active; p.reset_happened = io->reset_happened; p.flags = io->flags;
+    p.episode_stats = io->episode_stats;
+    p.obs_full = io->obs != h->obs_zero_ptr;
+}
+
+// ch_rollout_collect's fused step (launch_step_v2_actor): the step of `io` with the actor forward `fa` on the
+// observations it writes (fa.x == io->obs) and the sampling epilogue `ro`.  launch = false: hipSuccess iff the handle
+// and the net fit the fused kernel (nothing launched).
+static hipError_t step_actor(ch_handle* h, const ch_step_io* io, hipStream_t st, const MlpArgs& fa, const RolloutArgs& ro,
+                             bool launch) {
+    if (h->kernel != 2 || h->rsize != sizeof(double) || h->phase_mask) return hipErrorNotSupported;
+    StepParams<double> p = params<double>(h);
+    fill_step(h, io, p);
+    const hipError_t e = launch_step_v2_actor(p, h->block, h->lds, st, fa, ro, launch);
+    if (e == hipSuccess && launch) { h->obs_zero_ptr = io->obs; ++h->fused_steps; }
+    return e;
+}
+
 int ch_step(ch_handle* h, const ch_step_io* io, void* stream) {
     if (!h) return fail(nullptr, CH_ERR_INVALID, "ch_step: NULL handle");
     if (!io) return fail(h, CH_ERR_INVALID, "ch_step: io is NULL");
@@ -602,13 +627,7 @@ int ch_step(ch_handle* h, const ch_step_io* io, void* stream) {
     HIP_TRY(h, hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
     hipError_t e;
-    auto fill = [&](auto& p) {
-        p.actions = io->actions; p.actions_out = io->actions_out; p.obs = io->obs; p.reward = io->reward;
-        p.term = io->terminated; p.trunc = io->truncated; p.terminal_obs = io->terminal_obs;
-        p.agent_active = io->agent_active; p.reset_happened = io->reset_happened; p.flags = io->flags;
-        p.episode_stats = io->episode_stats;
-        p.obs_full = io->obs != h->obs_zero_ptr;
-    };
+    auto fill = [&](auto& p) { fill_step(h, io, p); };
     if (h->rsize == sizeof(double)) {
         StepParams<double> p = params<double>(h);
         fill(p);
@@ -771,12 +790,16 @@ extern "C" int ch__set_mlp_tstamp(long long* dev) {
 }
 
 /* Internal (tests / diagnostics): ch_rollout_collect's path, bit 0 copy each step's observation into the buffer
- * (CH_ROLLOUT_COPY=1), bit 1 the stand-alone store kernel instead of the forward epilogues (CH_ROLLOUT_STORE_KERNEL=1). */
+ * (CH_ROLLOUT_COPY=1), bit 1 the stand-alone store kernel instead of the forward epilogues (CH_ROLLOUT_STORE_KERNEL=1),
+ * bit 2 the actor forward fused into the step (CH_FUSED_ACTOR=1), bit 3 never fused. */
 int ch__set_rollout_path(ch_handle* h, int32_t bits) {
-    if (!h || bits < 0 || bits > 3) return CH_ERR_INVALID;
+    if (!h || bits < 0 || bits > 15) return CH_ERR_INVALID;
     h->rollout_path = bits;
     return CH_OK;
 }
+
+/* Internal (tests): steps ch_rollout_collect has launched as the fused step + actor kernel on this handle. */
+int64_t ch__rollout_fused_steps(const ch_handle* h) { return h ? (int64_t)h->fused_steps : -1; }
 
 int ch__set_phase_mask(ch_handle* h, int32_t mask) {
     if (!h) return CH_ERR_INVALID;
@@ -1078,16 +1101,31 @@ int ch_rollout_collect(ch_handle* h, const ch_rollout* rb, const ch_rollout_io* 
         // Two launches per step: the actor and critic forwards with the store folded into their epilogues (the
         // actor's samples its actions, log-probabilities and env actions; the critic's writes the values, the
         // previous step's post and the episode starts, and at t = 0 copies obs[0]), then the step.
+        // With the fused step (rollout_path bit 2: CH_FUSED_ACTOR=1 or ch__set_rollout_path; bit 3 forbids it) the
+        // actor forward of step t + 1 runs in the step kernel of step t, in the workgroup that wrote those
+        // observations (k_step2_actor), and the critic goes out alone: the same work in the same stream order.
         const int roles[2] = {kRoleSample, kRoleValue};
+        const bool fuse = (h->rollout_path & 4) && !(h->rollout_path & 8) &&
+                          step_actor(h, &s, st, segs[0], a, false) == hipSuccess;
         RolloutArgs ro = a;
         for (int32_t t = 0; t < rb->n_steps; ++t) {
             segs[0].x = segs[1].x = obs_at(t);
             ro.t = t;
             ro.copy_obs = t == 0 || copy_each;
-            HIP_TRY(h, launch_mlp_multi(segs, 2, st, roles, &ro));
+            if (fuse && t > 0) HIP_TRY(h, launch_mlp_multi(&segs[1], 1, st, &roles[1], &ro));   // the critic
+            else HIP_TRY(h, launch_mlp_multi(segs, 2, st, roles, &ro));
             if (bootstrap_truncated && t > 0 && t % kTvEvery == 0) HIP_TRY(h, flush());
             s.obs = (t + 1 < rb->n_steps && !copy_each) ? rb->obs + (size_t)(t + 1) * slot : sio->obs;
-            if ((rc = ch_step(h, &s, stream))) return rc;
+            if (fuse && t + 1 < rb->n_steps) {
+                MlpArgs fa = segs[0];
+                fa.x = obs_at(t + 1);   // = s.obs
+                RolloutArgs rn = ro;
+                rn.t = t + 1;
+                const hipError_t e = step_actor(h, &s, st, fa, rn, true);
+                if (e != hipSuccess) return fail(h, CH_ERR_DEVICE, std::string("ch_rollout_collect fused step: ") + hipGetErrorString(e));
+            } else if ((rc = ch_step(h, &s, stream))) {
+                return rc;
+            }
         }
         // the last step's post (and queue) and flush, V(obs after the last step), GAE without a post of its own
         RolloutArgs pa = a;

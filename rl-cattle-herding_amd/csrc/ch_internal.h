@@ -256,6 +256,15 @@ template <class R> hipError_t launch_reset(const StepParams<R>& p, int team, hip
 // step captured into a HIP graph needs no host-side setup)
 template <class R> hipError_t launch_step_v2(const StepParams<R>& p, int block, size_t lds, hipStream_t st,
                                              bool launch = true);
+// ch_rollout_collect's fused step (k_step2_actor): the step of the CTDE 16-env x 4-drone x 16-cattle geometry (f64,
+// CH_V2_MAX_BLOCK threads) followed in each workgroup by the actor forward with the sampling epilogue on the 16
+// observation rows it wrote.  hipErrorNotSupported (nothing launched) when the handle's geometry or the net does not
+// fit it; launch = false checks only.
+template <class R> hipError_t launch_step_v2_actor(const StepParams<R>& p, int block, size_t lds, hipStream_t st,
+                                                   const MlpArgs& a, const RolloutArgs& ro, bool launch = true);
+// k_mlp2's one-tile shape for a fused forward (ch_policy.hip): LDS strides and dynamic bytes; false when the net does
+// not fit a 12-wave, one-column-tile-per-wave tile (layers <= 192 wide, first-layer live width <= 1152)
+bool mlp2_fused_tile(const MlpArgs& a, int& lda, int& ldh, size_t& bytes);
 // the v2 kernel runs with per-wave env tables (V2Layout W > 0) for herds above this size
 constexpr int kPwMinCattle = 17;
 

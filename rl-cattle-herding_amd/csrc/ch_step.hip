@@ -28,6 +28,7 @@
 #include "ch_common.h"
 #include "ch_device.h"
 #include "ch_internal.h"
+#include "ch_mlp2_dev.h"   // mlp2_body (k_step2_actor)
 
 namespace ch {
 
@@ -768,10 +769,8 @@ __device__ __forceinline__ void flock_combine(const StepParams<R>& p, V2Smem<R>&
 // geometry, launched when the step asks for them); without it the same geometry takes the drained-copy path for them
 // The f32 geometry-specialised kernels keep 4 waves per SIMD (<= 128 VGPRs): their f64 torque path (ch_device.h
 // drone_substep) would otherwise take them to 135 and 3 waves, one resident workgroup fewer per CU at large E.
-template <class R, int MODE, int GT, int NT, int MT, bool PHYS = false, bool PW = false, bool TOBS = false>
-__global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK)
-__attribute__((amdgpu_waves_per_eu((sizeof(R) == 4 && GT > 0 && !PW && !PHYS) ? 4 : 1)))
-void k_step2(StepParams<R> p) {
+template <class R, int MODE, int GT, int NT, int MT, bool PHYS, bool PW, bool TOBS>
+__device__ __forceinline__ void step2_body(const StepParams<R>& p) {
     extern __shared__ __align__(16) unsigned char smem[];
     constexpr bool marl = MODE == 1;
     // f32 mode: positions, centroids and the approach delta in f64 (StepParams::pos64); PT = their type
@@ -2147,6 +2146,38 @@ void k_step2(StepParams<R> p) {
 }
 
 template <class R, int MODE, int GT, int NT, int MT, bool PHYS = false, bool PW = false, bool TOBS = false>
+__global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK)
+__attribute__((amdgpu_waves_per_eu((sizeof(R) == 4 && GT > 0 && !PW && !PHYS) ? 4 : 1)))
+void k_step2(StepParams<R> p) {
+    step2_body<R, MODE, GT, NT, MT, PHYS, PW, TOBS>(p);
+}
+
+// The PPO collection step with the actor forward of the next step fused in (ch_rollout_collect, CH_FUSED_ACTOR /
+// ch__set_rollout_path bit 2): the workgroup steps its 16 envs, then -- once every wave has written its observation
+// stores -- runs the SB3 actor (k_mlp2's body, one 16-row tile, 12 waves of which 8 carry the 128-wide layers' column
+// tiles) on the 16 observation rows it has just written, with the sampling epilogue (kRoleSample: actions,
+// log-probabilities, the next step's env actions).  The rows are read back through L2 (the stores of this workgroup,
+// a workgroup-scope release before the barrier and an agent-scope acquire after it, which drops the CU's L1 lines),
+// the weights stream from L2 as in the separate launch; the LDS of the step is dead by then and the forward's tile
+// reuses it.  The critic and its value epilogue stay a separate launch.  Same arithmetic as the separate forward
+// (the K order of each output does not depend on the wave count): bit-identical rollouts.
+struct FusedActor {
+    MlpArgs a;
+    RolloutArgs ro;
+    int lda, ldh;
+};
+template <class R, int MODE, int GT, int NT, int MT, bool TOBS>
+__global__ __launch_bounds__(CH_V2_MAX_BLOCK)
+void k_step2_actor(StepParams<R> p, FusedActor f) {
+    step2_body<R, MODE, GT, NT, MT, false, false, TOBS>(p);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __builtin_amdgcn_s_setprio(0);   // (the drone wave's raised priority)
+    mlp2_body<CH_V2_MAX_BLOCK / 64, 1, 1>(f.a, (long long)blockIdx.x, f.lda, f.ldh, kRoleSample, f.ro);
+}
+
+template <class R, int MODE, int GT, int NT, int MT, bool PHYS = false, bool PW = false, bool TOBS = false>
 static hipError_t launch_v2_kernel(const StepParams<R>& p, int block, size_t lds, hipStream_t st, bool launch) {
     // opt-in to > 64 KiB of dynamic LDS, once per device (the attribute is per device context)
     static std::atomic<unsigned long long> attr_set{0};
@@ -2196,7 +2227,52 @@ hipError_t launch_step_v2(const StepParams<R>& p, int block, size_t lds, hipStre
     return launch_v2_kernel<R, 0, 0, 0, 0>(p, block, lds, st, launch);
 }
 
+template <class R, bool TOBS>
+static hipError_t launch_actor_kernel(const StepParams<R>& p, int block, size_t lds, hipStream_t st, const FusedActor& f,
+                                      bool launch) {
+    static std::atomic<unsigned long long> attr_set{0};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const unsigned long long bit = 1ull << (dev & 63);
+    if (!(attr_set.load(std::memory_order_relaxed) & bit)) {
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_step2_actor<R, 0, 16, 4, 16, TOBS>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        attr_set.fetch_or(bit, std::memory_order_relaxed);
+    }
+    if (!launch) return hipSuccess;
+    hipLaunchKernelGGL((k_step2_actor<R, 0, 16, 4, 16, TOBS>), dim3((p.E + 15) / 16), dim3(block), lds, st, p, f);
+    return hipGetLastError();
+}
+
+template <class R>
+hipError_t launch_step_v2_actor(const StepParams<R>& p, int block, size_t lds, hipStream_t st, const MlpArgs& a,
+                                const RolloutArgs& ro, bool launch) {
+    if constexpr (sizeof(R) != sizeof(double)) {
+        return hipErrorNotSupported;
+    } else {
+        if (p.physics != CH_PHYS_PYB || p.pw || p.mode != 0 || p.G != 16 || p.NC != 4 || p.M != 16 ||
+            block != CH_V2_MAX_BLOCK || a.rows != p.E)
+            return hipErrorNotSupported;
+        FusedActor f;
+        size_t mb = 0;
+        if (!mlp2_fused_tile(a, f.lda, f.ldh, mb)) return hipErrorNotSupported;
+        f.a = a;
+        f.a.tstamp = nullptr;
+        f.ro = ro;
+        const size_t l = lds > mb ? lds : mb;
+        if (l > 160 * 1024 - 256) return hipErrorNotSupported;   // (the forward's few static words beside it)
+        return p.terminal_obs ? launch_actor_kernel<R, true>(p, block, l, st, f, launch)
+                              : launch_actor_kernel<R, false>(p, block, l, st, f, launch);
+    }
+}
+
 template hipError_t launch_step_v2<double>(const StepParams<double>&, int, size_t, hipStream_t, bool);
+template hipError_t launch_step_v2_actor<double>(const StepParams<double>&, int, size_t, hipStream_t, const MlpArgs&,
+                                                 const RolloutArgs&, bool);
+template hipError_t launch_step_v2_actor<float>(const StepParams<float>&, int, size_t, hipStream_t, const MlpArgs&,
+                                                const RolloutArgs&, bool);
 template hipError_t launch_step_v2<float>(const StepParams<float>&, int, size_t, hipStream_t, bool);
 
 }  // namespace ch

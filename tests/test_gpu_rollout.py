@@ -135,6 +135,44 @@ def test_native_collect_equals_python_loop(T, path):
         assert torch.equal(bufs[0][k], bufs[1][k]), k
 
 
+@pytest.mark.parametrize("T", [6, 24])
+def test_fused_step_actor_is_bit_identical(T):
+    """ch_rollout_collect with the actor forward fused into the step kernel (k_step2_actor: configs[3]'s geometry,
+    4096 envs, the workgroup's 16 observation rows read back right after it wrote them) fills the same buffers as
+    the separate actor + critic launch, across auto-resets and the deferred truncation bootstrap's flush; the fused
+    kernel is the one that ran (T - 1 fused steps per collection)."""
+    import ctypes
+    import torch
+    from cattleherd import _lib
+    from cattleherd.env import HerdBatch
+    from cattleherd.policy import DevicePolicy
+    from cattleherd.rollout import DeviceRolloutBuffer
+    L = _lib.lib()
+    L.ch__rollout_fused_steps.restype = ctypes.c_int64
+    E, n, m = 4096, 4, 16
+    sc = 4800 - T // 2 + (np.arange(E) % T)
+    bufs = []
+    for path in (8, 4):
+        b = HerdBatch(E, n, m, mode="ctde", curriculum_level=2)
+        b.reset()
+        b.set_state({"step_counter": sc})
+        assert L.ch__set_rollout_path(b.handle, ctypes.c_int32(path)) == 0
+        actor = DevicePolicy(DevicePolicy.random_layers([12 * 86, 128, 128, 4 * n], seed=1), "tanh", None)
+        critic = DevicePolicy(DevicePolicy.random_layers([12 * 86, 128, 128, 1], seed=2), "tanh", None)
+        rb = DeviceRolloutBuffer(b, T)
+        log_std = torch.full((4 * n,), -1.0, device=b.device)
+        rb.collect(actor, critic, log_std, seed=9)
+        torch.cuda.synchronize()
+        assert L.ch__rollout_fused_steps(b.handle) == (T - 1 if path == 4 else 0)
+        bufs.append({k: getattr(rb, k).cpu() for k in ("obs", "actions", "rewards", "episode_starts", "values",
+                                                        "log_probs", "advantages", "returns")})
+        bufs[-1]["env_obs"] = b.obs.cpu()
+        assert rb.episode_starts[1:].sum() > 0
+        b.close()
+    for k in bufs[0]:
+        assert torch.equal(bufs[0][k], bufs[1][k]), k
+
+
 def test_fused_actor_critic_is_bit_identical():
     """The SB3 actor and critic packed as one net (layer 1 stacked, layers 2-3 block-diagonal; one forward per
     step reads the observation once): its two heads equal the separate nets' forwards bit for bit -- the
