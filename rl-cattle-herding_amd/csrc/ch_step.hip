@@ -2161,6 +2161,7 @@ void k_step2(StepParams<R> p) {
 // the weights stream from L2 as in the separate launch; the LDS of the step is dead by then and the forward's tile
 // reuses it.  The critic and its value epilogue stay a separate launch.  Same arithmetic as the separate forward
 // (the K order of each output does not depend on the wave count): bit-identical rollouts.
+constexpr int kFusedLdsMax = 160 * 1024 - 256;   // k_step2_actor's dynamic LDS cap
 struct FusedActor {
     MlpArgs a;
     RolloutArgs ro;
@@ -2236,9 +2237,10 @@ static hipError_t launch_actor_kernel(const StepParams<R>& p, int block, size_t 
     if (e != hipSuccess) return e;
     const unsigned long long bit = 1ull << (dev & 63);
     if (!(attr_set.load(std::memory_order_relaxed) & bit)) {
+        // (the forward's static words -- kmax, kany, the row slots -- sit beside the dynamic LDS)
         e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_step2_actor<R, 0, 16, 4, 16, TOBS>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return e;
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kFusedLdsMax);
+        if (e != hipSuccess) { (void)hipGetLastError(); return e; }
         attr_set.fetch_or(bit, std::memory_order_relaxed);
     }
     if (!launch) return hipSuccess;
@@ -2262,7 +2264,7 @@ hipError_t launch_step_v2_actor(const StepParams<R>& p, int block, size_t lds, h
         f.a.tstamp = nullptr;
         f.ro = ro;
         const size_t l = lds > mb ? lds : mb;
-        if (l > 160 * 1024 - 256) return hipErrorNotSupported;   // (the forward's few static words beside it)
+        if (l > (size_t)kFusedLdsMax) return hipErrorNotSupported;
         return p.terminal_obs ? launch_actor_kernel<R, true>(p, block, l, st, f, launch)
                               : launch_actor_kernel<R, false>(p, block, l, st, f, launch);
     }

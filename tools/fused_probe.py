@@ -24,6 +24,9 @@ def run(path, nets, T=6, E=4096, act_dim=16):
     b.reset()
     b.set_state({"step_counter": 4800 - T // 2 + (np.arange(E) % T)})
     assert L.ch__set_rollout_path(b.handle, ctypes.c_int32(path)) == 0
+    g, blk, lds, kv = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int32()
+    L.ch__geometry(b.handle, ctypes.byref(g), ctypes.byref(blk), ctypes.byref(lds), ctypes.byref(kv))
+    print(f"geometry G {g.value} block {blk.value} lds {lds.value} kernel {kv.value}", flush=True)
     rb = DeviceRolloutBuffer(b, T, act_dim=act_dim)
     log_std = torch.full((act_dim,), -1.0, device=b.device)
     try:
