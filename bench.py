@@ -171,12 +171,13 @@ def burn_in(b, steps=PPO_BURN_IN):
         b.step(None, random_actions=True, autoreset=True, terminal_obs=False)
 
 
-def ppo_rollout(b, d, T=32, fused=False, fused_step=False):
+def ppo_rollout(b, d, T=32, fused=False, fused_step=False, reps=5):
     """SB3 collect_rollouts on the device (cattleherd.rollout): per step the actor and critic forwards (fused=True:
     one launch of the two heads packed as one net, DevicePolicy.sb3_actor_critic, bit-identical to the separate
     nets), Gaussian sample / log-prob / buffer store (with the previous step's reward bootstrap), env step with
-    auto-reset and terminal obs, V(terminal obs); then GAE.  env-steps/s of one whole T-step collection (after
-    one untimed collection)."""
+    auto-reset and terminal obs, V(terminal obs); then GAE.  env-steps/s of one whole T-step collection (the median
+    of `reps`, after one untimed collection).  fused_step: the actor forward in the step kernel (k_step2_actor)."""
+    import numpy as np
     import torch
     from cattleherd.policy import DevicePolicy
     from cattleherd.rollout import DeviceRolloutBuffer
@@ -195,14 +196,17 @@ def ppo_rollout(b, d, T=32, fused=False, fused_step=False):
     rb.collect(*nets, log_std, seed=1)
     torch.cuda.synchronize()
     f0 = L.ch__rollout_fused_steps(b.handle)
-    t0 = time.perf_counter()
-    rb.collect(*nets, log_std, seed=2)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    nf = L.ch__rollout_fused_steps(b.handle) - f0
+    dts = []
+    for r in range(reps):   # the median of `reps` collections, each from where the previous one left the envs
+        t0 = time.perf_counter()
+        rb.collect(*nets, log_std, seed=2 + r)
+        torch.cuda.synchronize()
+        dts.append(time.perf_counter() - t0)
+    dt = float(np.median(dts))
+    nf = (L.ch__rollout_fused_steps(b.handle) - f0) // reps
     L.ch__set_rollout_path(b.handle, ctypes.c_int32(0))
     out = {"env_steps_per_s": b.n_envs * T / dt, "ms_per_step": dt / T * 1000.0, "n_steps": T,
-           "burn_in": PPO_BURN_IN,
+           "burn_in": PPO_BURN_IN, "reps": reps, "min_max_ms_per_step": [min(dts) / T * 1e3, max(dts) / T * 1e3],
            "policy": ("actor + critic fused (one forward per step)" if fused else "actor and critic separately") +
                      (", actor forward in the step kernel (k_step2_actor)" if fused_step else ""),
            "fused_steps": int(nf),
