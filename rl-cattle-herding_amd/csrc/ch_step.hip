@@ -2156,8 +2156,8 @@ void k_step2(StepParams<R> p) {
 // ch__set_rollout_path bit 2): the workgroup steps its 16 envs, then -- once every wave has written its observation
 // stores -- runs the SB3 actor (k_mlp2's body, one 16-row tile, 12 waves of which 8 carry the 128-wide layers' column
 // tiles) on the 16 observation rows it has just written, with the sampling epilogue (kRoleSample: actions,
-// log-probabilities, the next step's env actions).  The rows are read back through L2 (the stores of this workgroup,
-// a workgroup-scope release before the barrier and an agent-scope acquire after it, which drops the CU's L1 lines),
+// log-probabilities, the next step's env actions).  The rows are read back through the CU's caches (the stores of
+// this workgroup; a workgroup-scope release before the barrier, a workgroup-scope acquire after it),
 // the weights stream from L2 as in the separate launch; the LDS of the step is dead by then and the forward's tile
 // reuses it.  The critic and its value epilogue stay a separate launch.  Same arithmetic as the separate forward
 // (the K order of each output does not depend on the wave count): bit-identical rollouts.
@@ -2170,12 +2170,20 @@ struct FusedActor {
 template <class R, int MODE, int GT, int NT, int MT, bool TOBS>
 __global__ __launch_bounds__(CH_V2_MAX_BLOCK)
 void k_step2_actor(StepParams<R> p, FusedActor f) {
+    // diagnostics (ch__set_mlp_tstamp): wall clocks of the workgroup's start, barrier and end in slots 13-15
+    long long* ts = f.a.tstamp && threadIdx.x == 0 ? f.a.tstamp + (long long)blockIdx.x * 16 : nullptr;
+    if (ts) ts[13] = (long long)wall_clock64();
     step2_body<R, MODE, GT, NT, MT, false, false, TOBS>(p);
+    // workgroup scope both ways: the waves of a workgroup share the CU's vector L1, so the release's store-counter
+    // wait makes every observation store visible to the forward's loads after the barrier (an agent-scope acquire
+    // would also invalidate this XCD's L2 -- measured: the forward's first weight loads then waited ~17 us)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     __builtin_amdgcn_s_setprio(0);   // (the drone wave's raised priority)
+    if (ts) ts[14] = (long long)wall_clock64();
     mlp2_body<CH_V2_MAX_BLOCK / 64, 1, 1>(f.a, (long long)blockIdx.x, f.lda, f.ldh, kRoleSample, f.ro);
+    if (ts) ts[15] = (long long)wall_clock64();
 }
 
 template <class R, int MODE, int GT, int NT, int MT, bool PHYS = false, bool PW = false, bool TOBS = false>
@@ -2261,7 +2269,9 @@ hipError_t launch_step_v2_actor(const StepParams<R>& p, int block, size_t lds, h
         size_t mb = 0;
         if (!mlp2_fused_tile(a, f.lda, f.ldh, mb)) return hipErrorNotSupported;
         f.a = a;
-        f.a.tstamp = nullptr;
+        // (diagnostics, ch__set_mlp_tstamp: the forward's phase clocks in the buffer's second half, rows [grid, 2 grid),
+        // so that the separate launches of the same collection, which use the first, do not overwrite them)
+        f.a.tstamp = g_mlp_tstamp ? g_mlp_tstamp + 16LL * ((p.E + 15) / 16) : nullptr;
         f.ro = ro;
         const size_t l = lds > mb ? lds : mb;
         if (l > (size_t)kFusedLdsMax) return hipErrorNotSupported;
