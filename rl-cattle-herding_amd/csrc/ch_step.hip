@@ -173,7 +173,7 @@ struct V2Smem {
     const uint16_t* pl;                              // [P] unordered cow pairs, copied from p.pairs
     uint8_t *dflags, *herded, *md1, *md2;            // [G*N], [G*M], [G*N], [G*N]
     uint8_t* tdf;                                    // [G*M*N] shepherd term in range | predator in range << 1
-    uint8_t* hasnb;                                  // (unused: has_sensing_neighbour)
+    uint8_t* hasnb;                                  // PW: [G] int flags, flock-list env f's alpha rows are written
     unsigned long long* nbm;                         // PW: [G*M] neighbours k whose pair is inside the bump support
     uint16_t* queue;                                 // PW: [W][P] pairs of the slot's env inside the bump support
 
@@ -790,6 +790,13 @@ __device__ __forceinline__ void step2_body(const StepParams<R>& p) {
     // drone wave's quads (env g = lanes 4g..4g+3, the env's drones) with the per-drone terms in registers and
     // gathered by DPP quad broadcasts in drone order, instead of on 16 env lanes reading them back from LDS.
     // CH_NO_QUAD for the env-lane form.
+    // PW_READY (per-wave tables): per-env ready flags between the alpha rows and the shepherd / velocity pass instead of
+    // a cow-wave barrier (CH_NO_PW_READY for the barrier)
+#ifdef CH_NO_PW_READY
+    constexpr bool PW_READY = false;
+#else
+    constexpr bool PW_READY = PW;
+#endif
 #ifdef CH_NO_QUAD
     constexpr bool QUAD = false;
 #else
@@ -888,6 +895,7 @@ __device__ __forceinline__ void step2_body(const StepParams<R>& p) {
     }
     if (tid < Gv) stepi_env = p.envi[9 * E + e0 + tid];   // env lanes: the counter the write-back advances
     if (tid < kV2Flags) fl[tid] = 0;
+    if constexpr (PW) { if (tid < G) reinterpret_cast<int*>(S.hasnb)[tid] = 0; }   // per-env alpha-row ready flags
     lds_barrier();   // hand-off counters cleared before anyone signals
 
     if (tid < 64) {
@@ -1730,6 +1738,7 @@ __device__ __forceinline__ void step2_body(const StepParams<R>& p) {
                 wave_sync();   // every table entry of the env
                 for (int j = lane; j < M; j += 64) alpha_row_pw(S, M, P, g, j, tb);
                 wave_sync();   // the slot is free again
+                if constexpr (PW_READY) lds_signal(reinterpret_cast<int*>(S.hasnb) + f_cur);   // the env's rows are in
                 f_cur = -1;
             }
             CHUNK_T1(0);
@@ -1872,7 +1881,10 @@ __device__ __forceinline__ void step2_body(const StepParams<R>& p) {
         if constexpr (PW) {
             while (alpha_step()) {   // the rest of the alpha work (the current env first)
             }
-            cow_sync(fl + F_W, W1, false, p.err);   // every alpha row (aux, auy) is written
+            // PW_READY: no cow-wave barrier here -- each env's shepherd sums and velocity update wait only for that env's
+            // alpha rows (its ready flag), so the waves that run out of alpha work take the envs that are done while the
+            // last envs' alpha work finishes (the velocity update reads the env's own positions, velocities and rows only)
+            if constexpr (!PW_READY) cow_sync(fl + F_W, W1, false, p.err);   // every alpha row (aux, auy) is written
             if (ct == 0) TS(21, (long long)clock64());
             // shepherd / predator sums and the velocity update, one cow per lane with its drones' terms in
             // registers (shepherd_sum, drone order), 64 / M flocking envs per wave at a time
@@ -1880,6 +1892,9 @@ __device__ __forceinline__ void step2_body(const StepParams<R>& p) {
             for (;;) {
                 const int f0 = grab(fl + C_DELTA, per, skip_post);
                 if (f0 >= nf) break;
+                if constexpr (PW_READY) {
+                    for (int fi = 0; fi < per && f0 + fi < nf; ++fi) lds_wait(reinterpret_cast<int*>(S.hasnb) + f0 + fi, 1, p.err);
+                }
                 CHUNK_T0;
                 for (int q = lane; q < per * M; q += 64) {
                     const int fi = per > 1 ? qdiv(q, M, rM) : 0, j = q - fi * M, f = f0 + fi;
