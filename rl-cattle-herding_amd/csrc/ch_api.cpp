@@ -783,7 +783,9 @@ int ch__obs_invalidate(ch_handle* h, void* stream) {
     return CH_OK;
 }
 
-// diagnostics: k_mlp2 writes wave 0's phase clocks of every workgroup to dev[blockIdx][16] (NULL: off)
+// diagnostics: k_mlp2 writes wave 0's phase clocks of every workgroup to dev[blockIdx][16] (NULL: off); the fused
+// step + actor kernel (k_step2_actor) writes its forward's clocks and wall-clock slots 13-15 to rows [grid, 2 grid),
+// so a buffer for a collection on the fused path holds 2 x 16 x (E / 16) entries (tools/fused_probe.py trace)
 extern "C" int ch__set_mlp_tstamp(long long* dev) {
     g_mlp_tstamp = dev;
     return CH_OK;
