@@ -7,9 +7,9 @@ the oracle -- nothing from ``/root/reference``.
 The trace was written by ``evaluate_policy(model, test_env_nogui, n_eval_episodes=5)`` with a deterministic SB3
 policy (reference ``simulator/CTDECattleHerder.py:169-185``, ``utils/evaluation.py:73-94``): 3 drones, 16 cattle,
 drone and cattle xy position and velocity after every control step, real Bullet in the loop.  The policy that
-drove it is not among the shipped checkpoints: none of the 22 with a 3 x 86 input
-(``simulator/models/*/best_model.zip``, ``archive/*``, read with ``torch.load(weights_only=True)``) reproduces even
-the sign pattern of the first step's drone velocities.  So the actions are recovered instead:
+drove it is not among the shipped checkpoints: none of the 19 (of 82) with a 3 x 86 input reproduces even the sign
+pattern of the first step's drone velocities (``make_trace_policy_search.py`` -> ``trace_policy_search.json``,
+DESIGN.md §3).  So the actions are recovered instead:
 
 * ``seg0`` is the first evaluation episode of a fresh env -- drones at rest at (1.75 i, 0, 0.45), identity
   attitude, PID state zero (the controllers are created in the constructor and never reset,
