@@ -191,7 +191,10 @@ def ppo_rollout(b, d, T=32, fused=False, fused_step=False, reps=5):
     from cattleherd import _lib
     L = _lib.lib()
     L.ch__rollout_fused_steps.restype = ctypes.c_int64
-    L.ch__set_rollout_path(b.handle, ctypes.c_int32(4 if fused_step else 8))
+    # set or clear only the fused-actor bits (2: fused, 3: never fused); the copy / store-kernel bits the
+    # environment chose for this handle stay, and the original value is restored after the leg
+    path0 = L.ch__get_rollout_path(b.handle)
+    L.ch__set_rollout_path(b.handle, ctypes.c_int32((path0 & 3) | (4 if fused_step else 8)))
     burn_in(b)
     rb.collect(*nets, log_std, seed=1)
     torch.cuda.synchronize()
@@ -204,7 +207,7 @@ def ppo_rollout(b, d, T=32, fused=False, fused_step=False, reps=5):
         dts.append(time.perf_counter() - t0)
     dt = float(np.median(dts))
     nf = (L.ch__rollout_fused_steps(b.handle) - f0) // reps
-    L.ch__set_rollout_path(b.handle, ctypes.c_int32(0))
+    L.ch__set_rollout_path(b.handle, ctypes.c_int32(path0))
     out = {"env_steps_per_s": b.n_envs * T / dt, "ms_per_step": dt / T * 1000.0, "n_steps": T,
            "burn_in": PPO_BURN_IN, "reps": reps, "min_max_ms_per_step": [min(dts) / T * 1e3, max(dts) / T * 1e3],
            "policy": ("actor + critic fused (one forward per step)" if fused else "actor and critic separately") +

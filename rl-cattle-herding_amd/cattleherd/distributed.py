@@ -10,6 +10,7 @@ end-of-rollout metric vector (``ch_metrics``) — an all-reduce(sum) of a few do
 (backend "nccl") or gloo on CPU — plus the max-over-ranks wall time the bench reports.
 """
 import os
+import socket
 
 import numpy as np
 
@@ -69,7 +70,8 @@ def rank_device_info(use_gpu=True):
     """Which device this rank drives: rank, local rank, device index and, on a GPU, its PCI address and name.
     Without a GPU (the gloo launch check) the device slot is the LOCAL_RANK the rank would bind."""
     rank, world, local = world_info()
-    info = {"rank": rank, "local_rank": local, "device": local, "pci_bus_id": None, "name": None}
+    info = {"rank": rank, "local_rank": local, "device": local, "pci_bus_id": None, "name": None,
+            "host": socket.gethostname()}
     if use_gpu:
         import torch
         d = torch.cuda.current_device()
@@ -92,8 +94,9 @@ def gather_rank_info(info):
 
 def distinct_devices(infos):
     """True when no two ranks drive the same device: PCI addresses when known (a launcher that narrows each rank's
-    visible devices makes every rank's index 0), else (host, device index)."""
-    keys = [i["pci_bus_id"] if i.get("pci_bus_id") else ("slot", i["device"]) for i in infos]
+    visible devices makes every rank's index 0), else the device slot; either keyed by host, so ranks on two nodes
+    with the same PCI layout are distinct."""
+    keys = [(i.get("host"), i["pci_bus_id"] if i.get("pci_bus_id") else ("slot", i["device"])) for i in infos]
     return len(set(keys)) == len(keys)
 
 

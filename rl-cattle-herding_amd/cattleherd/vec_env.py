@@ -49,10 +49,9 @@ class CattleHerdVecEnv(_VecEnvBase):
             raise ValueError("obs_ring must be >= 2 (collect_rollouts keeps the previous step's observations)")
         self._host = self.batch.host_outputs(ring=int(obs_ring), ended=True)
         self._copy_obs = bool(copy_obs)
-        # _computeInfo's {"answer": 42} per env (CattleAviary.py), never mutated here: each step returns a new list of
-        # them with a new dict for every env that ended (terminal_observation, TimeLimit.truncated, episode), so infos a
-        # caller keeps do not change under later steps (SubprocVecEnv hands out fresh dicts too)
-        self._infos = [{"answer": 42} for _ in range(n_envs)]
+        # _computeInfo's {"answer": 42} per env (CattleAviary.py): every step builds a new dict for every env (the envs
+        # that ended also get terminal_observation, TimeLimit.truncated, episode), so infos a caller keeps or mutates do
+        # not change under later steps (SubprocVecEnv hands out fresh dicts too)
         if _VecEnvBase is not object:  # SB3 bookkeeping
             _VecEnvBase.__init__(self, n_envs, self.observation_space, self.action_space)
 
@@ -89,7 +88,7 @@ class CattleHerdVecEnv(_VecEnvBase):
         te_np = h["terminated"][:, 0].astype(bool)
         tr_np = h["truncated"][:, 0].astype(bool)
         dones = te_np | tr_np
-        infos = list(self._infos)
+        infos = [{"answer": 42} for _ in range(self.num_envs)]   # fresh dicts every step (SubprocVecEnv semantics)
         idx = h["ended_env"]
         if len(idx):
             # Monitor.step: the episode's summed float64 reward and length, kept on the device by the step kernel

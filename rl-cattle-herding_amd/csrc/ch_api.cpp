@@ -800,6 +800,9 @@ int ch__set_rollout_path(ch_handle* h, int32_t bits) {
     return CH_OK;
 }
 
+/* Internal: the handle's current rollout path bits (ch__set_rollout_path), or -1 for a null handle. */
+int ch__get_rollout_path(const ch_handle* h) { return h ? h->rollout_path : -1; }
+
 /* Internal (tests): steps ch_rollout_collect has launched as the fused step + actor kernel on this handle. */
 int64_t ch__rollout_fused_steps(const ch_handle* h) { return h ? (int64_t)h->fused_steps : -1; }
 

@@ -1,0 +1,3 @@
+# Overlay: modules this package does not define (e.g. control/, simulator/, utils/flockUtils.py) resolve
+# from a reference checkout later on sys.path; this package's own modules come first.
+__path__ = __import__("pkgutil").extend_path(__path__, __name__)

@@ -123,6 +123,12 @@ def test_vec_env_outputs_kept_across_steps(patched):
                     assert np.array_equal(d[k], ds[k]) if k == "terminal_observation" else d[k] == ds[k]
             if copy_obs or t >= len(kept) - 2:   # ring of 3: this step and the two before it
                 assert np.array_equal(obs, snap), t
+        # no info dict is shared between envs or steps: mutating one leaks nowhere
+        ids = [id(d) for _, _, infos, _ in kept for d in infos]
+        assert len(set(ids)) == len(ids)
+        kept[0][2][0]["mutated"] = True
+        _, _, _, infos = venv.step(rng.uniform(-1, 1, (4, 4, 4)).astype(np.float32))
+        assert all("mutated" not in d for d in infos)
     with pytest.raises(ValueError):
         ve.CattleHerdVecEnv(4, num_drones=4, num_cattle=16, obs_ring=1)
 

@@ -121,6 +121,11 @@ def test_distinct_devices_rule():
     assert not D.distinct_devices([a, dict(b, pci_bus_id="0000:05:00")])
     c, d = dict(a, pci_bus_id=None), dict(b, pci_bus_id=None, device=0)
     assert not D.distinct_devices([c, d]) and D.distinct_devices([c, dict(d, device=1)])
+    # two nodes with the same PCI layout (or the same LOCAL_RANK slots) are distinct devices
+    h0, h1 = dict(a, host="node0"), dict(a, rank=1, host="node1")
+    assert D.distinct_devices([h0, h1]) and not D.distinct_devices([h0, dict(h1, host="node0")])
+    assert D.distinct_devices([dict(c, host="node0"), dict(d, host="node1")])
+    assert D.rank_device_info(use_gpu=False)["host"]
 
 
 def test_bench_world_size_mismatch_fails():
