@@ -32,6 +32,9 @@ WORKLOADS = {
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_F32_PEAK_TFLOPS = 157.3   # f32-input MFMA: 64 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz (dense)
 POLICY_GOLDEN = os.path.join(ROOT, "tests", "golden", "policy_ctde_v16_6.npz")
+# the reference's trained RLlib PPO weights (simulator/policy_weights.pkl, read data-only into this fixture by
+# tests/golden/make_policy_marl_golden.py)
+POLICY_MARL_GOLDEN = os.path.join(ROOT, "tests", "golden", "policy_marl_rllib.npz")
 PROFILES = os.path.join(ROOT, "profiles")
 
 
@@ -218,18 +221,64 @@ def ppo_rollout(b, d, T=32, fused=False, fused_step=False, reps=5):
     return out
 
 
+def ppo_train_iteration(b, T=32, batch_size=64, n_envs_ref=24):
+    """configs[2] end to end: one PPO training iteration of the CTDE driver (CTDECattleHerder.py:107-127) on the device
+    -- the collection (cattleherd.rollout, T steps of every env) then the update (cattleherd.ppo.PPOUpdate: SB3 PPO.train
+    with the driver's hyper-parameters, n_epochs 10 over the whole buffer, Adam, clip_grad_norm; each 32 minibatch steps
+    one captured HIP graph) -- on a fresh SB3 MlpPolicy (pi/vf 128-128 tanh, log_std -1, torch's default init).  The
+    update's cost per env-step is n_epochs / batch_size SGD steps whatever n_steps is, so T < the driver's 2048 changes
+    the rate only by the collection's per-iteration constants.  Two minibatch sizes: the driver's 64, and 64 x E / 24
+    (the driver's 24 envs' rows per minibatch per env).  Timed: the second iteration (the first captures the graphs)."""
+    import torch
+    from cattleherd.ppo import PPOUpdate, SB3ActorCritic
+    from cattleherd.rollout import DeviceRolloutBuffer
+    out = {}
+    E = b.n_envs
+    for name, bs in (("driver_batch", batch_size), ("batch_scaled_with_envs", int(round(batch_size * E / n_envs_ref)))):
+        model = SB3ActorCritic(obs_dim=b.obs_rows * 86, act_dim=48, device=b.device, seed=0)
+        actor, critic, log_std = model.device_nets()
+        rb = DeviceRolloutBuffer(b, T, act_dim=48)
+        upd = PPOUpdate(model, batch_size=bs)
+        burn_in(b)
+        rb.collect(actor, critic, log_std, seed=1)
+        upd.train(rb)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        rb.collect(actor, critic, log_std, seed=2)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        steps = upd.train(rb)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        out[name] = {"env_steps_per_s": E * T / (t2 - t0), "collect_env_steps_per_s": E * T / (t1 - t0),
+                     "collect_s": t1 - t0, "update_s": t2 - t1, "update_share": (t2 - t1) / (t2 - t0),
+                     "batch_size": bs, "sgd_steps": steps, "us_per_sgd_step": (t2 - t1) / steps * 1e6,
+                     "rows": E * T, "n_steps": T, "n_epochs": upd.n_epochs}
+        del rb, upd, model
+        torch.cuda.empty_cache()
+    out["note"] = ("one PPO iteration = device collection of T steps x E envs + SB3 PPO.train over that buffer "
+                   "(lr 3e-4, n_epochs 10, clip 0.1, ent 0.1, vf 0.7, max_grad_norm 0.5, CTDECattleHerder.py:107-127); "
+                   "SB3 semantics restated (parity unpinned); the reference's published SB3 time/fps is 93-269 "
+                   "(24 CPU envs, SURVEY 6)")
+    return out
+
+
 def marl_ppo_rollout(b, T=32):
     """configs[4]'s training use: RLlib PPO sampling with one shared policy over every agent (DTDECattleHerder.py:
     62-97; the RLlib default model, 86 -> 256 -> 256 -> 8 tanh = DiagGaussian mean and log_std, and a separate value
-    branch 86 -> 256 -> 256 -> 1, random-initialised) on the device (cattleherd.rollout.DeviceMarlRolloutBuffer): per
+    branch 86 -> 256 -> 256 -> 1, with the reference's trained weights simulator/policy_weights.pkl) on the device
+    (cattleherd.rollout.DeviceMarlRolloutBuffer): per
     step the two forwards (f32 MFMA), the per-agent sample / log-prob / store, the env step with the wrapper's
     drop-out; then per-agent GAE.  env-steps/s (and agent-steps/s) of one whole T-step collection after an untimed
     one."""
     import torch
     from cattleherd.policy import DevicePolicy
     from cattleherd.rollout import DeviceMarlRolloutBuffer
-    policy = DevicePolicy(DevicePolicy.random_layers([86, 256, 256, 8], seed=1), "tanh", None)
-    value = DevicePolicy(DevicePolicy.random_layers([86, 256, 256, 1], seed=2), "tanh", None)
+    import numpy as np
+    d = np.load(POLICY_MARL_GOLDEN)
+    w = {k.replace("__", "."): d[k] for k in d.files if "__" in k}
+    policy = DevicePolicy.rllib_policy(w, cache_packed=True)
+    value = DevicePolicy.rllib_value(w, cache_packed=True)
     rb = DeviceMarlRolloutBuffer(b, T)
     burn_in(b)
     rb.collect(policy, value, seed=1)
@@ -240,7 +289,8 @@ def marl_ppo_rollout(b, T=32):
     dt = time.perf_counter() - t0
     out = {"env_steps_per_s": b.n_envs * T / dt, "agent_steps_per_s": b.n_envs * b.num_drones * T / dt,
            "ms_per_step": dt / T * 1000.0, "n_steps": T, "burn_in": PPO_BURN_IN,
-           "policy": "RLlib default model 86-256-256-8 (mean, log_std) + value 86-256-256-1, tanh, random init, f32",
+           "policy": "RLlib default model 86-256-256-8 (mean, log_std) + value 86-256-256-1, tanh, f32, the reference's "
+                     "trained weights (simulator/policy_weights.pkl)",
            "gae": "per agent, gamma 0.99, lambda 1.0 (RLlib PPO default)",
            "buffer_GB": sum(t.numel() * t.element_size() for t in (rb.obs, rb.actions)) / 1e9}
     del rb
@@ -448,6 +498,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--policy", action="store_true",
                     help="also time a rollout driven by the on-device SB3 policy (model-v16-6 weights, CTDE only)")
+    ap.add_argument("--train", action="store_true",
+                    help="CTDE: also time one PPO training iteration (device collection + SB3 PPO update, configs[2])")
     ap.add_argument("--graph", type=int, default=0,
                     help="steps per captured HIP graph in the timed loop (0 = one host launch per step)")
     ap.add_argument("--backend", default="nccl", help="process-group backend (nccl = RCCL over xGMI)")
@@ -649,6 +701,8 @@ def main():
                                                                          "source") if k in fr} or fr_why
         if args.policy and mode == "ctde":
             out["policy_rollout"] = policy_rollout(b, n, args.steps, args.warmup)
+        if args.train and mode == "ctde":
+            out["ppo_train_iteration"] = ppo_train_iteration(b)
         if args.policy and mode == "marl":
             out["marl_ppo_rollout"] = marl_ppo_rollout(b)
         if mode == "marl" and not args.no_extras:

@@ -26,6 +26,11 @@ def load_sb3_state_dict(path):
         return torch.load(io.BytesIO(z.read("policy.pth")), weights_only=True, map_location="cpu")
 
 
+def _first(x):
+    import numpy as np
+    return np.asarray(x.cpu() if hasattr(x, "cpu") else x).reshape(-1)[0]
+
+
 class DevicePolicy:
     """A dense MLP (1-4 layers, widths <= 256) evaluated by ``ch_mlp_forward``.
 
@@ -113,6 +118,33 @@ class DevicePolicy:
         layers = [(sd["mlp_extractor.value_net.0.weight"], sd["mlp_extractor.value_net.0.bias"]),
                   (sd["mlp_extractor.value_net.2.weight"], sd["mlp_extractor.value_net.2.bias"]),
                   (sd["value_net.weight"], sd["value_net.bias"])]
+        return cls(layers, "tanh", None, device, cache_packed=cache_packed)
+
+    @classmethod
+    def rllib_policy(cls, weights, device=None, cache_packed=False):
+        """The DTDE driver's RLlib PPO policy (``DTDECattleHerder.py:62-97``; the trained weights
+        ``simulator/policy_weights.pkl`` = ``algo.get_weights()[policy]``, ``simulator/test.py:19-30``): the actor
+        encoder Linear(86, 256) tanh Linear(256, 256) tanh, then ``pi`` Linear(256, 2A) = DiagGaussian (mean, log_std).
+        The log_std half's clamp to [-20, 20] (``pi.log_std_clip_param_const``) is applied where the rollout reads it
+        (``k_marl_store``); ``weights``: name -> array, RLlib's own key names."""
+        w = weights
+        layers = [(w["encoder.actor_encoder.net.mlp.0.weight"], w["encoder.actor_encoder.net.mlp.0.bias"]),
+                  (w["encoder.actor_encoder.net.mlp.2.weight"], w["encoder.actor_encoder.net.mlp.2.bias"]),
+                  (w["pi.net.mlp.0.weight"], w["pi.net.mlp.0.bias"])]
+        clip = w.get("pi.log_std_clip_param_const")
+        if clip is not None and abs(float(_first(clip)) - 20.0) > 0:
+            raise ValueError("k_marl_store clamps log_std to RLlib's default 20; these weights carry "
+                             f"log_std_clip_param {float(_first(clip))}")
+        return cls(layers, "tanh", None, device, cache_packed=cache_packed)
+
+    @classmethod
+    def rllib_value(cls, weights, device=None, cache_packed=False):
+        """The RLlib PPO value branch: critic encoder (the actor's shape, its own weights: vf_share_layers False)
+        and ``vf`` Linear(256, 1)."""
+        w = weights
+        layers = [(w["encoder.critic_encoder.net.mlp.0.weight"], w["encoder.critic_encoder.net.mlp.0.bias"]),
+                  (w["encoder.critic_encoder.net.mlp.2.weight"], w["encoder.critic_encoder.net.mlp.2.bias"]),
+                  (w["vf.net.mlp.0.weight"], w["vf.net.mlp.0.bias"])]
         return cls(layers, "tanh", None, device, cache_packed=cache_packed)
 
     @classmethod

@@ -150,7 +150,10 @@ __global__ void k_rollout_gae(RolloutArgs a) {
 // ---- the DTDE (RLlib) per-agent rollout (ch_marl_rollout_collect; DTDECattleHerder.py:62-97, marl_wrapper.py:77-119)
 // RLlib PPO with one shared policy over every agent row (RLlib is not in this image: its defaults restated, "parity
 // unpinned"): the policy output is DiagGaussian's (mean, log_std), actions a = mean + exp(log_std) eps stored
-// unclipped, the env gets them clipped to Box(-1, 1); the log-probability is summed in action order.
+// unclipped, the env gets them clipped to Box(-1, 1); the log-probability is summed in action order.  The log_std
+// half is clamped to [-20, 20] first, as RLlib's MLP head does for a DiagGaussian (clip_log_std with
+// log_std_clip_param 20: the trained weights simulator/policy_weights.pkl carry pi.log_std_clip_param_const = 20).
+constexpr float kRllibLogStdClip = 20.0f;
 
 // after the env step t - 1: the agent's reward / terminated / truncated into the buffer (0 where it was not live)
 __device__ __forceinline__ void marl_post(const MarlArgs& a, int t, long long r) {
@@ -189,7 +192,9 @@ __global__ __launch_bounds__(256) void k_marl_store(MarlArgs a) {
             const float u1 = ((float)(c[0] >> 8) + 1.0f) * (1.0f / 16777216.0f);   // (0, 1]
             const float u2 = (float)(c[1] >> 8) * (1.0f / 16777216.0f);
             const float eps = sqrtf(-2.0f * logf(u1)) * cosf(6.2831853071795865f * u2);
-            const float mu = a.pol[r * 2 * a.A + k], ls = a.pol[r * 2 * a.A + a.A + k], sd = expf(ls);
+            const float mu = a.pol[r * 2 * a.A + k];
+            const float ls = fminf(fmaxf(a.pol[r * 2 * a.A + a.A + k], -kRllibLogStdClip), kRllibLogStdClip);
+            const float sd = expf(ls);
             act = mu + sd * eps;
             const float d = act - mu, var = sd * sd;
             lps += -(d * d) / (2.0f * var) - ls - 0.91893853320467274f;

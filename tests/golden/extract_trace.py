@@ -16,7 +16,7 @@ import sys
 import numpy as np
 
 ALLOWED_GLOBALS = {("numpy.core.multiarray", "_reconstruct"), ("numpy", "ndarray"), ("numpy", "dtype"),
-                   ("numpy.core.multiarray", "scalar")}
+                   ("numpy.core.multiarray", "scalar"), ("collections", "OrderedDict")}
 
 
 class _G:
@@ -58,6 +58,8 @@ def load_data_only(path):
             stack.append({})
         elif n == "EMPTY_LIST":
             stack.append([])
+        elif n == "EMPTY_TUPLE":
+            stack.append(())
         elif n == "MEMOIZE":
             memo[len(memo)] = stack[-1]
         elif n in ("BINGET", "LONG_BINGET"):
@@ -93,6 +95,10 @@ def load_data_only(path):
                 stack.append(_Arr())
             elif fn.key == ("numpy", "dtype"):
                 stack.append(_DT(args[0]))
+            elif fn.key == ("collections", "OrderedDict"):
+                if args != ():
+                    raise ValueError("OrderedDict with constructor arguments")
+                stack.append({})   # filled by the SETITEMS that follow; key order is kept by dict
             elif fn.key == ("numpy.core.multiarray", "scalar"):
                 dt, raw = args
                 stack.append(np.frombuffer(raw, dtype=dt.np())[0])

@@ -51,7 +51,25 @@ def _make(E, n, m, near):
     return b
 
 
-def test_marl_rollout_matches_rllib_semantics_configs4():
+GOLD = "tests/golden/policy_marl_rllib.npz"
+
+
+def _trained():
+    """The reference's trained RLlib weights (simulator/policy_weights.pkl, via tests/golden/make_policy_marl_golden)."""
+    import os
+    from cattleherd.policy import DevicePolicy
+    d = np.load(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), GOLD))
+    w = {k.replace("__", "."): d[k] for k in d.files if "__" in k}
+    return DevicePolicy.rllib_policy(w), DevicePolicy.rllib_value(w)
+
+
+def _log_std(out, A=4):
+    """RLlib's MLP head clamps the DiagGaussian log_std half to [-20, 20] (log_std_clip_param)."""
+    return out[..., A:].clamp(-20.0, 20.0)
+
+
+@pytest.mark.parametrize("weights", ["random", "trained"])
+def test_marl_rollout_matches_rllib_semantics_configs4(weights):
     import torch
     from cattleherd.policy import DevicePolicy
     from cattleherd.rollout import DeviceMarlRolloutBuffer
@@ -59,8 +77,11 @@ def test_marl_rollout_matches_rllib_semantics_configs4():
     rows = E * n
     near = np.arange(E) % 3 == 0
     b = _make(E, n, m, near)
-    policy = DevicePolicy(DevicePolicy.random_layers([86, 256, 256, 8], seed=1), "tanh", None)
-    value = DevicePolicy(DevicePolicy.random_layers([86, 256, 256, 1], seed=2), "tanh", None)
+    if weights == "trained":
+        policy, value = _trained()
+    else:
+        policy = DevicePolicy(DevicePolicy.random_layers([86, 256, 256, 8], seed=1), "tanh", None)
+        value = DevicePolicy(DevicePolicy.random_layers([86, 256, 256, 1], seed=2), "tanh", None)
     rb = DeviceMarlRolloutBuffer(b, T)
     rb.collect(policy, value, seed=11)
     torch.cuda.synchronize()
@@ -69,7 +90,7 @@ def test_marl_rollout_matches_rllib_semantics_configs4():
     assert mask[0].all()
     # 1. log-probabilities and values of the stored samples under the torch forward, on the live rows
     out = policy.reference(rb.obs.view(T * rows, 86)).view(T, rows, 8)
-    mean, log_std = out[..., :4], out[..., 4:]
+    mean, log_std = out[..., :4], _log_std(out)
     std = torch.exp(log_std)
     want_lp = torch.distributions.Normal(mean, std).log_prob(rb.actions).sum(-1)
     assert torch.allclose(rb.log_probs[mb], want_lp[mb], rtol=1e-5, atol=1e-4)
@@ -126,4 +147,29 @@ def test_marl_rollout_gae_lambda_and_cpu_restatement_agree_on_a_small_case():
     assert np.allclose(rb.advantages.cpu().numpy(), adv, rtol=2e-6, atol=2e-6, equal_nan=True)
     assert np.allclose(rb.returns.cpu().numpy(), ret, rtol=2e-6, atol=2e-6, equal_nan=True)
     assert (term != 0).any()
+    b.close()
+
+
+def test_marl_rollout_clamps_log_std_like_rllib():
+    """A policy whose log_std outputs leave [-20, 20]: the samples and log-probabilities use the clamped values (RLlib's
+    MLP head, log_std_clip_param 20; the trained weights carry pi.log_std_clip_param_const = 20)."""
+    import torch
+    from cattleherd.policy import DevicePolicy
+    from cattleherd.rollout import DeviceMarlRolloutBuffer
+    E, n, m, T = 64, 3, 8, 3
+    b = _make(E, n, m, np.zeros(E, bool))
+    w = torch.zeros(8, 86)   # outputs = the bias exactly, on the device and in torch
+    bias = torch.tensor([0.1, -0.2, 0.3, 0.0, 30.0, -30.0, 25.0, -1.0])
+    policy = DevicePolicy([(w, bias)], "tanh", None)
+    value = DevicePolicy(DevicePolicy.random_layers([86, 16, 1], seed=5), "tanh", None)
+    rb = DeviceMarlRolloutBuffer(b, T)
+    rb.collect(policy, value, seed=3)
+    torch.cuda.synchronize()
+    mb = rb.agent_mask != 0
+    out = policy.reference(rb.obs.view(T * E * n, 86)).view(T, E * n, 8)
+    mean, std = out[..., :4], torch.exp(_log_std(out))
+    eps = (rb.actions.double() - mean) / std
+    assert float(eps[mb][:, [0, 2]].abs().max()) < 7.0   # the e^20 columns: unclamped e^30 / e^25 would give e^10 / e^5 x eps
+    want_lp = torch.distributions.Normal(mean, std).log_prob(rb.actions.double()).sum(-1)
+    assert torch.allclose(rb.log_probs[mb].double(), want_lp[mb], rtol=1e-5, atol=1e-3)
     b.close()

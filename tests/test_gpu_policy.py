@@ -58,6 +58,31 @@ def test_sb3_actor_and_critic_match_reference_model():
     assert (a.abs() <= 1).all()
 
 
+def test_rllib_policy_and_value_match_reference_weights():
+    """The reference's trained RLlib PPO weights (simulator/policy_weights.pkl, read data-only by
+    tests/golden/make_policy_marl_golden.py): pi logits (mean, log_std) and values on oracle MARL observations, against
+    the fp32 torch outputs in the fixture and an fp64 forward, at 2e-5."""
+    import os
+    import torch
+    from cattleherd.policy import DevicePolicy
+    d = np.load(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                             "tests/golden/policy_marl_rllib.npz"))
+    w = {k.replace("__", "."): d[k] for k in d.files if "__" in k}
+    pol, val = DevicePolicy.rllib_policy(w), DevicePolicy.rllib_value(w)
+    assert pol.dims == [86, 256, 256, 8] and val.dims == [86, 256, 256, 1]
+    x = torch.tensor(d["obs"])
+    lg = pol.forward(x)
+    v = val.forward(x)
+    torch.cuda.synchronize()
+    assert float(lg[:, 4:].abs().max()) < 20.0    # inside RLlib's log_std clamp: the head output is the logits
+    ok, err = _close(lg, torch.tensor(d["logits"]))
+    assert ok, err
+    ok, err = _close(v[:, 0], torch.tensor(d["values"]))
+    assert ok, err
+    ok, err = _close(lg, _ref64(pol, x))
+    assert ok, err
+
+
 @pytest.mark.parametrize("dims,act,rows", [((1032, 128, 128, 48), "tanh", 4096), ((86, 256, 256, 8), "tanh", 4095),
                                            ((50, 16, 3), "relu", 17), ((1032, 128, 128, 1), "tanh", 1),
                                            ((7, 200, 33, 250, 5), "none", 100)])
