@@ -77,7 +77,10 @@ typedef struct ch_config {
     int32_t pyb_freq;         /* 240 (CattleAviary.py:22) */
     int32_t compat;           /* 1 = reproduce reference quirks bit-for-bit (DESIGN.md "Quirks") */
     int32_t precision;        /* CH_PREC_F64 (reference arithmetic) or CH_PREC_F32 */
-    int32_t torque_world;     /* link_lag = 0 only: 1 = applyExternalTorque(LINK_FRAME) acts in world frame */
+    int32_t torque_world;     /* link_lag = 0 only: 1 = applyExternalTorque(LINK_FRAME) acts in world frame.  With
+                                 link_lag = 1 the z torque turns with the cached link frame whatever this says: the
+                                 recorded real-PyBullet trace rejects a world-frame z torque there (2e-5 vs 2e-13
+                                 m/s by step 4) */
     int32_t gyro;             /* 1 = gyroscopic term (btMultiBody default) */
     int32_t marl_wrapper;     /* MARL only: 1 = RLlibMultiAgentWrapper.step semantics (marl_wrapper.py:77-119:
                                  per-agent recomputation, finished agents drop out, episode ends when all

@@ -340,7 +340,12 @@ void och_dyn_integrate(double* y, const double* rpm, double dt, int64_t steps, i
     }
 }
 
-/* ql != NULL (config link_lag): Bullet's cached link frame.  PyBullet's applyExternalForce / applyExternalTorque
+/* torque_world applies with link_lag = 0 (rounds 1-4: the z torque in the world frame, PyBullet's LINK_FRAME torque
+ * quirk on a base).  Under the cached link frame the z torque turns with that frame like the prop forces: the torque
+ * is applied to link 4, and PyBullet rotates a link's LINK_FRAME torque by the link's cached transform; the trace
+ * rejects the world-frame alternative (torque_world = 2 here, a test-only value: 2e-5 m/s vs 2e-13 by step 4,
+ * DESIGN.md §3).
+ * ql != NULL (config link_lag): Bullet's cached link frame.  PyBullet's applyExternalForce / applyExternalTorque
  * with LINK_FRAME on a multibody link rotate the link-frame vector by that link's cached world transform, which a
  * link without a collision shape (the cf2x prop links and center_of_mass_link, cf2x.urdf:34-98) only gets from the
  * forward-kinematics pass at the start of the previous stepSimulation: the base attitude one substep old (ql).  The
@@ -349,6 +354,12 @@ void och_dyn_integrate(double* y, const double* rpm, double dt, int64_t steps, i
  * recorded real-PyBullet trace (tests/golden/trace_inverse.npz): the first evaluation episode's
  * drone xy velocities and positions to ~1e-12 relative over its first steps, where the current-attitude model
  * (ql = NULL) misses the first step's velocity by a factor 2.5. */
+/* Test hook (tests/golden/make_trace_inverse.py): alternative rigid-body models the real-PyBullet trace is checked
+ * against.  Bit 0: the base's linear acceleration with a velocity-product term -m (w x v) (what integrating Bullet's
+ * body-frame spatial acceleration as a world-frame one would add).  Its trace residual is 7e-9 m/s on the first step
+ * against 2e-16 without it, so 0 (the default) is the model. */
+static int g_model_flags = 0;
+void och__set_model_flags(int f) { g_model_flags = f; }
 static void drone_substep(const och_config* c, double* p, double* q, double* v, double* w, const double* rpm, double dt,
                           const phys_ctx* x, double* ql) {
     double R[9]; och_matrix_from_quat(q, R);
@@ -368,9 +379,15 @@ static void drone_substep(const och_config* c, double* p, double* q, double* v, 
         for (int i = 0; i < 3; ++i) u[i] = (R[0 + i] * Rl[2] + R[3 + i] * Rl[5]) + R[6 + i] * Rl[8];
         const double sy = 0.028 * (((-f[0] - f[1]) + f[2]) + f[3]);   /* sum_i f_i r_iy */
         const double sx = 0.028 * (((-f[0] + f[1]) + f[2]) - f[3]);   /* -sum_i f_i r_ix */
-        tb[0] = sy * u[2] + u[0] * tz;
-        tb[1] = sx * u[2] + u[1] * tz;
-        tb[2] = (-sx * u[1] - sy * u[0]) + u[2] * tz;
+        if (c->torque_world == 2) {   /* alternative model (trace inversion only): world-frame z torque, rejected */
+            tb[0] = sy * u[2] + R[6] * tz;
+            tb[1] = sx * u[2] + R[7] * tz;
+            tb[2] = (-sx * u[1] - sy * u[0]) + R[8] * tz;
+        } else {
+            tb[0] = sy * u[2] + u[0] * tz;
+            tb[1] = sx * u[2] + u[1] * tz;
+            tb[2] = (-sx * u[1] - sy * u[0]) + u[2] * tz;
+        }
     } else if (body) {
         /* PYB with the world-frame motor torque (the default): the four +z prop forces (LINK_FRAME at
          * (px, py, 0), cf2x.urdf:42-78) reduced to the body frame in closed form.  Their world torque
@@ -392,7 +409,7 @@ static void drone_substep(const och_config* c, double* p, double* q, double* v, 
             double t[3]; cross3(rw, fw, t);
             for (int k = 0; k < 3; ++k) { F[k] += fw[k]; Tw[k] += t[k]; }
         }
-        if (c->torque_world && !ql) Tw[2] += tz;
+        if (c->torque_world && (!ql || c->torque_world == 2)) Tw[2] += tz;
         else { Tw[0] += Rl[2] * tz; Tw[1] += Rl[5] * tz; Tw[2] += Rl[8] * tz; }
         if (x) physics_forces(x, p, q, v, R, Rl, rpm, F, Tw);
     }
@@ -419,6 +436,10 @@ static void drone_substep(const och_config* c, double* p, double* q, double* v, 
         for (int i = 0; i < 3; ++i) tb[i] -= g[i];
     }
     double ab[3] = {tb[0] / J[0], tb[1] / J[1], tb[2] / J[2]};
+    if (g_model_flags & 1) {   /* alternative model (trace inversion only): a velocity-product term m w x v, rejected */
+        double wxv[3]; cross3(w, v, wxv);
+        for (int i = 0; i < 3; ++i) F[i] -= MASS * wxv[i];
+    }
     for (int i = 0; i < 3; ++i) {
         double aw = R[i * 3 + 0] * ab[0] + R[i * 3 + 1] * ab[1] + R[i * 3 + 2] * ab[2];
         v[i] = v[i] + (F[i] / MASS) * dt;
@@ -961,6 +982,12 @@ void och_init(const och_config* c, och_state* s, int64_t env_id) {
 /* ---------------------------------------------------------------------------------------------
  * step: BaseAviary.step (sb3_envs/BaseAviary.py:335-465; rllib_envs/BaseAviary.py:320-438)
  * ------------------------------------------------------------------------------------------- */
+/* Test hook (tests/golden/make_trace_inverse.py): when set, the PID's target velocity of drone k is tv[3k..3k+2] in
+ * float64 instead of the one _preprocessAction derives from the float32 action row -- a pure physics-model test that
+ * the action's float32 rounding does not limit.  NULL (the default) restores the reference path. */
+static const double* g_tv_override = NULL;
+void och__set_target_vel(const double* tv) { g_tv_override = tv; }
+
 int och_step(const och_config* c, och_state* s, const float* actions, float* obs, double* reward,
              uint8_t* terminated, uint8_t* truncated, float* terminal_obs, int autoreset) {
     int n = s->n;
@@ -982,6 +1009,7 @@ int och_step(const och_config* c, och_state* s, const float* actions, float* obs
         if (hn != 0.0f) { ux = hx / hn; uy = hy / hn; }
         float sc = (float)sl * fabsf(a[3]);
         double tv[3] = {(double)ux * (double)sc, (double)uy * (double)sc, 0.0 * (double)sc};
+        if (g_tv_override) { tv[0] = g_tv_override[3 * k]; tv[1] = g_tv_override[3 * k + 1]; tv[2] = g_tv_override[3 * k + 2]; }
         double rpy[3]; och_euler_from_quat(s->dq[k], rpy);
         double tp[3] = {s->dp[k][0], s->dp[k][1], TARGET_ALT};
         double tr[3] = {0.0, 0.0, rpy[2]};

@@ -82,6 +82,8 @@ void och_init(const och_config* c, och_state* s, int64_t env_id);
 int  och_step(const och_config* c, och_state* s, const float* actions, float* obs, double* reward,
               uint8_t* terminated, uint8_t* truncated, float* terminal_obs, int autoreset);
 void och_task(const och_config* c, och_state* s, double* reward, uint8_t* terminated, uint8_t* truncated);
+void och__set_target_vel(const double* tv);   /* test hook: float64 PID target velocities, NULL = off */
+void och__set_model_flags(int f);            /* test hook: alternative rigid-body models (trace inversion) */
 void och_random_actions(const och_config* c, int64_t env_id, int64_t step, float* actions);
 /* CPU baseline: E envs x T steps of random-action rollout, OpenMP over envs; returns seconds */
 double och_batch_rollout(const och_config* c, och_state* states, int64_t E, int64_t T, int threads);

@@ -279,6 +279,8 @@ template <class R> __device__ __forceinline__ void pos_add(R p[3], double* pacc,
 // with the current attitude.  Body frame, u = M^T ql_z: torque sum_i f_i (r_i x u) + u tz, force ql_z sum f.  Pinned
 // by the real-PyBullet trace (oracle/ch_oracle.c drone_substep, the same operation order).
 // extra(M, Ml, F, Tw): M the current attitude, Ml the cached link frame (== M without link_lag).
+// torque_world acts only without the cached frame: under it the z torque (on link 4) turns with Ml like the forces;
+// the trace rejects a world-frame z torque there (make_trace_inverse.py model lag_worldtz).
 template <class R, class X = NoExtraForces>
 __device__ __forceinline__ void drone_substep(R p[3], R q[4], R v[3], R w[3], const double rpm[4], R dt, R damping,
                                               bool torque_world, bool gyro, const X& extra = X(),

@@ -2,10 +2,12 @@
 
 ``trace_inverse.npz`` holds the first evaluation episode of ``simulator/evaluation_data.pkl`` (3 drones, 16 cattle,
 real Bullet, CTDECattleHerder.py:169-185) and the float32 VEL actions recovered from it
-(``tests/golden/make_trace_inverse.py``).  Stepping ``libcattleherd`` with them from the episode's initial state must
-reproduce every drone's recorded xy velocity and position, as the oracle does (``test_oracle_golden.py::
-test_drone_rigid_body_pinned_to_real_pybullet``).  Tolerances: velocity 3e-8 m/s, position 1e-9 m absolute -- the
-float32 rounding of the recovered actions; the rounds 1-4 model (link_lag=0) misses by > 1e-5.
+(``tests/golden/make_trace_inverse.py``: float64 target velocities fitted per drone-step, realised as float32 action
+triples).  Stepping ``libcattleherd`` with them from the episode's initial state must reproduce every drone's recorded
+xy velocity and position, as the oracle does (``test_oracle_golden.py::test_drone_rigid_body_pinned_to_real_pybullet``).
+Tolerances, per step: twice the oracle replay's residual recorded in the fixture (+1e-12 m/s, +1e-13 m): <= 6e-8 m/s
+through step 11 (0.40 m/s, 28.5 deg of tilt), 1.4e-6 m/s at steps 12-13 (0.57 m/s), where the model departs from the
+trace; the rounds 1-4 model (link_lag=0) misses by > 1e-3 m/s.
 """
 import numpy as np
 import pytest
@@ -35,7 +37,9 @@ def _replay(link_lag, E=4):
 
 
 def test_hip_drone_rigid_body_matches_real_pybullet_trace():
+    t = load("trace_inverse.npz")
     dv, dp = _replay(True)
-    assert dv.max() <= 3e-8 and dp.max() <= 1e-9, (dv, dp)
+    assert (dv <= 2 * t["replay_dv"] + 1e-12).all() and (dp <= 2 * t["replay_dp"] + 1e-13).all(), (dv, dp)
+    assert int(t["steps"]) >= 14 and dv[:12].max() <= 6e-8
     dv0, dp0 = _replay(False)
-    assert dp0.max() > 1e-5 and dv0.max() > 1e-4, (dv0, dp0)
+    assert dp0.max() > 1e-5 and dv0.max() > 1e-3, (dv0, dp0)
