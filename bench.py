@@ -102,12 +102,16 @@ def valu_issue(d, dtype, kern_us):
                     "active_frac from SQ_ACTIVE_INST_VALU (quad-cycles, summed over waves)"}
 
 
-def kernel_name(b):
-    """Which step kernel the handle launches (internal diagnostics entry point)."""
+def kernel_name(b, multi=False):
+    """Which step kernel the handle launches (internal diagnostics entry point); `multi`: ch_step_n's k_step2_multi
+    (at most 512 threads per workgroup)."""
     import ctypes
     from cattleherd import _lib
     g, blk, lds, kv = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int32()
     _lib.lib().ch__geometry(b.handle, ctypes.byref(g), ctypes.byref(blk), ctypes.byref(lds), ctypes.byref(kv))
+    if kv.value == 2 and multi:
+        return (f"ch::k_step2_multi (every workgroup steps its envs back to back; {g.value} envs/workgroup, "
+                f"{min(blk.value, 512)} threads, {lds.value} B LDS)")
     if kv.value == 2:
         return f"ch::k_step2 (drone wave + cow waves; {g.value} envs/workgroup, {blk.value} threads, {lds.value} B LDS)"
     return "ch::k_env (team per env)"
@@ -500,6 +504,12 @@ def main():
                     help="also time a rollout driven by the on-device SB3 policy (model-v16-6 weights, CTDE only)")
     ap.add_argument("--train", action="store_true",
                     help="CTDE: also time one PPO training iteration (device collection + SB3 PPO update, configs[2])")
+    ap.add_argument("--steps-per-launch", type=int, default=-1,
+                    help="timed steps per ch_step_n call (k_step2_multi: every workgroup steps its envs back to back "
+                         "in one launch); -1 (default) = all timed steps in one call; 1 = one ch_step launch per step")
+    ap.add_argument("--counter-probe", type=int, default=0,
+                    help="(tools/counter_record.py --multi) after the burn-in, 10 ch_step_n calls of this many steps "
+                         "each, nothing else; no JSON line")
     ap.add_argument("--graph", type=int, default=0,
                     help="steps per captured HIP graph in the timed loop (0 = one host launch per step)")
     ap.add_argument("--backend", default="nccl", help="process-group backend (nccl = RCCL over xGMI)")
@@ -570,16 +580,34 @@ def main():
     # episode phases -- and auto-resets -- at their steady-state spread rather than K steps of fresh episodes
     for _ in range(args.burn_in):
         b.step(random_actions=True, autoreset=True, terminal_obs=False)
-    for _ in range(args.warmup):
-        b.step(random_actions=True, autoreset=True, terminal_obs=False)
+    if args.counter_probe:   # the multi-step kernel's counter passes: equal dispatches of a known step count
+        for _ in range(10):
+            b.step_n(args.counter_probe, random_actions=True)
+        torch.cuda.synchronize()
+        b.close()
+        D.shutdown()
+        return
+    # steps per ch_step_n call: -1 (default) = every timed step in one call; 1 = one ch_step launch per step
+    spl = args.steps if args.steps_per_launch < 0 else max(1, args.steps_per_launch)
+    if spl > 1:
+        b.step_n(max(args.warmup, 1), random_actions=True)   # (also uploads the multi-step kernel's parameters)
+    else:
+        for _ in range(args.warmup):
+            b.step(random_actions=True, autoreset=True, terminal_obs=False)
     # the timed loop: K steps as whole graph replays of `chunk` steps (plus single launches for the rest)
-    chunk = args.graph if args.graph > 0 and args.steps >= args.graph else 0
+    chunk = args.graph if args.graph > 0 and args.steps >= args.graph and spl == 1 else 0
     graph = b.capture_rollout(chunk) if chunk else None
     end_of_rollout()   # warm: reduction kernel, pinned copy, first collective; zeroes the metric rows
     b.sync()
 
     def run(k):
         done = 0
+        if spl > 1:   # ch_step_n: each workgroup steps its envs back to back inside one launch
+            while done < k:
+                n = min(spl, k - done)
+                b.step_n(n, random_actions=True)
+                done += n
+            return
         if graph is not None:
             while done + chunk <= k:
                 graph.replay()
@@ -613,11 +641,14 @@ def main():
     nk = min(200, args.steps)
     s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s_ev.record(stream)
-    for _ in range(nk):
-        b.step(random_actions=True, autoreset=True, terminal_obs=False)
+    if spl > 1:
+        b.step_n(nk, random_actions=True)   # one k_step2_multi launch of nk steps
+    else:
+        for _ in range(nk):
+            b.step(random_actions=True, autoreset=True, terminal_obs=False)
     e_ev.record(stream)
     torch.cuda.synchronize()
-    kern_us = s_ev.elapsed_time(e_ev) / nk * 1000.0
+    kern_us = s_ev.elapsed_time(e_ev) / nk * 1000.0   # per step
     rb = 8 if args.precision == "f64" else 4
     bytes_step = algorithmic_bytes(mode, n, m, b.obs_rows, rb)
     survey_step = survey_bytes(mode, n, m, b.obs_rows)
@@ -626,9 +657,13 @@ def main():
     achieved = bytes_step * E / (kern_us * 1e-6) / 1e9
     achieved_survey = survey_step * E / (kern_us * 1e-6) / 1e9
     default_cfg = E == WORKLOADS[args.workload][1] and args.physics == "pyb"
-    rec, rec_why = counter_record(f"{args.workload}_{args.precision}") if default_cfg else ({}, "not a default workload")
+    from cattleherd import _lib as _L
+    multi_ran = spl > 1 and _L.lib().ch__multi_steps(b.handle) > 0   # (other geometries: one launch per step)
+    # the counter record of the kernel the headline ran (the multi-step kernel's per step, tools/counter_record.py --multi)
+    rec_name = f"{args.workload}_{args.precision}" + ("_multi" if multi_ran else "")
+    rec, rec_why = counter_record(rec_name) if default_cfg else ({}, "not a default workload")
     traffic = rec.get("traffic_bytes_per_launch")
-    kname = kernel_name(b)
+    kname = kernel_name(b, multi=multi_ran)
     # the same kernel with SB3's terminal observations requested (the synced reset path: the headline's sync-free
     # one does not write info["terminal_observation"])
     term_leg = None
@@ -645,6 +680,31 @@ def main():
         term_leg = {"env_steps_per_s": E * world * nt / dt1, "ms_per_step": dt1 / nt * 1e3, "steps": nt,
                     "note": "ch_step with terminal_obs (SB3 info['terminal_observation'] written for every auto-reset): "
                             "the VecEnv / rollout-buffer path; the headline value is the sync-free path without it"}
+    # the same random-action rollout with one ch_step launch per step (the form an SB3 / RLlib caller steps in: a
+    # policy between two steps), beside the headline's ch_step_n form
+    single_leg = None
+    if not args.no_extras or spl > 1:
+        ns = min(2000, args.steps)
+        for _ in range(5):
+            b.step(random_actions=True, autoreset=True, terminal_obs=False)
+        torch.cuda.synchronize()
+        D.barrier()
+        t2 = time.perf_counter()
+        for _ in range(ns):
+            b.step(random_actions=True, autoreset=True, terminal_obs=False)
+        torch.cuda.synchronize()
+        D.barrier()
+        dt2 = time.perf_counter() - t2
+        _, dt2 = D.reduce_rollout([0.0], dt2, device=b.device)
+        s_ev.record(stream)
+        for _ in range(nk):
+            b.step(random_actions=True, autoreset=True, terminal_obs=False)
+        e_ev.record(stream)
+        torch.cuda.synchronize()
+        single_leg = {"env_steps_per_s": E * world * ns / dt2, "ms_per_step": dt2 / ns * 1e3, "steps": ns,
+                      "kernel": kernel_name(b), "kernel_us": s_ev.elapsed_time(e_ev) / nk * 1000.0,
+                      "note": "one ch_step launch per step (k_step2): the grid of every step waits for its slowest "
+                              "workgroup and the next launch"}
     wg = rec.get("wg_trace") or {}
 
     out = None
@@ -660,7 +720,11 @@ def main():
                     "auto-resets inside the timed steps at their long-run rate); headline without SB3 terminal "
                     "observations (terminal_obs=False, the sync-free auto-reset path), the terminal-observation path in "
                     "terminal_obs_leg",
-            "launch": f"HIP graph of {chunk} steps per replay" if graph is not None else "one host launch per step",
+            "launch": (f"ch_step_n, {spl} steps per call: every workgroup steps its envs back to back in one "
+                       f"k_step2_multi launch (bit-identical to ch_step launches, tests/test_gpu_runtime.py)" if multi_ran else
+                       f"ch_step_n, {spl} steps per call, one launch per step (no multi-step kernel for this geometry)"
+                       if spl > 1 else
+                       f"HIP graph of {chunk} steps per replay" if graph is not None else "one host launch per step"),
             "ranks": ranks,   # each rank's device index and PCI address (distinct, checked above)
             "rollout_end_us": rollout_end_us,
             "config": {"workload": desc, "envs_per_gpu": E, "num_drones": n, "num_cattle": m, "mode": mode,
@@ -688,6 +752,7 @@ def main():
                                 "byte_model": "SURVEY.md 8(d): fp32 SoA, minimal carried state, full obs block"},
             "valu": valu_issue(rec, args.precision, kern_us) if rec else None,
             "terminal_obs_leg": term_leg,
+            "single_launch_leg": single_leg,
             "rollout_metrics": {"episodes": mv[1], "mean_return": (mv[2] / mv[1]) if mv[1] else None,
                                 "nan_rewards": mv[6], "terminated": mv[4], "truncated": mv[5], "env_steps": mv[0],
                                 # what the timed steps were: truncation flags per (agent-)step and episode ends in the

@@ -11,7 +11,10 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(ROOT, "csrc")
 BUILD = os.path.join(ROOT, "build")
 LIB = os.path.join(PKG, "libcattleherd.so")
-SOURCES = ["ch_kernels.hip", "ch_step.hip", "ch_policy.hip", "ch_aux.hip", "ch_api.cpp"]
+SOURCES = ["ch_kernels.hip", "ch_step.hip", "ch_step_multi.hip", "ch_policy.hip", "ch_aux.hip", "ch_api.cpp"]
+# per-source flags: ch_step_multi.hip's step loop keeps k_step2's register allocation only with machine LICM off
+# (ch_step_multi.hip header)
+SOURCE_FLAGS = {"ch_step_multi.hip": ["-mllvm", "-disable-machine-licm"]}
 HEADERS = ["ch_device.h", "ch_internal.h", "ch_common.h", "ch_spawn_table.inc", "ch_mlp2_dev.h", "ch_rollout_dev.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("CH_OFFLOAD_ARCH", "gfx950")
@@ -39,7 +42,7 @@ def build(force=False, verbose=False, extra_flags=(), out=None):
     # the translation units compile in parallel (ch_step.hip's instantiations dominate the build)
     for src in SOURCES:
         obj = os.path.join(BUILD, src + ("".join(extra_flags).replace("-", "_") if extra_flags else "") + ".o")
-        cmd = [HIPCC, *FLAGS, *extra_flags, "-c", os.path.join(CSRC, src), "-o", obj]
+        cmd = [HIPCC, *FLAGS, *SOURCE_FLAGS.get(src, []), *extra_flags, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append((cmd, subprocess.Popen(cmd)))

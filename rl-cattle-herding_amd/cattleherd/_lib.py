@@ -21,7 +21,7 @@ PHYSICS = {"pyb": 0, "dyn": 1, "pyb_gnd": 2, "pyb_drag": 3, "pyb_dw": 4, "pyb_gn
 
 # every symbol include/cattleherd.h declares
 EXPORTS = ("ch_default_config", "ch_create", "ch_destroy", "ch_last_error", "ch_shape", "ch_reset", "ch_reset_with",
-           "ch_step",
+           "ch_step", "ch_step_n",
            "ch_state_size", "ch_get_state", "ch_set_state", "ch_metrics", "ch_metrics_device", "ch_sync",
            "ch_get_eval", "ch_builtin_spawn_table", "ch_rollout_store", "ch_rollout_post", "ch_rollout_gae", "ch_rollout_collect",
            "ch_spawn_table", "ch_mlp_forward", "ch_mlp_forward_masked", "ch_policy_forward", "ch_mlp_packed_size",
@@ -91,6 +91,10 @@ def lib():
     L.ch_reset.argtypes = [vp, vp, vp, vp]
     L.ch_reset_with.argtypes = [vp, vp, vp, vp, vp, vp]
     L.ch_step.argtypes = [vp, P(ChStepIO), vp]
+    if hasattr(L, "ch_step_n"):   # (an older library, e.g. an A/B baseline loaded through CH_LIB_PATH, lacks it)
+        L.ch_step_n.argtypes = [vp, P(ChStepIO), i32, vp]
+        L.ch__multi_steps.argtypes = [vp]
+        L.ch__multi_steps.restype = i64
     L.ch_state_size.argtypes = [vp, P(i64), P(i64)]
     L.ch_get_state.argtypes = [vp, vp, vp, vp]
     L.ch_set_state.argtypes = [vp, vp, vp, vp]
@@ -107,7 +111,7 @@ def lib():
     L.ch_mlp_pack.argtypes = [P(ChMlp), vp, vp]
     L.ch_outputs_to_host.argtypes = [vp, P(ChStepIO), P(ChHostOut), vp]
     for name in EXPORTS:
-        if name not in ("ch_last_error",):
+        if name not in ("ch_last_error",) and (name != "ch_step_n" or hasattr(L, name)):
             getattr(L, name).restype = ctypes.c_int
     L.ch_mlp_packed_size.restype = ctypes.c_int64
     _lib = L

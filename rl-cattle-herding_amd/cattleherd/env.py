@@ -175,6 +175,31 @@ class HerdBatch:
             L.check(rc, self.handle)
         return self.obs, self.reward, self.terminated, self.truncated
 
+    def step_n(self, n_steps, actions=None, autoreset=True, random_actions=True):
+        """``n_steps`` calls of ``step(..., terminal_obs=False)`` with the same arguments, in one ``ch_step_n``: the
+        first step is one launch, the other ``n_steps - 1`` run in one launch in which every workgroup steps its envs
+        back to back (the BASELINE geometries; one launch per step elsewhere).  Random actions are drawn per step on
+        the device.  Returns the last step's outputs."""
+        io = self._io
+        flags = (L.CH_STEP_AUTORESET if autoreset else 0) | (L.CH_STEP_RANDOM_ACTIONS if random_actions else 0)
+        if random_actions:
+            io.actions = None
+            io.actions_out = self._actions_ptr
+        else:
+            if actions is None:
+                actions = self.actions
+            if actions.dtype != self.torch.float32 or actions.device != self.device or not actions.is_contiguous():
+                actions = actions.to(device=self.device, dtype=self.torch.float32).contiguous()
+            if tuple(actions.shape) != (self.n_envs, self.num_drones, 4):
+                raise ValueError(f"actions must have shape {(self.n_envs, self.num_drones, 4)}, got {tuple(actions.shape)}")
+            self._keep = actions
+            io.actions = actions.data_ptr()
+            io.actions_out = None
+        io.terminal_obs = None
+        io.flags = flags
+        L.check(L.lib().ch_step_n(self.handle, self._io_ref, int(n_steps), self._stream()), self.handle)
+        return self.obs, self.reward, self.terminated, self.truncated
+
     def host_outputs(self, ring=2, ended=True, agents=False):
         """A HostOutputs over this batch: pinned host buffers the last step's outputs are delivered into
         (ch_outputs_to_host), ``ring`` sets of them used in turn."""

@@ -78,6 +78,9 @@ struct ch_handle {
     // bit 2 the actor forward fused into the step kernel (k_step2_actor, where the geometry takes it), bit 3 never fused
     int rollout_path = 0;
     long long fused_steps = 0;   // fused steps launched by ch_rollout_collect (ch__rollout_fused_steps)
+    long long multi_steps = 0;   // steps ch_step_n ran inside k_step2_multi (ch__multi_steps)
+    void* d_params = nullptr;    // k_step2_multi's parameters (device copy, ch_step_n)
+    std::vector<unsigned char> params_host;   // what d_params holds (uploaded again only when the parameters change)
     // ch_outputs_to_host's device staging of the envs that auto-reset (allocated on first use): count, indices,
     // episode statistics, terminal observation blocks; and the pinned host copy of the count
     long long* st_count = nullptr;
@@ -259,9 +262,12 @@ int ch_default_config(ch_config* c, int32_t mode, int32_t num_drones, int32_t nu
 
 const char* ch_last_error(const ch_handle* h) { return h ? h->err.c_str() : g_create_err.c_str(); }
 
+constexpr size_t kParamsBytes = 1024;   // ch_step_n's device copy of StepParams
+
 static void free_all(ch_handle* h) {
     void* ptrs[] = {h->drone, h->rpy, h->cattle, h->phys, h->envr, h->envi, h->metrics, h->spawn, h->pairs,
-                    h->errw, h->mdev, h->stale, h->obs_tag, h->evald, h->rdn, h->rdv, h->pos64, h->cpos64, h->prev64};
+                    h->errw, h->mdev, h->stale, h->obs_tag, h->evald, h->rdn, h->rdv, h->pos64, h->cpos64, h->prev64,
+                    h->d_params};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (void* p : {(void*)h->tv_obs, (void*)h->tv_row, (void*)h->tv_count, (void*)h->tv_val, (void*)h->st_count,
@@ -646,6 +652,65 @@ int ch_step(ch_handle* h, const ch_step_io* io, void* stream) {
     // to flag (HerdBatch.step(obs_out=...) calls invalidate_obs when the tensor changes).
     return CH_OK;
 }
+
+int ch_step_n(ch_handle* h, const ch_step_io* io, int32_t n_steps, void* stream) {
+    if (!h) return fail(nullptr, CH_ERR_INVALID, "ch_step_n: NULL handle");
+    if (n_steps < 1) return fail(h, CH_ERR_INVALID, "ch_step_n: n_steps must be >= 1");
+    if (!io) return fail(h, CH_ERR_INVALID, "ch_step_n: io is NULL");
+    // the same validation as ch_step
+    if (!io->obs || !io->reward || !io->terminated || !io->truncated)
+        return fail(h, CH_ERR_INVALID, "ch_step_n: obs, reward, terminated and truncated are required");
+    if (!(io->flags & CH_STEP_RANDOM_ACTIONS) && !io->actions)
+        return fail(h, CH_ERR_INVALID, "ch_step_n: actions is NULL (and CH_STEP_RANDOM_ACTIONS not set)");
+    if ((io->actions && (reinterpret_cast<uintptr_t>(io->actions) & 15)) || (reinterpret_cast<uintptr_t>(io->obs) & 15) ||
+        (io->terminal_obs && (reinterpret_cast<uintptr_t>(io->terminal_obs) & 15)))
+        return fail(h, CH_ERR_INVALID, "ch_step_n: actions and obs buffers must be 16-byte aligned");
+    HIP_TRY(h, hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    int done = 0, rc = CH_OK;
+    // a buffer whose constant observation bytes are not known to be in place gets one plain step first (it writes
+    // them); every step of the multi-step kernel then finds them there
+    if (io->obs != h->obs_zero_ptr || h->kernel != 2 || h->phase_mask) {
+        if ((rc = ch_step(h, io, stream)) != CH_OK) return rc;
+        done = 1;
+    }
+    if (done == n_steps) return CH_OK;
+    const int rest = n_steps - done;
+    hipError_t e = hipErrorNotSupported;
+    if (h->kernel == 2 && !h->phase_mask) {
+        // the multi-step kernel reads its parameters from a device copy (k_step2_multi), uploaded when they differ
+        // from the last upload (stream-ordered; a pageable source is staged by the runtime before the call returns)
+        if (!h->d_params) HIP_TRY(h, hipMalloc(&h->d_params, kParamsBytes));
+        auto go = [&](auto p) -> hipError_t {
+            fill_step(h, io, p);
+            using P = decltype(p);
+            static_assert(sizeof(P) <= kParamsBytes, "StepParams fits the device copy");
+            const P* pd = static_cast<const P*>(h->d_params);
+            if (launch_step_v2_multi(p, pd, h->block, h->lds, st, rest, false) != hipSuccess) return hipErrorNotSupported;
+            if (h->params_host.size() != sizeof(P) || std::memcmp(h->params_host.data(), &p, sizeof(P)) != 0) {
+                const hipError_t ce = hipMemcpyAsync(h->d_params, &p, sizeof(P), hipMemcpyHostToDevice, st);
+                if (ce != hipSuccess) return ce;
+                h->params_host.assign(reinterpret_cast<const unsigned char*>(&p),
+                                      reinterpret_cast<const unsigned char*>(&p) + sizeof(P));
+            }
+            return launch_step_v2_multi(p, pd, h->block, h->lds, st, rest);
+        };
+        e = h->rsize == sizeof(double) ? go(params<double>(h)) : go(params<float>(h));
+    }
+    if (e == hipSuccess) {
+        h->multi_steps += rest;
+        h->obs_zero_ptr = io->obs;
+        return CH_OK;
+    }
+    if (e != hipErrorNotSupported) return fail(h, CH_ERR_DEVICE, std::string("ch_step_n launch: ") + hipGetErrorString(e));
+    (void)hipGetLastError();
+    for (int k = 0; k < rest; ++k)   // other geometries: one launch per step
+        if ((rc = ch_step(h, io, stream)) != CH_OK) return rc;
+    return CH_OK;
+}
+
+/* Internal (tests): steps ch_step_n has run inside its multi-step kernel on this handle. */
+int64_t ch__multi_steps(const ch_handle* h) { return h ? (int64_t)h->multi_steps : -1; }
 
 int ch_state_size(const ch_handle* h, int64_t* n_doubles, int64_t* n_ints) {
     if (!h) return fail(nullptr, CH_ERR_INVALID, "ch_state_size: NULL handle");

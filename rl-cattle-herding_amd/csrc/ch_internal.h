@@ -256,6 +256,12 @@ template <class R> hipError_t launch_reset(const StepParams<R>& p, int team, hip
 // step captured into a HIP graph needs no host-side setup)
 template <class R> hipError_t launch_step_v2(const StepParams<R>& p, int block, size_t lds, hipStream_t st,
                                              bool launch = true);
+// ch_step_n: n consecutive steps of the same io in one launch (k_step2_multi), for the BASELINE geometries under PYB
+// without terminal observations; hipErrorNotSupported (nothing launched) elsewhere.  launch = false: the attribute
+// opt-in only.
+// `pd`: a device copy of p (the kernel reads its parameters from it).
+template <class R> hipError_t launch_step_v2_multi(const StepParams<R>& p, const StepParams<R>* pd, int block, size_t lds,
+                                                   hipStream_t st, int n_steps, bool launch = true);
 // ch_rollout_collect's fused step (k_step2_actor): the step of the CTDE 16-env x 4-drone x 16-cattle geometry (f64,
 // CH_V2_MAX_BLOCK threads) followed in each workgroup by the actor forward with the sampling epilogue on the 16
 // observation rows it wrote.  hipErrorNotSupported (nothing launched) when the handle's geometry or the net does not

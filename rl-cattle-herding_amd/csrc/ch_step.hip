@@ -769,9 +769,13 @@ __device__ __forceinline__ void flock_combine(const StepParams<R>& p, V2Smem<R>&
 // geometry, launched when the step asks for them); without it the same geometry takes the drained-copy path for them
 // The f32 geometry-specialised kernels keep 4 waves per SIMD (<= 128 VGPRs): their f64 torque path (ch_device.h
 // drone_substep) would otherwise take them to 135 and 3 waves, one resident workgroup fewer per CU at large E.
+// salt: 0.  k_step2_multi passes an opaque 0 per step (an empty asm's output), so that the values derived from the
+// thread / workgroup indices and the LDS carve are computed inside each step instead of being hoisted out of its step
+// loop and held across it (which overflowed the registers); k_step2's constant 0 folds away.
 template <class R, int MODE, int GT, int NT, int MT, bool PHYS, bool PW, bool TOBS>
-__device__ __forceinline__ void step2_body(const StepParams<R>& p) {
-    extern __shared__ __align__(16) unsigned char smem[];
+__device__ __forceinline__ void step2_body(const StepParams<R>& p, int salt = 0) {
+    extern __shared__ __align__(16) unsigned char smem_[];
+    unsigned char* const smem = smem_ + salt;
     constexpr bool marl = MODE == 1;
     // f32 mode: positions, centroids and the approach delta in f64 (StepParams::pos64); PT = their type
     constexpr bool MIX = sizeof(R) == 4;
@@ -807,8 +811,8 @@ __device__ __forceinline__ void step2_body(const StepParams<R>& p) {
     const V2Layout L(G, N, M, P, MODE, (int)sizeof(R), PW ? (int)(blockDim.x >> 6) - 1 : 0, !PW && p.sep);
     const bool sep = L.sep;
     V2Smem<R> S(smem, L);
-    const int BS = blockDim.x, tid = threadIdx.x;
-    const int e0 = blockIdx.x * G;
+    const int BS = blockDim.x + salt, tid = threadIdx.x + salt;
+    const int e0 = (blockIdx.x + salt) * G;
     const int Gv = min(G, p.E - e0);
     const long long E = p.E, DS = E * N, CS = E * M;
     const int m_obs = M < 16 ? M : 16, cat_off = marl ? 18 : 34, RW = rows * 86;
@@ -2160,6 +2164,7 @@ __device__ __forceinline__ void step2_body(const StepParams<R>& p) {
     }
 }
 
+#ifndef CH_STEP_BODY_ONLY   // (ch_step_multi.hip includes this file for step2_body alone)
 template <class R, int MODE, int GT, int NT, int MT, bool PHYS = false, bool PW = false, bool TOBS = false>
 __global__ __launch_bounds__((PW || PHYS) ? CH_V2_MAX_BLOCK_PW : CH_V2_MAX_BLOCK)
 __attribute__((amdgpu_waves_per_eu((sizeof(R) == 4 && GT > 0 && !PW && !PHYS) ? 4 : 1)))
@@ -2301,5 +2306,7 @@ template hipError_t launch_step_v2_actor<double>(const StepParams<double>&, int,
 template hipError_t launch_step_v2_actor<float>(const StepParams<float>&, int, size_t, hipStream_t, const MlpArgs&,
                                                 const RolloutArgs&, bool);
 template hipError_t launch_step_v2<float>(const StepParams<float>&, int, size_t, hipStream_t, bool);
+
+#endif   // CH_STEP_BODY_ONLY
 
 }  // namespace ch

@@ -170,3 +170,54 @@ def test_handoff_timeout_is_reported_not_silent():
     torch.cuda.synchronize()
     for h in (ok, bad):
         h.close()
+
+
+@pytest.mark.parametrize("mode,n,m,E,prec,multi", [("ctde", 4, 16, 4096, "f64", True), ("ctde", 2, 8, 4096, "f64", True),
+                                                   ("ctde", 2, 8, 1024, "f64", True), ("marl", 4, 32, 4096, "f64", True),
+                                                   ("ctde", 4, 16, 4096, "f32", True), ("ctde", 3, 8, 300, "f64", False)])
+def test_step_n_equals_n_steps(mode, n, m, E, prec, multi):
+    """ch_step_n (k_step2_multi: each workgroup steps its envs back to back inside one launch) against the same number
+    of ch_step calls: state, last outputs, metrics and the device-drawn actions bit for bit, with auto-resets inside the
+    window (envs burnt in first so that episodes end at their long-run rate).  `multi`: the geometry has the multi-step
+    kernel (the BASELINE ones); elsewhere ch_step_n falls back to one launch per step, with the same result."""
+    import torch
+    from cattleherd import _lib
+    L = _lib.lib()
+    a, b = _pair(mode, n, m, E, precision=prec)
+    for h in (a, b):
+        h.reset()
+        for _ in range(140):
+            h.step(random_actions=True, autoreset=True, terminal_obs=False)
+    torch.cuda.synchronize()
+    assert _same(_outs(a), _outs(b))
+    K = 23
+    m0 = L.ch__multi_steps(a.handle)
+    ep0 = a.metrics()[1]
+    a.step_n(K, random_actions=True)
+    for _ in range(K):
+        b.step(random_actions=True, autoreset=True, terminal_obs=False)
+    torch.cuda.synchronize()
+    assert (L.ch__multi_steps(a.handle) - m0 == K) == multi   # (the buffer's constant bytes are in place: no plain step)
+    assert _same(_outs(a), _outs(b))
+    assert torch.equal(a.actions, b.actions)
+    sa, sb = a.get_state(), b.get_state()
+    for k in sa:
+        assert np.array_equal(np.asarray(sa[k]), np.asarray(sb[k]), equal_nan=True), k
+    assert np.array_equal(a.metrics(), b.metrics(), equal_nan=True)
+    # episodes ended (auto-resets) inside the window: CTDE at these sizes resets a few envs per step
+    assert a.metrics()[1] > ep0 or mode == "marl"
+    # a buffer whose constant observation bytes are unknown (invalidate_obs): one plain step first, then the kernel
+    m1 = L.ch__multi_steps(a.handle)
+    a.invalidate_obs()
+    b.invalidate_obs()
+    a.step_n(5, random_actions=True)
+    for _ in range(5):
+        b.step(random_actions=True, autoreset=True, terminal_obs=False)
+    torch.cuda.synchronize()
+    assert (L.ch__multi_steps(a.handle) - m1 == 4) == multi
+    assert _same(_outs(a), _outs(b))
+    sa, sb = a.get_state(), b.get_state()
+    for k in sa:
+        assert np.array_equal(np.asarray(sa[k]), np.asarray(sb[k]), equal_nan=True), k
+    a.close()
+    b.close()

@@ -33,10 +33,14 @@ def trace(mode, E, n, m, prec, G=None, B=None, steps=4, summary=None):
     if os.environ.get("CH_PHASE_MASK"):
         L.ch__set_phase_mask(b.handle, ctypes.c_int32(int(os.environ["CH_PHASE_MASK"])))
     print(f"== {prec} {mode} E={E} N={n} M={m} G={g.value} block={blk.value} lds={lds.value} grid={grid}")
+    multi = bool(os.environ.get("CH_TRACE_MULTI"))   # ch_step_n's k_step2_multi: the stamps of a launch's third step
     for s in range(steps):
         ts.zero_()
         torch.cuda.synchronize()
-        b.step(random_actions=True, autoreset=True, terminal_obs=False)
+        if multi:
+            b.step_n(3, random_actions=True)
+        else:
+            b.step(random_actions=True, autoreset=True, terminal_obs=False)
         torch.cuda.synchronize()
         t = ts.cpu().numpy()
         w0, w1 = t[:, 0], t[:, 1]
