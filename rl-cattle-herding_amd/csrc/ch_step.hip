@@ -1059,6 +1059,15 @@ __device__ __forceinline__ void step2_body(const StepParams<R>& p, int salt = 0)
 #pragma unroll
                     for (int c = 0; c < 3; ++c) CH_STS(&p.phys[(4 + c) * DS + di], ph_rr[c]);
                 } else {
+#ifdef CH_SUBSTEP_UNROLL
+                    // (ch_step_multi.hip: its translation unit runs without machine LICM; the default 4 substeps
+                    // straight-line keep the loop-invariant parts of the substep out of a loop there)
+                    if (p.substeps == 4) {
+                        CH_UNROLL for (int s = 0; s < 4; ++s)
+                            drone_substep(pos, q, v, w, rpm, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0,
+                                          NoExtraForces(), MIX ? pd : nullptr, ql, zl, p.link_lag != 0);
+                    } else
+#endif
                     for (int s = 0; s < p.substeps; ++s)
                         drone_substep(pos, q, v, w, rpm, R(p.dt), R(p.damping), p.torque_world != 0, p.gyro != 0,
                                       NoExtraForces(), MIX ? pd : nullptr, ql, zl, p.link_lag != 0);

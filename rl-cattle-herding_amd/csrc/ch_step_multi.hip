@@ -30,7 +30,10 @@ __device__ __forceinline__ void step2_once(const StepParams<R>* p, int salt) {
 }
 // n consecutive steps in one launch (ch_step_n); `pd`: the step's parameters in device memory
 template <class R, int MODE, int GT, int NT, int MT, bool PHYS = false, bool PW = false>
-__global__ __launch_bounds__(CH_V2_MAX_BLOCK_PW)
+#ifndef CH_MULTI_MAX_BLOCK
+#define CH_MULTI_MAX_BLOCK CH_V2_MAX_BLOCK_PW   // 512 threads: 2 waves per SIMD (A/B)
+#endif
+__global__ __launch_bounds__(PW ? CH_V2_MAX_BLOCK_PW : CH_MULTI_MAX_BLOCK)
 void k_step2_multi(const StepParams<R>* __restrict__ pd, int n_steps) {
     for (int k = 0; k < n_steps; ++k) {
         int salt = 0;
@@ -62,7 +65,7 @@ static hipError_t launch_v2_multi_kernel(const StepParams<R>& p, const StepParam
     dim3 grid((p.E + p.G - 1) / p.G);
     // at most 8 waves: the step loop needs the registers of 2 waves per SIMD (at 3 per SIMD, 768 threads, the loop's
     // longer live ranges spilled); the cow waves share their work out dynamically, so the outputs do not depend on it
-    hipLaunchKernelGGL((k_step2_multi<R, MODE, GT, NT, MT, PHYS, PW>), grid, dim3(block < CH_V2_MAX_BLOCK_PW ? block : CH_V2_MAX_BLOCK_PW),
+    hipLaunchKernelGGL((k_step2_multi<R, MODE, GT, NT, MT, PHYS, PW>), grid, dim3(block < (PW ? CH_V2_MAX_BLOCK_PW : CH_MULTI_MAX_BLOCK) ? block : (PW ? CH_V2_MAX_BLOCK_PW : CH_MULTI_MAX_BLOCK)),
                        lds, st, pd, n_steps);
     return hipGetLastError();
 }
@@ -82,6 +85,7 @@ hipError_t launch_step_v2_multi(const StepParams<R>& p, const StepParams<R>* pd,
         }
         if (p.mode != 0) return hipErrorNotSupported;
         if (G == 16 && N == 4 && M == 16) return launch_v2_multi_kernel<R, 0, 16, 4, 16>(p, pd, block, lds, st, n_steps, launch);   // configs[3]
+        if (G == 8 && N == 4 && M == 16) return launch_v2_multi_kernel<R, 0, 8, 4, 16>(p, pd, block, lds, st, n_steps, launch);     // configs[3], 2 per CU
         if (G == 16 && N == 2 && M == 8) return launch_v2_multi_kernel<R, 0, 16, 2, 8>(p, pd, block, lds, st, n_steps, launch);     // configs[2]
         if (G == 4 && N == 2 && M == 8) return launch_v2_multi_kernel<R, 0, 4, 2, 8>(p, pd, block, lds, st, n_steps, launch);       // configs[1]
         return hipErrorNotSupported;
