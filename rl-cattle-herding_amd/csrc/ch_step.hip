@@ -108,12 +108,27 @@ __device__ __forceinline__ int lds_peek(int* f) {
 __device__ __forceinline__ void handoff_failed(int* err) {
     if (err && (threadIdx.x & 63) == 0) atomicOr(err, CH_DEVERR_HANDOFF);
 }
+// diagnostics (-DCH_COUNT_SPINS builds only, tools/spin_split.py): sleep iterations of the hand-off waits, per wave
+// kind (drone wave, cow waves), and the number of waits, summed over every k_step2 launch since the last read
+#ifdef CH_COUNT_SPINS
+static __device__ unsigned long long g_ch_spins[4];
+__device__ __forceinline__ void spin_note(int n) {
+    if ((threadIdx.x & 63) == 0) {
+        const int w = threadIdx.x < 64 ? 0 : 1;
+        atomicAdd(&g_ch_spins[w], (unsigned long long)n);
+        atomicAdd(&g_ch_spins[2 + w], 1ull);
+    }
+}
+#else
+__device__ __forceinline__ void spin_note(int) {}
+#endif
 // spin until *f >= target (bounded, about 0.1 s)
 __device__ __forceinline__ void lds_wait(int* f, int target, int* err) {
     int spins = 0;
     while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target && ++spins < (1 << 22))
         __builtin_amdgcn_s_sleep(1);
     if (spins >= (1 << 22)) handoff_failed(err);
+    spin_note(spins);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
@@ -448,13 +463,15 @@ __device__ __forceinline__ void alpha_full(V2Smem<R>& S, int* fl, int M, int P, 
         if (b >= (1 << 28)) break;   // (skip)
         int qn = 0;
         bool done = false;
-        for (int spins = 0;; ++spins) {
+        int spins = 0;
+        for (;; ++spins) {
             done = lds_peek(fl + F_C) >= W1;      // F_C before Q_LEN: once every wave is done, Q_LEN is final
             qn = lds_peek(fl + Q_LEN);
             if (done || qn >= b + 64) break;
             if (spins >= (1 << 22)) { handoff_failed(err); done = true; break; }
             __builtin_amdgcn_s_sleep(1);
         }
+        spin_note(spins);
         if (b >= qn) break;   // done: no slot of this chunk was ever reserved
 #else
         if (b >= qn) break;
@@ -967,10 +984,12 @@ __device__ __forceinline__ void step2_body(const StepParams<R>& p, int salt = 0)
         cow_sync(fl + F_E, W1, false, p.err);   // env scalars, flocking list, tables: seen by every cow wave
         {
             int ds = lds_peek(fl + V_DSIMD);
-            for (int spins = 0; ds == 0 && spins < (1 << 22); ++spins) {   // stored by the drone wave at its start
+            int spins = 0;
+            for (; ds == 0 && spins < (1 << 22); ++spins) {   // stored by the drone wave at its start
                 __builtin_amdgcn_s_sleep(1);
                 ds = lds_peek(fl + V_DSIMD);
             }
+            spin_note(spins);
             co_simd = (int)((__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3) + 1 == ds;
         }
         if (ct == 0) TS(11, (long long)clock64());
@@ -1790,9 +1809,10 @@ __device__ __forceinline__ void step2_body(const StepParams<R>& p, int salt = 0)
             lds_signal(fl + F_A);
             // alpha rows while the drone wave still integrates: once every pair is in the table, row chunks
             // are taken until the drone positions arrive; the rest follows the drone hand-off below
+            int sleeps = 0;
             for (int spins = 0; spins < (1 << 22); ++spins) {
                 if (lds_peek(fl + F_D) >= 1) break;
-                if (lds_peek(fl + F_A) < W1) { __builtin_amdgcn_s_sleep(1); continue; }
+                if (lds_peek(fl + F_A) < W1) { __builtin_amdgcn_s_sleep(1); ++sleeps; continue; }
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");   // the pair table
                 const int b = grab(fl + C_ROWS, 64, skip_pre), u = b + lane;
                 if (b >= nf * M) break;
@@ -1804,6 +1824,7 @@ __device__ __forceinline__ void step2_body(const StepParams<R>& p, int salt = 0)
                 }
                 CHUNK_T1(2);
             }
+            spin_note(sleeps);
         }
         if (ct == 0) TS(8, (long long)clock64());
         lds_wait(fl + F_D, 1, p.err);
@@ -2308,6 +2329,17 @@ hipError_t launch_step_v2_actor(const StepParams<R>& p, int block, size_t lds, h
                               : launch_actor_kernel<R, false>(p, block, l, st, f, launch);
     }
 }
+
+#ifdef CH_COUNT_SPINS
+// (diagnostic builds) read and clear the k_step2 spin counters: out[0..3] = drone-wave sleeps, cow-wave sleeps,
+// drone-wave waits, cow-wave waits
+extern "C" int ch__spin_counts(unsigned long long* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ch_spins), sizeof(g_ch_spins)) != hipSuccess) return -1;
+    const unsigned long long z[4] = {0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_ch_spins), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 template hipError_t launch_step_v2<double>(const StepParams<double>&, int, size_t, hipStream_t, bool);
 template hipError_t launch_step_v2_actor<double>(const StepParams<double>&, int, size_t, hipStream_t, const MlpArgs&,

@@ -172,18 +172,27 @@ def test_handoff_timeout_is_reported_not_silent():
         h.close()
 
 
-@pytest.mark.parametrize("mode,n,m,E,prec,multi", [("ctde", 4, 16, 4096, "f64", True), ("ctde", 2, 8, 4096, "f64", True),
-                                                   ("ctde", 2, 8, 1024, "f64", True), ("marl", 4, 32, 4096, "f64", True),
-                                                   ("ctde", 4, 16, 4096, "f32", True), ("ctde", 3, 8, 300, "f64", False)])
-def test_step_n_equals_n_steps(mode, n, m, E, prec, multi):
+@pytest.mark.parametrize("mode,n,m,E,prec,multi,geom", [("ctde", 4, 16, 4096, "f64", True, None),
+                                                        ("ctde", 2, 8, 4096, "f64", True, None),
+                                                        ("ctde", 2, 8, 1024, "f64", True, None),
+                                                        ("marl", 4, 32, 4096, "f64", True, None),
+                                                        ("ctde", 4, 16, 4096, "f32", True, None),
+                                                        ("ctde", 3, 8, 300, "f64", False, None),
+                                                        ("ctde", 4, 16, 4096, "f64", True, (8, 256)),
+                                                        ("ctde", 4, 16, 1001, "f64", True, (8, 256))])
+def test_step_n_equals_n_steps(mode, n, m, E, prec, multi, geom):
     """ch_step_n (k_step2_multi: each workgroup steps its envs back to back inside one launch) against the same number
     of ch_step calls: state, last outputs, metrics and the device-drawn actions bit for bit, with auto-resets inside the
     window (envs burnt in first so that episodes end at their long-run rate).  `multi`: the geometry has the multi-step
-    kernel (the BASELINE ones); elsewhere ch_step_n falls back to one launch per step, with the same result."""
+    kernel (the BASELINE ones); elsewhere ch_step_n falls back to one launch per step, with the same result.  `geom`:
+    the multi-step handle runs that workgroup geometry (8-env workgroups, two per CU), the plain one the default."""
+    import ctypes
     import torch
     from cattleherd import _lib
     L = _lib.lib()
     a, b = _pair(mode, n, m, E, precision=prec)
+    if geom is not None:
+        assert L.ch__set_geometry(a.handle, ctypes.c_int32(geom[0]), ctypes.c_int32(geom[1])) == 0
     for h in (a, b):
         h.reset()
         for _ in range(140):
