@@ -301,18 +301,21 @@ def marl_ppo_rollout(b, T=32):
     return out
 
 
-def near_herd_leg(b, n, m, reps=8, steps=100, burn=10, seed=11):
+def near_herd_leg(b, n, m, reps=8, steps=100, burn=10, seed=11, multi=False):
     """configs[4] at training conditions: the headline's random actions drive the drones away from the herd (the
     steady state is ~96 % truncated agent-steps with every cow-drone pair beyond the predator range, where the
     shepherd term takes its far-drone closed form).  Here, `reps` times, every env's drones are put 0.6-1.4 m from a
     random cow of their herd (set_state, untimed), `burn` untimed steps run, then `steps` timed steps: the flock's
     near-drone shepherd and predator terms and the task's non-truncated paths run as in training.  Reports the rate
-    and, from each window's first state, the share of cow-drone pairs within 1 m (mu < 1) and 1.1 m (predator)."""
+    and, from each window's first state, the share of cow-drone pairs within 1 m (mu < 1) and 1.1 m (predator).
+    `multi` (the headline ran ch_step_n): each window also runs from the same state through ch_step_n -- one plain
+    step after the state restore, then one k_step2_multi launch of the rest -- and that is the reported rate, with
+    the single-launch one beside it."""
     import numpy as np
     import torch
     rng = np.random.default_rng(seed)
     E = b.n_envs
-    times, near1, pred, ends, trunc, steps_done = [], [], [], 0.0, 0.0, 0.0
+    times, times_n, near1, pred, ends, trunc, steps_done = [], [], [], [], 0.0, 0.0, 0.0
     for _ in range(reps):
         s = b.get_state()
         cows = s["cow_pos"][:, :m]
@@ -331,6 +334,7 @@ def near_herd_leg(b, n, m, reps=8, steps=100, burn=10, seed=11):
         live = np.arange(n)[None, :, None] < g["n"][:, None, None]
         near1.append(float((d[np.broadcast_to(live, d.shape)] < 1.0).mean()))
         pred.append(float((d[np.broadcast_to(live, d.shape)] <= 1.1).mean()))
+        s0 = b.get_state_raw() if multi else None
         b.metrics(reset=True)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -340,8 +344,23 @@ def near_herd_leg(b, n, m, reps=8, steps=100, burn=10, seed=11):
         times.append(time.perf_counter() - t0)
         mv = b.metrics(reset=True)
         ends += mv[1]; trunc += mv[5]; steps_done += mv[0]
+        if multi:   # the same window from the same state through ch_step_n (the headline's form)
+            b.set_state_raw(*s0)
+            b.step_n(1, random_actions=True)   # (set_state rewrote the observation blocks: one plain step)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            b.step_n(steps - 1, random_actions=True)
+            torch.cuda.synchronize()
+            times_n.append((time.perf_counter() - t0) * steps / (steps - 1))
+            b.metrics(reset=True)
     dt = float(np.sum(times))
-    return {"env_steps_per_s": E * steps * reps / dt, "us_per_step": dt / (steps * reps) * 1e6,
+    out = {"env_steps_per_s": E * steps * reps / dt, "us_per_step": dt / (steps * reps) * 1e6}
+    if multi:
+        dn = float(np.sum(times_n))
+        out = {"env_steps_per_s": E * steps * reps / dn, "us_per_step": dn / (steps * reps) * 1e6,
+               "launch": "ch_step_n (k_step2_multi), the same windows from the same states as the single-launch figure",
+               "single_launch": out}
+    return {**out,
             "windows": reps, "steps_per_window": steps, "untimed_steps_after_placement": burn,
             "cow_drone_pairs_within_1m": float(np.mean(near1)), "cow_drone_pairs_within_1.1m": float(np.mean(pred)),
             "episode_ends": ends, "truncated_agent_step_fraction": trunc / max(steps_done * n, 1.0),
@@ -771,7 +790,7 @@ def main():
         if args.policy and mode == "marl":
             out["marl_ppo_rollout"] = marl_ppo_rollout(b)
         if mode == "marl" and not args.no_extras:
-            out["near_herd_leg"] = near_herd_leg(b, n, m)
+            out["near_herd_leg"] = near_herd_leg(b, n, m, multi=multi_ran)
         if args.marl_vec and mode == "marl":
             b.close()
             out["marl_vec_env"] = marl_vec_rollout(n, m, E, args.steps, args.warmup, args.burn_in)
