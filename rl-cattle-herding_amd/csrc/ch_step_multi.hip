@@ -29,11 +29,15 @@ __device__ __forceinline__ void step2_once(const StepParams<R>* p, int salt) {
     step2_body<R, MODE, GT, NT, MT, PHYS, PW, false>(*(const StepParams<R>*)kp, salt);
 }
 // n consecutive steps in one launch (ch_step_n); `pd`: the step's parameters in device memory
-template <class R, int MODE, int GT, int NT, int MT, bool PHYS = false, bool PW = false>
+// WPE: the waves per SIMD the registers are allocated for (4: two workgroups per CU, for grids of more workgroups than
+// CUs -- the f32 mode at 262 144 envs: 395.5 vs 294.4 M env-steps/s; at 4096 envs, one workgroup per CU, the register
+// cap only spills: 261.9 vs 297.2 M, profiles/r06/ab/r6n_*)
 #ifndef CH_MULTI_MAX_BLOCK
 #define CH_MULTI_MAX_BLOCK CH_V2_MAX_BLOCK_PW   // 512 threads: 2 waves per SIMD (A/B)
 #endif
+template <class R, int MODE, int GT, int NT, int MT, bool PHYS = false, bool PW = false, int WPE = 1>
 __global__ __launch_bounds__(PW ? CH_V2_MAX_BLOCK_PW : CH_MULTI_MAX_BLOCK)
+__attribute__((amdgpu_waves_per_eu(WPE)))
 void k_step2_multi(const StepParams<R>* __restrict__ pd, int n_steps) {
     for (int k = 0; k < n_steps; ++k) {
         int salt = 0;
@@ -47,7 +51,7 @@ void k_step2_multi(const StepParams<R>* __restrict__ pd, int n_steps) {
     }
 }
 
-template <class R, int MODE, int GT, int NT, int MT, bool PHYS = false, bool PW = false>
+template <class R, int MODE, int GT, int NT, int MT, bool PHYS = false, bool PW = false, int WPE = 1>
 static hipError_t launch_v2_multi_kernel(const StepParams<R>& p, const StepParams<R>* pd, int block, size_t lds,
                                          hipStream_t st, int n_steps, bool launch) {
     static std::atomic<unsigned long long> attr_set{0};
@@ -56,7 +60,7 @@ static hipError_t launch_v2_multi_kernel(const StepParams<R>& p, const StepParam
     if (e != hipSuccess) return e;
     const unsigned long long bit = 1ull << (dev & 63);
     if (!(attr_set.load(std::memory_order_relaxed) & bit)) {
-        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_step2_multi<R, MODE, GT, NT, MT, PHYS, PW>),
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_step2_multi<R, MODE, GT, NT, MT, PHYS, PW, WPE>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr_set.fetch_or(bit, std::memory_order_relaxed);
@@ -65,7 +69,7 @@ static hipError_t launch_v2_multi_kernel(const StepParams<R>& p, const StepParam
     dim3 grid((p.E + p.G - 1) / p.G);
     // at most 8 waves: the step loop needs the registers of 2 waves per SIMD (at 3 per SIMD, 768 threads, the loop's
     // longer live ranges spilled); the cow waves share their work out dynamically, so the outputs do not depend on it
-    hipLaunchKernelGGL((k_step2_multi<R, MODE, GT, NT, MT, PHYS, PW>), grid, dim3(block < (PW ? CH_V2_MAX_BLOCK_PW : CH_MULTI_MAX_BLOCK) ? block : (PW ? CH_V2_MAX_BLOCK_PW : CH_MULTI_MAX_BLOCK)),
+    hipLaunchKernelGGL((k_step2_multi<R, MODE, GT, NT, MT, PHYS, PW, WPE>), grid, dim3(block < (PW ? CH_V2_MAX_BLOCK_PW : CH_MULTI_MAX_BLOCK) ? block : (PW ? CH_V2_MAX_BLOCK_PW : CH_MULTI_MAX_BLOCK)),
                        lds, st, pd, n_steps);
     return hipGetLastError();
 }
@@ -90,8 +94,17 @@ hipError_t launch_step_v2_multi(const StepParams<R>& p, const StepParams<R>* pd,
         if (G == 4 && N == 2 && M == 8) return launch_v2_multi_kernel<R, 0, 4, 2, 8>(p, pd, block, lds, st, n_steps, launch);       // configs[1]
         return hipErrorNotSupported;
     } else {
-        if (!p.pw && p.mode == 0 && G == 16 && N == 4 && M == 16)
+        if (!p.pw && p.mode == 0 && G == 16 && N == 4 && M == 16) {
+            // two workgroups per CU once the grid has them (more than 256 workgroups); attribute opt-in for both at
+            // ch_create (launch == false)
+            if (!launch) {
+                const hipError_t e = launch_v2_multi_kernel<R, 0, 16, 4, 16, false, false, 4>(p, pd, block, lds, st, n_steps, false);
+                if (e != hipSuccess) return e;
+            }
+            if ((p.E + G - 1) / G > 256)
+                return launch_v2_multi_kernel<R, 0, 16, 4, 16, false, false, 4>(p, pd, block, lds, st, n_steps, launch);
             return launch_v2_multi_kernel<R, 0, 16, 4, 16>(p, pd, block, lds, st, n_steps, launch);
+        }
         return hipErrorNotSupported;
     }
 }

@@ -177,6 +177,7 @@ def test_handoff_timeout_is_reported_not_silent():
                                                         ("ctde", 2, 8, 1024, "f64", True, None),
                                                         ("marl", 4, 32, 4096, "f64", True, None),
                                                         ("ctde", 4, 16, 4096, "f32", True, None),
+                                                        ("ctde", 4, 16, 8200, "f32", True, None),
                                                         ("ctde", 3, 8, 300, "f64", False, None),
                                                         ("ctde", 4, 16, 4096, "f64", True, (8, 256)),
                                                         ("ctde", 4, 16, 1001, "f64", True, (8, 256))])
@@ -185,7 +186,8 @@ def test_step_n_equals_n_steps(mode, n, m, E, prec, multi, geom):
     of ch_step calls: state, last outputs, metrics and the device-drawn actions bit for bit, with auto-resets inside the
     window (envs burnt in first so that episodes end at their long-run rate).  `multi`: the geometry has the multi-step
     kernel (the BASELINE ones); elsewhere ch_step_n falls back to one launch per step, with the same result.  `geom`:
-    the multi-step handle runs that workgroup geometry (8-env workgroups, two per CU), the plain one the default."""
+    the multi-step handle runs that workgroup geometry (8-env workgroups, two per CU), the plain one the default.  f32
+    at 8200 envs: more workgroups than CUs, the instantiation allocated for two workgroups per CU."""
     import ctypes
     import torch
     from cattleherd import _lib
