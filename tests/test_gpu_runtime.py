@@ -172,6 +172,37 @@ def test_handoff_timeout_is_reported_not_silent():
         h.close()
 
 
+@pytest.mark.parametrize("mode,n,m,E,autoreset", [("ctde", 4, 16, 4096, True), ("ctde", 4, 16, 4096, False),
+                                                   ("marl", 4, 32, 4096, True), ("ctde", 2, 8, 1024, True)])
+def test_step_n_given_actions(mode, n, m, E, autoreset):
+    """ch_step_n with caller actions (the same action buffer every step, as n ch_step calls with it) and with
+    auto-reset on or off: state, outputs and metrics equal to n ch_step calls bit for bit, the multi-step kernel ran."""
+    import torch
+    from cattleherd import _lib
+    L = _lib.lib()
+    a, b = _pair(mode, n, m, E)
+    for h in (a, b):
+        h.reset()
+        for _ in range(60):
+            h.step(random_actions=True, autoreset=True, terminal_obs=False)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    act = (torch.rand((E, n, 4), generator=g) * 2 - 1).to(a.device)
+    K = 17
+    m0 = L.ch__multi_steps(a.handle)
+    a.step_n(K, actions=act, autoreset=autoreset, random_actions=False)
+    for _ in range(K):
+        b.step(act, random_actions=False, autoreset=autoreset, terminal_obs=False)
+    torch.cuda.synchronize()
+    assert L.ch__multi_steps(a.handle) - m0 == K
+    assert _same(_outs(a), _outs(b))
+    sa, sb = a.get_state(), b.get_state()
+    for k in sa:
+        assert np.array_equal(np.asarray(sa[k]), np.asarray(sb[k]), equal_nan=True), k
+    assert np.array_equal(a.metrics(), b.metrics(), equal_nan=True)
+    a.close()
+    b.close()
+
+
 @pytest.mark.parametrize("mode,n,m,E,prec,multi,geom", [("ctde", 4, 16, 4096, "f64", True, None),
                                                         ("ctde", 2, 8, 4096, "f64", True, None),
                                                         ("ctde", 2, 8, 1024, "f64", True, None),
