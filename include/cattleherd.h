@@ -164,11 +164,12 @@ typedef struct ch_step_io {
 int ch_step(ch_handle* h, const ch_step_io* io, void* stream);
 
 /* n_steps consecutive ch_step calls with the same io, in as few launches as the geometry allows: the steps run in one
- * launch in which every workgroup steps its envs back to back (k_step2_multi, DESIGN.md 4.1) -- the BASELINE
+ * launch in which every workgroup steps its envs back to back (k_step2_multi, DESIGN.md 4.1b) -- the BASELINE
  * geometries under PYB without terminal observations; elsewhere one launch per step.  A buffer whose constant
  * observation bytes are not known to be in place (first use, after ch_set_state / invalidation) gets one plain
  * ch_step first.  The kernel reads its parameters from a device copy that is re-uploaded (stream-ordered) when they
- * change: use one stream per handle.  The outputs in io are those of the last step; state, auto-resets, metrics and the device-drawn
+ * change (from host memory, staged by the runtime at the call): use one stream per handle.  Under stream capture
+ * (a HIP graph) the call records n_steps plain ch_step launches instead.  The outputs in io are those of the last step; state, auto-resets, metrics and the device-drawn
  * random actions (CH_STEP_RANDOM_ACTIONS: each step draws its own) equal n_steps ch_step calls bit for bit.  For
  * random-action rollouts and data generation; a policy that reads each step's observation calls ch_step.
  * Replaces: n_steps iterations of the reference's env.step loop (BaseAviary.step, sb3_envs/BaseAviary.py:335-465). */

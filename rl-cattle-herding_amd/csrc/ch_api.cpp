@@ -668,6 +668,15 @@ int ch_step_n(ch_handle* h, const ch_step_io* io, int32_t n_steps, void* stream)
     HIP_TRY(h, hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
     int done = 0, rc = CH_OK;
+    // under stream capture: n_steps plain launches (a captured multi-step launch would read the handle's parameter copy
+    // as a later call left it, and the upload's host source would not outlive the call)
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cap) != hipSuccess) { (void)hipGetLastError(); cap = hipStreamCaptureStatusNone; }
+    if (cap != hipStreamCaptureStatusNone) {
+        for (int k = 0; k < n_steps; ++k)
+            if ((rc = ch_step(h, io, stream)) != CH_OK) return rc;
+        return CH_OK;
+    }
     // a buffer whose constant observation bytes are not known to be in place gets one plain step first (it writes
     // them); every step of the multi-step kernel then finds them there
     if (io->obs != h->obs_zero_ptr || h->kernel != 2 || h->phase_mask) {

@@ -172,6 +172,48 @@ def test_handoff_timeout_is_reported_not_silent():
         h.close()
 
 
+def test_step_n_under_graph_capture():
+    """ch_step_n inside a HIP graph capture records plain ch_step launches (no multi-step launch, no parameter
+    upload in the graph): two replays equal 2 x K ch_step calls bit for bit, also after a ch_step_n of other io
+    (which re-uploads the handle's parameter copy) ran between them."""
+    import torch
+    from cattleherd import _lib
+    L = _lib.lib()
+    a, b = _pair("ctde", 4, 16, 4096)
+    for h in (a, b):
+        h.reset()
+        for _ in range(30):
+            h.step(random_actions=True, autoreset=True, terminal_obs=False)
+    torch.cuda.synchronize()
+    K = 6
+    m0 = L.ch__multi_steps(a.handle)
+    side = torch.cuda.Stream(device=a.device)
+    side.wait_stream(torch.cuda.current_stream(a.device))
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(graph, stream=side):
+            a.step_n(K, random_actions=True)
+    torch.cuda.current_stream(a.device).wait_stream(side)
+    torch.cuda.synchronize()
+    assert L.ch__multi_steps(a.handle) == m0   # nothing ran, no multi-step launch recorded
+    graph.replay()
+    act = torch.zeros((4096, 4, 4), device=a.device)
+    a.step_n(3, actions=act, random_actions=False)   # other parameters: the device copy is rewritten
+    graph.replay()
+    for _ in range(K):
+        b.step(random_actions=True, autoreset=True, terminal_obs=False)
+    b.step_n(3, actions=act, random_actions=False)
+    for _ in range(K):
+        b.step(random_actions=True, autoreset=True, terminal_obs=False)
+    torch.cuda.synchronize()
+    assert _same(_outs(a), _outs(b))
+    sa, sb = a.get_state(), b.get_state()
+    for k in sa:
+        assert np.array_equal(np.asarray(sa[k]), np.asarray(sb[k]), equal_nan=True), k
+    a.close()
+    b.close()
+
+
 @pytest.mark.parametrize("mode,n,m,E,autoreset", [("ctde", 4, 16, 4096, True), ("ctde", 4, 16, 4096, False),
                                                    ("marl", 4, 32, 4096, True), ("ctde", 2, 8, 1024, True)])
 def test_step_n_given_actions(mode, n, m, E, autoreset):
