@@ -854,16 +854,31 @@ __device__ __forceinline__ void step2_body(const StepParams<R>& p, int salt = 0)
     int stepi = 0, n0 = 0, act0 = 0, stepi_env = 0;
     double ev_acc = 0;   // update_evaluation_metrics' distance of this drone (optional)
     R spx_r[3] = {0, 0, 0}, spy_r[3] = {0, 0, 0};   // cow waves: prefetched spawn positions
-    bool rpy_valid = false;
     bool co_simd = false;   // a cow wave on the drone wave's SIMD (starved while the drone wave issues)
-    // cow waves: the first cow of this lane and, on the first cow wave's env lanes, the env scalars
+    // Phase 0 issues loads only: the values are combined after the barrier (the Euler cache flag, the obs block flag),
+    // and the cow waves' registers are not zeroed for the lanes that load nothing (those lanes never read them) -- a
+    // compare right after a load, or a zero written to a register whose load is in flight on other lanes, made the
+    // wave wait for its loads before the barrier, one round trip each, and the barrier held the drone wave's chain
+    // (CH_PHASE0_ZERO: the zeroed, combined-before-the-barrier form).
+    uint8_t stale_d = 1;   // drone lanes: this env's Euler cache flag (0: valid)
+#ifdef CH_PHASE0_ZERO
     R c0[4] = {0, 0, 0, 0};
-    double c0d[2] = {0, 0}, prev0d = 0, pd[3] = {0, 0, 0};   // MIX: f64 cow position, prev_cent, drone position
+    double c0d[2] = {0, 0}, prev0d = 0;
     int ei0[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     R er0[2] = {0, 0};
     double met0[kMetricRows];
 #pragma unroll
     for (int r = 0; r < kMetricRows; ++r) met0[r] = 0;
+#else
+    R c0[4];
+    double c0d[2], prev0d;
+    int ei0[10];
+    R er0[2];
+    double met0[kMetricRows];
+#endif
+    double pd[3] = {0, 0, 0};   // MIX: f64 drone position
+    uint8_t stale_o = 0;        // cow waves' env lanes: the obs block flag and the buffer tag, combined after the barrier
+    unsigned long long tag_o = 0;
     if (tid >= 64) {
         if (ct < Gv * M) {
             const long long ci = (long long)e0 * M + ct;
@@ -876,7 +891,12 @@ __device__ __forceinline__ void step2_body(const StepParams<R>& p, int salt = 0)
 #pragma unroll
             for (int r = 0; r < 9; ++r) ei0[r] = p.envi[r * E + e];
             // constant obs bytes unknown: flagged, or this buffer is not the one that holds them
+#ifdef CH_PHASE0_ZERO
             ei0[9] = p.stale[E + e] | (p.obs_tag[e] != (unsigned long long)(uintptr_t)p.obs ? 1 : 0);
+#else
+            stale_o = p.stale[E + e];
+            tag_o = p.obs_tag[e];
+#endif
             er0[0] = p.envr[e]; er0[1] = p.envr[E + e];
             if constexpr (MIX) prev0d = p.prev64[e];
 #pragma unroll
@@ -886,7 +906,11 @@ __device__ __forceinline__ void step2_body(const StepParams<R>& p, int salt = 0)
         // the drone wave loads only what its chain reads, so the chain starts after one round trip; the
         // cow waves stage the env scalars, the curriculum table and the pair list meanwhile
         n0 = p.envi[0 * E + e0 + dg];
-        rpy_valid = p.stale[e0 + dg] == 0;   // this env's Euler cache (written by the last v2 step)
+#ifdef CH_PHASE0_ZERO
+        stale_d = p.stale[e0 + dg] == 0 ? 0 : 1;   // (compared before the barrier)
+#else
+        stale_d = p.stale[e0 + dg];   // this env's Euler cache (written by the last v2 step)
+#endif
         if (marl) act0 = p.envi[7 * E + e0 + dg];
         pos[0] = p.drone[0 * DS + di]; pos[1] = p.drone[1 * DS + di]; pos[2] = p.drone[2 * DS + di];
         if constexpr (MIX) {
@@ -970,6 +994,9 @@ __device__ __forceinline__ void step2_body(const StepParams<R>& p, int salt = 0)
             ei[I_TALLY * G + g] = ei0[5]; ei[I_SPAWN * G + g] = ei0[6];
             ei[I_ACTIVE * G + g] = ei0[7]; ei[I_EPISODE * G + g] = ei0[8];
             ei[I_FLOCK * G + g] = flk; ei[I_RESET * G + g] = 0; ei[I_HERD * G + g] = 0;
+#ifndef CH_PHASE0_ZERO
+            ei0[9] = stale_o | (tag_o != (unsigned long long)(uintptr_t)p.obs ? 1 : 0);
+#endif
             ei[I_OBSD * G + g] = ei0[9];   // the obs block's constant bytes are unknown
             S.prev[g] = er0[0]; S.clock[g] = er0[1];
             if constexpr (MIX) S.prevd[g] = prev0d;
@@ -1063,7 +1090,7 @@ __device__ __forceinline__ void step2_body(const StepParams<R>& p, int salt = 0)
             if (marl && !((act0 >> dk) & 1)) { a[0] = a[1] = a[2] = a[3] = 0.0f; }  // marl_wrapper.py:80-84
             R Rm[9], rpy[3];
             quat_to_mat(q, Rm);
-            if (rpy_valid) { rpy[0] = rpy_in[0]; rpy[1] = rpy_in[1]; rpy[2] = rpy_in[2]; }
+            if (stale_d == 0) { rpy[0] = rpy_in[0]; rpy[1] = rpy_in[1]; rpy[2] = rpy_in[2]; }
             else quat_to_euler(q, rpy);
             if (!(p.phase_mask & 1)) {
                 double rpm[4];
