@@ -428,6 +428,16 @@ int ch_create(const ch_config* c, int64_t n_envs, int32_t device, ch_handle** ou
             // at 4096; f64 keeps 768, 230 vs 225 M at 262144 and 1 % faster at 4096)
             h->block = (c->physics == CH_PHYS_PYB && h->rsize == 8) ? CH_V2_MAX_BLOCK : CH_V2_MAX_BLOCK_PW;
         }
+        // 2 drones x 8 cattle (configs[1]/[2]), f64: 16 envs / 512 threads per workgroup from 1024 envs up, also when
+        // that leaves CUs idle (configs[1]: 64 workgroups) -- tools/multi_geom.py, profiles/r06/ab/r6y_*: at 1024 envs
+        // 78.1 vs 76.4 M env-steps/s (ch_step_n) and 61.8 vs 58.5 M (ch_step) against 4 envs / 256 threads; at 4096
+        // envs 311.9 vs 311.0 M and 238.3 vs 229.4 M against 16 envs / 256 threads
+        if (c->mode == CH_MODE_CTDE && h->NC == 2 && h->M == 8 && h->rsize == 8 && c->physics == CH_PHYS_PYB &&
+            E >= 1024 && V2Layout(16, 2, 8, h->P, c->mode, (int)h->rsize).bytes() <= budget) {
+            h->G = 16;
+            h->lds = V2Layout(16, 2, 8, h->P, c->mode, (int)h->rsize).bytes();
+            h->block = CH_V2_MAX_BLOCK_PW;
+        }
         // measured (tools/ab/marl.py, MI355X, 4096 envs): the dataflow kernel wins for every CTDE size
         // (2x8 19.4 vs 41.1 us, 8x16 39.7 vs 55.8, 12x16 59.9 vs 67.1) and for MARL with up to 16
         // cattle (3x8 25.8 vs 43.2).  Above 16 cows one shared pair table per workgroup (15.9 KB per
